@@ -1,0 +1,251 @@
+/*
+ * clrrt.h — C-ABI of libclrrt, the MI355X (gfx950) closed-loop RRT tree-expansion engine.
+ *
+ * This is the drop-in boundary for the reference's `expandTree` hot path (vdBerg93/cl-rrt).
+ * Every entry point is extern "C", takes plain pointers and sizes, and returns an int
+ * status (0 = ok, <0 = error; the message is available from clrrt_last_error()).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference root):
+ *   clrrt_params_default   <- updateParameters() rrt/src/rrt_node.cpp:28-38, parameters.launch:3-20,
+ *                             Vehicle::setPrius rrt/include/rrt/vehicle.h:39-60,
+ *                             MyRRT::MyRRT Wcost rrt/src/rrtplanner.cpp:12-19,
+ *                             updateReferenceResolution rrt/src/controller.cpp:18-21
+ *   clrrt_rng_*            <- glibc rand()/srand() as consumed by rrt/src/rrtplanner.cpp:142,193-194
+ *   clrrt_draw_samples     <- sampleAroundVehicle rrt/src/rrtplanner.cpp:187-201 + heuristic draw :142-143
+ *   clrrt_set_obstacles    <- MotionPlanner::updateObstacles rrt/src/motionplanner.cpp:81-86 (det) feeding
+ *                             checkObsDistance rrt/src/collisioncheck.cpp:6-8 (stub) or the OBB SAT of
+ *                             rrt/src/old_collisioncheck.cpp:6-148
+ *   clrrt_tree_init        <- initializeTree (empty branch) rrt/src/rrtplanner.cpp:39-48 + addInitialNode :21-37
+ *   clrrt_tree_load        <- RRT.tree assignment (std::vector<Node>) rrt/include/rrt/rrtplanner.h:75
+ *   clrrt_expand           <- the budget loop `for(; timer.Get(); ) expandTree(...)`
+ *                             rrt/src/motionplanner.cpp:39-43 around expandTree rrt/src/rrtplanner.cpp:123-174
+ *   clrrt_round_eval /     <- one batch of expandTree iterations split in its evaluate half (sampling, sort,
+ *   clrrt_round_commit        Simulation) and its append half (RRT.addNode, rrtplanner.h:111-113), so the host
+ *                             can all-gather accepted nodes across GPUs between the two halves
+ *   clrrt_rollout_batch    <- Simulation::Simulation + propagate rrt/src/simulation.cpp:36-47,55-143
+ *   clrrt_nn_batch         <- sortNodesExplore / sortNodesOptimize rrt/src/rrtplanner.cpp:227-268
+ *   clrrt_get_counters     <- sim_count / fail_* globals rrt/src/rrt_node.cpp:21-24
+ *
+ * Threading: one context per host thread; a context is not thread-safe (the reference is not
+ * reentrant either: rrt_node.cpp globals).  Device buffers are owned by the context.
+ */
+#ifndef CLRRT_H
+#define CLRRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLRRT_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define CLRRT_OK 0
+#define CLRRT_EINVAL (-1)
+#define CLRRT_EHIP (-2)
+#define CLRRT_ECAPACITY (-3)
+#define CLRRT_ESTATE (-4)
+
+/* ---- expansion modes ---- */
+/* EXACT: the reference's sequential semantics (every iteration sees every node appended before it),
+ *        realised by speculative rounds + in-order prefix commit.  Trees equal the reference's.
+ * BATCH: frozen tree per round, every sample of the round is committed (throughput mode). */
+#define CLRRT_MODE_EXACT 0
+#define CLRRT_MODE_BATCH 1
+
+/* ---- collision modes ---- */
+#define CLRRT_COLLISION_STUB 0 /* checkObsDistance returns 100 (rrt/src/collisioncheck.cpp:6-8) */
+#define CLRRT_COLLISION_OBB 1  /* OBB separating-axis test (rrt/src/old_collisioncheck.cpp:6-148) */
+
+/* ---- rollout outcomes (Simulation flags + the fail_* counter it bumped) ---- */
+#define CLRRT_ROLL_ITERLIMIT 0 /* horizon exhausted: fail_iterlimit (simulation.cpp:142) */
+#define CLRRT_ROLL_END 1       /* endReached (simulation.cpp:115-121) */
+#define CLRRT_ROLL_GOAL 2      /* goalReached (simulation.cpp:125-132) */
+#define CLRRT_ROLL_COLLISION 3 /* fail_collision (simulation.cpp:84-86) */
+#define CLRRT_ROLL_ACCLIMIT 4  /* fail_acclimit (simulation.cpp:100-104) */
+
+/* Vehicle parameters (class Vehicle, rrt/include/rrt/vehicle.h:4-60).  Only the fields the
+ * hot path reads are carried. */
+typedef struct clrrt_vehicle {
+  double dmax;  /* max steering angle */
+  double ddmax; /* max steering rate */
+  double Td;    /* steer damping */
+  double Ta;    /* acceleration damping */
+  double amin;  /* min acceleration */
+  double amax;  /* max acceleration */
+  double L;     /* wheel base */
+  double Vch;   /* characteristic velocity */
+  double Kus;   /* understeer gradient */
+} clrrt_vehicle;
+
+/* Everything the reference reads from mutable globals, the ROS parameter server and MyRRT
+ * (rrt_node.cpp:13-18, parameters.launch:3-20, rrtplanner.cpp:12-19). */
+typedef struct clrrt_params {
+  clrrt_vehicle veh;
+  double sim_dt;       /* ctrl/sampleTime */
+  double ctrl_tla;     /* ctrl/tla */
+  double ctrl_mindla;  /* ctrl/mindla */
+  double ctrl_dlavmin; /* ctrl/dlavmin */
+  double ctrl_Kp;      /* ctrl/Kp */
+  double ctrl_Ki;      /* ctrl/Ki */
+  double ref_int;      /* ctrl/refint */
+  double ref_mindist;  /* ctrl/refmindist */
+  double ref_res;      /* reference resolution of the query (updateReferenceResolution) */
+  double vmax;         /* MotionRequest.vmax */
+  double ay_road_max;  /* never set in the reference: 0 */
+  double goal[4];      /* MotionRequest.goal: x, y, heading, velocity (car frame) */
+  double Wcost[5];     /* motionplanner/weight_* */
+  double lane_shift0;  /* MotionRequest.laneShifts[0] (only read when bend) */
+  double Cxy[3];       /* MotionRequest.Cxy (only read when bend) */
+  int32_t bend;        /* MotionRequest.bend */
+  int32_t obs_use_pred;   /* obstacle constant-velocity prediction at x[6] (rrt_node.cpp:11) */
+  int32_t sort_limit;     /* MyRRT::sortLimit = 10 */
+  int32_t collision_mode; /* CLRRT_COLLISION_* */
+} clrrt_params;
+
+/* car_msgs/Obstacle2D: bbox centre (x, y, theta), size (x, y), twist linear (x, y). */
+typedef struct clrrt_obstacle {
+  double cx, cy, theta, size_x, size_y, vx, vy;
+} clrrt_obstacle;
+
+/* Tree node header (the hot-path part of struct Node, rrt/include/rrt/rrtplanner.h:35-48).
+ * The trajectory (Node::tra) lives in a row arena: rows [row_offset, row_offset+nrows) of
+ * 10 doubles each (x, y, theta, delta, v, a, t, IDwp, vref, delta_cmd).  ref_* are the
+ * reference endpoints Node::ref.x/y.front()/back() and Node::ref.v.back(). */
+typedef struct clrrt_node {
+  double state[10];
+  double ref_front[2];
+  double ref_back[2];
+  double ref_vback;
+  double ang_par; /* atan2(ref_back - ref_front): feasibleNode's angPar (rrtplanner.cpp:273) */
+  int32_t parent;
+  float costE;
+  float costS;
+  int32_t goal;
+  int32_t nrows;
+  int32_t owner; /* rank whose arena holds the rows */
+  int64_t row_offset;
+} clrrt_node; /* 160 bytes */
+
+/* glibc TYPE_3 additive-feedback generator state (random_r, srand(seed) semantics). */
+typedef struct clrrt_rng {
+  int32_t r[34];
+  int32_t pos;
+} clrrt_rng;
+
+/* One expansion sample (a drawn iteration): point + heuristic (1 = explore, Dubins; 0 = optimize). */
+typedef struct clrrt_sample {
+  double x, y;
+  int32_t explore;
+  int32_t pad;
+} clrrt_sample;
+
+typedef struct clrrt_counters {
+  int64_t sim_count;      /* simulated steps */
+  int64_t fail_collision;
+  int64_t fail_acclimit;
+  int64_t fail_iterlimit;
+  int64_t rollouts;
+} clrrt_counters;
+
+typedef struct clrrt_stats {
+  int64_t iterations;   /* expandTree iterations consumed (3 rand() draws each) */
+  int64_t nodes_added;  /* regular + goal-biased */
+  int64_t goal_nodes_added;
+  int64_t rounds;
+  int64_t speculated;   /* samples evaluated (>= iterations in EXACT mode) */
+  double elapsed_ms;
+} clrrt_stats;
+
+typedef struct clrrt_capacity {
+  int64_t max_nodes; /* tree header capacity */
+  int64_t max_rows;  /* trajectory arena capacity (rows of 10 doubles) */
+  int32_t max_batch; /* samples per round */
+  int32_t max_obstacles;
+} clrrt_capacity;
+
+/* Kernel-level rollout job: a Simulation from tree node `parent` towards `sample`
+ * (gb = 0: getReference + regular profile; gb = 1: getGoalReference + GoalBiased profile). */
+typedef struct clrrt_rollout_job {
+  int32_t parent;
+  int32_t gb;
+  double sample[2];
+} clrrt_rollout_job;
+
+typedef struct clrrt_rollout_result {
+  int32_t outcome; /* CLRRT_ROLL_* */
+  int32_t nrows;   /* rows in stateArray (steps + 1) */
+  double costE;    /* Simulation::costE (double, before the Node's float narrowing) */
+  double costS;
+  double final_state[10];
+  double ref_back[2];
+  double ref_vback;
+  int32_t ref_n;
+  int32_t pad;
+} clrrt_rollout_result;
+
+/* ---- parameters / RNG (host only, no device needed) ---- */
+int clrrt_abi_version(void);
+int clrrt_params_default(clrrt_params* p, double v0, const double goal[4], double vmax);
+void clrrt_rng_seed(clrrt_rng* rng, uint32_t seed);
+int32_t clrrt_rng_next(clrrt_rng* rng);
+int clrrt_draw_samples(const clrrt_params* p, clrrt_rng* rng, int32_t n, clrrt_sample* out);
+
+/* ---- context ---- */
+typedef struct clrrt_ctx clrrt_ctx;
+int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, clrrt_ctx** out);
+void clrrt_destroy(clrrt_ctx* ctx);
+const char* clrrt_last_error(const clrrt_ctx* ctx);
+int clrrt_set_stream(clrrt_ctx* ctx, void* hip_stream);
+int clrrt_set_params(clrrt_ctx* ctx, const clrrt_params* p);
+int clrrt_set_obstacles(clrrt_ctx* ctx, const clrrt_obstacle* obs, int32_t m);
+int clrrt_set_rank(clrrt_ctx* ctx, int32_t rank);
+
+/* ---- tree ---- */
+int clrrt_tree_init(clrrt_ctx* ctx, const double root_state[10]);
+int clrrt_tree_load(clrrt_ctx* ctx, const clrrt_node* nodes, int64_t n);
+int clrrt_tree_size(clrrt_ctx* ctx, int64_t* n_nodes, int64_t* n_rows);
+int clrrt_tree_download(clrrt_ctx* ctx, int64_t first, int64_t count, clrrt_node* out);
+int clrrt_tree_rows(clrrt_ctx* ctx, int64_t row_offset, int64_t nrows, double* out);
+
+/* ---- expansion ---- */
+/* Runs expandTree iterations drawn from `rng` until `n_iters` iterations are consumed
+ * (n_iters > 0) or, with n_iters == 0, until `budget_ms` of wall time has elapsed (checked
+ * between rounds).  EXACT mode reproduces the reference's sequential tree; BATCH mode evaluates
+ * `batch` samples per round against a frozen tree and commits all of them in sample order. */
+int clrrt_expand(clrrt_ctx* ctx, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t mode,
+                 int32_t batch, clrrt_stats* out);
+
+/* Evaluate `n` samples (host array) against the current tree; accepted nodes (regular and
+ * goal-biased, in sample order) are written compacted to `dev_out` (device pointer, capacity
+ * 2*n records) with row_offset local to this context's arena and owner = this rank.
+ * *n_out receives the count. */
+int clrrt_round_eval(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, void* dev_out,
+                     int32_t* n_out);
+/* Append `n` node records (device pointer) to the tree; `local_first`/`local_count` name the
+ * slice of them that this context produced in its last clrrt_round_eval (their rows are moved
+ * into the arena); records outside that slice are remote nodes whose rows stay on their owner. */
+int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t local_first,
+                       int32_t local_count);
+
+/* ---- kernel-level parity entries ---- */
+int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n,
+                        clrrt_rollout_result* out, double* rows_out, int32_t rows_cap);
+int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t* out_ids,
+                   float* out_keys);
+
+int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);
+int clrrt_reset_counters(clrrt_ctx* ctx);
+
+/* Launch-time profile of the last clrrt_expand / round call: device milliseconds per kernel
+ * family measured with HIP events on the context stream.  which: 0 = nn, 1 = rollout,
+ * 2 = commit; returns the summed ms and the launch count. */
+int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
+int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CLRRT_H */

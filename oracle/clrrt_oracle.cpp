@@ -1,0 +1,796 @@
+// clrrt_oracle.cpp — TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by, or called from
+// the product (cl-rrt_amd/).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg use it, as the checker / the timed CPU reference.
+//
+// A plain C++ restatement of the reference's expandTree hot path (vdBerg93/cl-rrt, paths relative
+// to the reference root), kept arithmetic-for-arithmetic faithful so that it reproduces the
+// reference's outputs bit-for-bit on the same glibc:
+//   * float/double typing exactly as the reference declares it (Dubins key and OBB SAT in float,
+//     dynamics in double, Node costs narrowed to float);
+//   * std::sort over (node id, key) pairs, nodes passed BY VALUE to the Dubins key (the
+//     reference's cost profile, rrtplanner.cpp:371);
+//   * glibc rand() consumed in the reference order;
+//   * canonical semantics for the reference's out-of-bounds reads: every read of
+//     ref.x / ref.y / ref.v past the end yields 0.0 — what the reference computes when its heap is
+//     zero-filled, which is how the survey pinned it (SURVEY §8(c) "Determinism recipe").
+//   * OBB axis 3 (setNorms leaves normsY[3] unset, old_collisioncheck.cpp:74-75): taken as the
+//     proper edge normal of edge 3->0.  Decision-neutral (any separating axis proves separation).
+//
+// Pinned against the survey's golden outputs of the reference (tests/golden/survey_pins.json).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <chrono>
+#include <utility>
+#include <vector>
+
+#include "../include/clrrt.h"
+
+namespace orc {
+
+using std::vector;
+typedef vector<double> Row;
+
+struct Pt { double x = 0, y = 0; };
+
+// MyReference (rrtplanner.h:27-33)
+struct Ref {
+  vector<double> x, y, v;
+  int dir = 1;
+};
+
+// Out-of-range reads yield 0.0 (canonical zero-fill semantics).
+static inline double at0(const vector<double>& a, long i) {
+  return (i >= 0 && (size_t)i < a.size()) ? a[(size_t)i] : 0.0;
+}
+
+// Node (rrtplanner.h:35-48)
+struct Node {
+  vector<double> state;
+  int parentID = -1;
+  Ref ref;
+  float costE = 0, costS = 0;
+  bool goalReached = false;
+  vector<Row> tra;
+};
+
+struct Obs { double cx, cy, th, sx, sy, vx, vy; };
+
+struct Oracle {
+  clrrt_params p;
+  double ctrl_dla = 0;
+  int64_t sim_count = 0, fail_collision = 0, fail_acclimit = 0, fail_iterlimit = 0, rollouts = 0;
+  vector<Obs> det;
+  vector<Node> tree;
+};
+
+// ---------------------------------------------------------------- helpers (functions.h)
+// LinearSpacedVector functions.h:11-20 — accumulating linspace (val += h)
+static vector<double> linspace(double a, double b, size_t N) {
+  double h = (b - a) / static_cast<double>(N - 1);
+  vector<double> out(N);
+  double val = a;
+  for (size_t k = 0; k < N; ++k, val += h) out[k] = val;
+  return out;
+}
+template <typename T> static int sgn(T v) { return (T(0) < v) - (v < T(0)); }
+// wrapToPi functions.h:43-48
+static double wrap_pi(double x) {
+  x = std::fmod(x + M_PI, 2 * M_PI);
+  if (x < 0) x += 2 * M_PI;
+  return x - M_PI;
+}
+// angleDiff functions.h:50-57
+static double angle_diff(double a, double b) {
+  double d = std::fmod(b - a + M_PI, 2 * M_PI);
+  if (d < 0) d += 2 * M_PI;
+  return d - M_PI;
+}
+// checkSaturation functions.h:61-63 / enforceConstraints simulation.cpp:7-9
+static double sat(double lo, double hi, double v) { return std::max(std::min(v, hi), lo); }
+
+// ---------------------------------------------------------------- controller (controller.cpp)
+static void update_lookahead(Oracle& o, double v) {  // controller.cpp:13-16
+  double dla_c = o.p.ctrl_mindla - o.p.ctrl_tla * o.p.ctrl_dlavmin;
+  o.ctrl_dla = std::max(o.p.ctrl_mindla, dla_c + o.p.ctrl_tla * std::abs(v));
+}
+
+static int closest_point(const Ref& r, const Pt& q, int from) {  // controller.cpp:96-113
+  double best = INFINITY, d;
+  int arg = 0;
+  for (int i = from; i < (int)r.x.size(); i++) {
+    d = (r.x[i] - q.x) * (r.x[i] - q.x) + (r.y[i] - q.y) * (r.y[i] - q.y);
+    if (d < best) { best = d; arg = i; }
+  }
+  return arg;
+}
+
+// transformToVehicle controller.cpp:115-132 then interpolate :134-148
+static double lateral_error(const Ref& r, const Row& x, int wp, const Pt& P) {  // :70-93
+  int lo, hi;
+  if (wp == 0) { lo = wp; hi = wp + 2; }
+  else if (wp == (int)r.x.size()) { lo = wp - 2; hi = wp; }
+  else { lo = wp - 1; hi = wp + 1; }
+  double xv[3] = {at0(r.x, lo), at0(r.x, lo + 1), at0(r.x, hi)};
+  double yv[3] = {at0(r.y, lo), at0(r.y, lo + 1), at0(r.y, hi)};
+  double X0 = P.x, X1 = P.y, X2 = x[2];
+  double tx[3], ty[3];
+  for (int i = 0; i < 3; i++) {
+    tx[i] = xv[i] * cos(X2) - X0 * cos(X2) - yv[i] * sin(X2) + X1 * sin(X2);
+    ty[i] = yv[i] * cos(X2) - X1 * cos(X2) + xv[i] * sin(X2) - X0 * sin(X2);
+  }
+  double y = 0, L;
+  for (int i = 0; i < 3; i++) {
+    L = 1;
+    for (int j = 0; j < 3; j++)
+      if (i != j) L = L * (tx[j]) / (tx[i] - tx[j]);
+    y = y + ty[i] * L;
+  }
+  return y;
+}
+
+struct Ctrl {  // class Controller controller.h:8-28
+  int IDwp = 0;
+  Pt P;
+  double ym = 0, iE = 0;
+  bool endreached = false;
+
+  void update_waypoint(Oracle& o, const Ref& r, const Row& x) {  // controller.cpp:53-68
+    update_lookahead(o, x[4]);
+    P.x = x[0] + o.ctrl_dla * r.dir * std::cos(x[2]);
+    P.y = x[1] + o.ctrl_dla * r.dir * std::sin(x[2]);
+    IDwp = closest_point(r, P, IDwp);
+    if ((size_t)IDwp >= r.x.size() - 1 - 2) endreached = true;
+    if (at0(r.x, IDwp) == r.x.back() && at0(r.y, IDwp) == r.y.back()) endreached = true;
+  }
+  Ctrl(Oracle& o, const Ref& r, const Row& x) {  // controller.cpp:23-28
+    update_lookahead(o, x[4]);
+    IDwp = 0; endreached = false; iE = 0;
+    update_waypoint(o, r, x);
+  }
+  double steer(Oracle& o, const Ref& r, const Row& x) {  // :47-51
+    const clrrt_vehicle& veh = o.p.veh;
+    ym = lateral_error(r, x, IDwp, P);
+    double cmd = 2 * ((veh.L + veh.Kus * x[4] * x[4]) / pow(o.ctrl_dla, 2)) * ym;
+    return sat(-veh.dmax, veh.dmax, cmd);
+  }
+  double accel(Oracle& o, const Ref& r, const Row& x) {  // :37-45 (LAlong = 2, :35)
+    double E = at0(r.v, IDwp + 2) - x[4];
+    iE = iE + E * o.p.sim_dt;
+    return sat(o.p.veh.amin, o.p.veh.amax, o.p.ctrl_Kp * E + o.p.ctrl_Ki * iE);
+  }
+};
+
+// ---------------------------------------------------------------- references (reference.cpp)
+static Ref get_reference(Oracle& o, Pt s, Node node, int dir) {  // reference.cpp:9-22 (node by value)
+  Ref r;
+  double L = sqrt(pow(s.x - node.ref.x.back(), 2) + pow(s.y - node.ref.y.back(), 2));
+  int N = round(L / o.p.ref_res) + 1;
+  r.x = linspace(node.ref.x.back(), s.x, N);
+  r.y = linspace(node.ref.y.back(), s.y, N);
+  r.dir = dir;
+  return r;
+}
+
+static Ref get_goal_reference(Oracle& o, Node node, vector<double> g) {  // reference.cpp:25-70
+  double dla_c = o.p.ctrl_mindla - o.p.ctrl_tla * o.p.ctrl_dlavmin;
+  double dla_end = std::max(o.p.ctrl_mindla, dla_c + o.p.ctrl_tla * std::abs(g[3]));
+  double Dext = dla_end, Dal = 1;
+  Ref r;
+  Pt P1, P2, Pc, Pf;
+  P1.x = g[0] + Dal * cos(g[2]); P1.y = g[1] + Dal * sin(g[2]);
+  P2.x = g[0] - Dal * cos(g[2]); P2.y = g[1] - Dal * sin(g[2]);
+  double bx = node.ref.x.back(), by = node.ref.y.back();
+  if (sqrt(pow(P1.x - bx, 2) + pow(P1.y - by, 2)) < sqrt(pow(P2.x - bx, 2) + pow(P2.y - by, 2))) {
+    Pc = P1; Pf = P1;
+  } else {
+    Pc = P2; Pf = P2;
+  }
+  Pf.x += (Dext + Dal) * cos(g[2]);
+  Pf.y += (Dext + Dal) * sin(g[2]);
+  double N1 = round(sqrt(pow(Pc.x - bx, 2) + pow(Pc.y - by, 2)) / o.p.ref_res) + 1;
+  double N2 = round(sqrt(pow(Pf.x - Pc.x, 2) + pow(Pf.y - Pc.y, 2)) / o.p.ref_res) + 1;
+  vector<double> ax = linspace(bx, Pc.x, N1), bxv = linspace(Pc.x, Pf.x, N2);
+  vector<double> ay = linspace(by, Pc.y, N1), byv = linspace(Pc.y, Pf.y, N2);
+  r.x = ax; r.x.insert(r.x.end(), bxv.begin(), bxv.end());
+  r.y = ay; r.y.insert(r.y.end(), byv.begin(), byv.end());
+  return r;
+}
+
+// generateVelocityProfile reference.cpp:73-170 (a_acc = 1, a_dec = -1, tmin = 1 at :77)
+static void velocity_profile(Oracle& o, Ref& r, double v0, double vmax, const vector<double>& g,
+                             bool GB) {
+  double vend = g[3];
+  double aa = 1, ad = -1, tmin = 1;
+  double Lp, res;
+  if (GB) {
+    double Dg = sqrt(pow(g[0] - r.x.front(), 2) + pow(g[1] - r.y.front(), 2));
+    Lp = Dg + o.p.ctrl_mindla;
+    res = Lp / (r.x.size() - 1);
+  } else {
+    double Dg = sqrt(pow(g[0] - r.x.back(), 2) + pow(g[1] - r.y.back(), 2));
+    double Lref = sqrt(pow(r.x.front() - r.x.back(), 2) + pow(r.y.front() - r.y.back(), 2));
+    res = Lref / (r.x.size() - 1);
+    Lp = Lref + Dg + o.p.ctrl_mindla;
+  }
+  double Dacc = (pow(vmax, 2) - pow(v0, 2)) / (2 * aa);
+  double Dcst = vmax * tmin;
+  double Dbrk = (pow(vend, 2) - pow(vmax, 2)) / (2 * ad);
+  bool fits = (Dacc + Dcst + Dbrk) < Lp;
+  double Vc;
+  if (vend > (v0 + 0.1)) {
+    Vc = vend;
+  } else if (fits) {
+    Vc = vmax;
+  } else {
+    double D = Lp;
+    Vc = (sqrt(pow(aa, 2) * pow(ad, 2) * pow(tmin, 2) - 2 * D * pow(aa, 2) * ad +
+               pow(aa, 2) * pow(vend, 2) + 2 * D * aa * pow(ad, 2) - aa * ad * pow(v0, 2) -
+               aa * ad * pow(vend, 2) + pow(ad, 2) * pow(v0, 2)) +
+          aa * ad * tmin) /
+         (aa - ad);
+  }
+  Dacc = (pow(Vc, 2) - pow(v0, 2)) / (2 * aa);
+  if (Dacc < 0) { Dacc = 0; Vc = v0; }
+  Dbrk = std::max(double(0), (pow(vend, 2) - pow(Vc, 2)) / (2 * ad));
+  Dcst = std::max(double(0), Lp - Dacc - Dbrk);
+  double tbrk = (vend - Vc) / ad;
+  r.v.clear();
+  for (size_t i = 0; i != r.x.size(); i++) {
+    double D = i * res;
+    if (D < Dacc) {
+      double t1 = -(v0 - sqrt(pow(v0, 2) + 2 * aa * D)) / aa;
+      double t2 = -(v0 + sqrt(pow(v0, 2) + 2 * aa * D)) / aa;
+      double t = (t1 >= 0) * t1 + (t2 >= 0) * t2;
+      r.v.push_back(v0 + aa * t);
+    } else if (D <= (Dacc + Dcst)) {
+      r.v.push_back(Vc);
+    } else {
+      double q = pow(Vc, 2) + 2 * D * ad - 2 * Dacc * ad - 2 * Dcst * ad;
+      double t1 = -(Vc + sqrt(q)) / ad;
+      double t2 = -(Vc - sqrt(q)) / ad;
+      double dt = (t1 != tbrk) * (t1 >= 0) * (t1 <= tbrk) * t1 + (t2 >= 0) * (t2 <= tbrk) * t2;
+      r.v.push_back(std::max(double(0), Vc + ad * dt));
+    }
+  }
+}
+
+// ---------------------------------------------------------------- collision (old_collisioncheck.cpp)
+struct Box {  // class OBB collision.h:16-34 (float fields)
+  double px, py;
+  float w, h, o;
+  float vx[4], vy[4], nx[4], ny[4], mm[2];
+  Box(double _px, double _py, float _w, float _h, float _o) : px(_px), py(_py), w(_w), h(_h), o(_o) {
+    // setVertices old_collisioncheck.cpp:56-65
+    vx[0] = px + std::cos(o) * (h / 2) - std::sin(o) * (w / 2);
+    vy[0] = py + std::sin(o) * (h / 2) + std::cos(o) * (w / 2);
+    vx[1] = px + std::cos(o) * (h / 2) - std::sin(o) * (-w / 2);
+    vy[1] = py + std::sin(o) * (h / 2) + std::cos(o) * (-w / 2);
+    vx[2] = px + std::cos(o) * (-h / 2) - std::sin(o) * (-w / 2);
+    vy[2] = py + std::sin(o) * (-h / 2) + std::cos(o) * (-w / 2);
+    vx[3] = px + std::cos(o) * (-h / 2) - std::sin(o) * (w / 2);
+    vy[3] = py + std::sin(o) * (-h / 2) + std::cos(o) * (w / 2);
+    // setNorms :67-76, axis 3 canonicalised to the proper edge normal
+    for (int i = 0; i < 3; i++) {
+      nx[i] = vy[i + 1] - vy[i];
+      ny[i] = -(vx[i + 1] - vx[i]);
+    }
+    nx[3] = vy[0] - vy[3];
+    ny[3] = -(vx[0] - vx[3]);
+  }
+  void maxmin(float ax, float ay) {  // findMaxMin :78-95
+    mm[0] = vx[0] * ax + vy[0] * ay;
+    mm[1] = mm[0];
+    for (int i = 1; i <= 3; i++) {
+      float pr = vx[i] * ax + vy[i] * ay;
+      if (pr > mm[0]) mm[0] = pr;
+      else if (pr < mm[1]) mm[1] = pr;
+    }
+  }
+};
+
+static double box_gap(Box a, Box b) {  // getOBBdist :98-148 (first separating gap, 0 = overlap)
+  for (int pass = 0; pass < 2; pass++) {
+    const Box& src = pass == 0 ? a : b;
+    float ax[4], ay[4];
+    for (int i = 0; i < 4; i++) { ax[i] = src.nx[i]; ay[i] = src.ny[i]; }
+    for (int i = 0; i <= 3; i++) {
+      a.maxmin(ax[i], ay[i]);
+      float ap[2] = {a.mm[0], a.mm[1]};
+      b.maxmin(ax[i], ay[i]);
+      float bp[2] = {b.mm[0], b.mm[1]};
+      float D1 = bp[1] - ap[0];
+      float D2 = ap[1] - bp[0];
+      if (D1 > 0) return D1;
+      else if (D2 > 0) return D2;
+    }
+  }
+  return 0;
+}
+
+// checkObsDistance: stub collisioncheck.cpp:6-8, or the obstacle form old_collisioncheck.cpp:24-51
+static double obs_distance(Oracle& o, const Row& x) {
+  if (o.p.collision_mode == CLRRT_COLLISION_STUB) return 100;
+  double t = o.p.obs_use_pred ? x[6] : 0;
+  vector<Box> boxes;  // getOBBvector :6-22 (rebuilt every call, as the reference does)
+  for (size_t i = 0; i != o.det.size(); i++) {
+    const Obs& d = o.det[i];
+    boxes.push_back(Box(d.cx + d.vx * t, d.cy + d.vy * t, d.sx / 2, d.sy / 2, d.th));
+  }
+  Box veh(x[0] + 1.424 * cos(x[2]), x[1] + 1.424 * sin(x[2]), 2, 4.848, x[2]);
+  double best = 10000;
+  for (size_t j = 0; j != boxes.size(); j++) {
+    double D = box_gap(veh, boxes[j]);
+    if (D == 0) return 0;
+    else if (D < best) best = D;
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------- simulation (simulation.cpp)
+struct Sim {
+  vector<Row> rows;
+  double costE = 0, costS = 0;
+  bool goalReached = false, endReached = false;
+  int outcome = CLRRT_ROLL_ITERLIMIT;
+};
+
+static double dist_to_lane(double x, double y, double S, const double* C) {  // :49-53
+  double Lx = (x - S * C[1] + y * C[1] - C[1] * C[2]) / (pow(C[1], 2) + 1);
+  double Ly = S + C[2] + (C[1] * (x - S * C[1] + y * C[1] - C[1] * C[2])) / (pow(C[1], 2) + 1);
+  return sqrt(pow(Lx - x, 2) + pow(Ly - y, 2));
+}
+
+static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
+  const clrrt_vehicle& veh = o.p.veh;
+  const double dt = o.p.sim_dt;
+  for (int i = 0; i < (20 / dt); i++) {
+    o.sim_count++;
+    Row x = s.rows[i];
+    // getControls controller.cpp:30-34 (braced init: steer before accel)
+    c.update_waypoint(o, r, x);
+    double dc = c.steer(o, r, x);
+    double ac = c.accel(o, r, x);
+    // VehicleODE :11-25
+    double dx[7];
+    double Gss = 1 / (1 + pow((x[4] / veh.Vch), 2));
+    dx[0] = x[4] * cos(x[2]);
+    dx[1] = x[4] * sin(x[2]);
+    dx[2] = (x[4] / veh.L) * tan(x[3]) * Gss;
+    dx[3] = (1 / veh.Td) * (dc - x[3]);
+    dx[4] = x[5];
+    dx[5] = (1 / veh.Ta) * (ac - x[5]);
+    dx[6] = 1;
+    dx[4] = sat(veh.amin, veh.amax, dx[4]);
+    dx[3] = sat(-veh.ddmax, veh.ddmax, dx[3]);
+    // IntegrateEuler :27-34 (indices 7.. read zero dx and are overwritten below)
+    for (int k = 0; k < 7; k++) x[k] = x[k] + dx[k] * dt;
+    x[3] = sat(-veh.dmax, veh.dmax, x[3]);
+    x[7] = c.IDwp;
+    x[8] = at0(r.v, c.IDwp + 2);
+    x[9] = dc;
+    s.rows.push_back(x);
+    double Dobs = obs_distance(o, x);
+    if (Dobs == 0) { s.endReached = false; o.fail_collision++; s.outcome = CLRRT_ROLL_COLLISION; return; }
+    s.costE += x[4] * dt;
+    double kappa = tan(x[3]) / veh.L;
+    s.costS += o.p.Wcost[0] * x[4] * dt + o.p.Wcost[1] * std::abs(kappa) +
+               o.p.Wcost[2] * exp(-o.p.Wcost[3] * Dobs);
+    if (o.p.bend) s.costS += o.p.Wcost[4] * dist_to_lane(x[0], x[1], o.p.lane_shift0, o.p.Cxy);
+    double ay = std::abs(x[4] * dx[2]);
+    if (ay + o.p.ay_road_max > 3) { s.endReached = false; o.fail_acclimit++; s.outcome = CLRRT_ROLL_ACCLIMIT; return; }
+    double dg = sqrt(pow(x[0] - o.p.goal[0], 2) + pow(x[1] - o.p.goal[1], 2));
+    double he = std::abs(angle_diff(x[2], o.p.goal[2]));
+    double Ve = (x[4] - r.v.back());
+    if (c.endreached && std::abs(Ve < 0.1)) { s.endReached = true; s.outcome = CLRRT_ROLL_END; return; }
+    if ((dg <= 1) && (he < 0.05)) { s.goalReached = true; s.outcome = CLRRT_ROLL_GOAL; return; }
+  }
+  o.fail_iterlimit++;
+}
+
+// Simulation::Simulation :36-47 — mutates ref (fills ref.v)
+static Sim simulate(Oracle& o, const vector<double>& state, Ref& r, bool GB, double Vstart) {
+  Sim s;
+  o.rollouts++;
+  s.rows.push_back(state);
+  Ctrl c(o, r, state);
+  s.rows.back()[7] = c.IDwp;
+  vector<double> g(o.p.goal, o.p.goal + 4);
+  velocity_profile(o, r, Vstart, o.p.vmax, g, GB);
+  propagate(o, s, c, r);
+  return s;
+}
+
+// ---------------------------------------------------------------- tree (rrtplanner.cpp)
+static Pt sample_around(Oracle& o) {  // :187-201
+  const double* g = o.p.goal;
+  double dGoal = sqrt(pow(g[0], 2) + pow(g[1], 2));
+  double hd = atan2(g[1], g[0]);
+  double latMin = -7, latMax = 7;
+  Pt s;
+  double rLong = static_cast<float>(rand()) / (static_cast<float>(RAND_MAX / (dGoal + 10)));
+  double rLat = latMin + static_cast<float>(rand()) / (static_cast<float>(RAND_MAX / (latMax - latMin)));
+  s.x = rLong * cos(hd) + rLat * cos(hd + M_PI / 2);
+  s.y = rLong * sin(hd) + rLat * sin(hd + M_PI / 2);
+  return s;
+}
+
+static float dubins(Pt S, Node N, int dir) {  // dubinsDistance :371-406 (Node by value, as the reference)
+  float rho = 4.77;
+  float qx = S.x - N.state[0];
+  float qy = S.y - N.state[1];
+  float ang = -N.state[2] - M_PI * (dir != 1);
+  float tmp = std::cos(ang) * qx - std::sin(ang) * qy;
+  qy = std::abs(std::sin(ang) * qx + std::cos(ang) * qy);
+  qx = tmp;
+  float dc = std::sqrt(qx * qx + (qy - rho) * (qy - rho));
+  float thc = std::atan2(qx, rho - qy);
+  while (thc < 0) thc = thc + 2 * M_PI;
+  float df = std::sqrt(qx * qx + (qy + rho) * (qy + rho));
+  float alpha = 2 * M_PI - std::acos((5 * rho * rho - df * df) / (4 * rho * rho));
+  bool inside = (qx * qx + (qy + rho) * (qy + rho) <= rho * rho) |
+                (qx * qx + (qy - rho) * (qy - rho) <= rho * rho);
+  if (!inside) return std::sqrt(dc * dc - rho * rho) + rho * (thc - std::acos(rho / dc));
+  return rho * (alpha + std::asin(qx / df) - std::asin(rho * std::sin(alpha) / df));
+}
+
+static bool feasible_node(Oracle& o, const Node& n, const Pt& s) {  // :271-289
+  double angPar = atan2(n.ref.y.back() - n.ref.y.front(), n.ref.x.back() - n.ref.x.front());
+  double angNew = atan2(s.y - n.ref.y.back(), s.x - n.ref.x.back());
+  double Lref = sqrt(pow(n.ref.x.back() - s.x, 2) + pow(n.ref.y.back() - s.y, 2));
+  if (std::abs(angle_diff(angNew, angPar)) > (M_PI / 4)) return false;
+  if (Lref < (2.1 * o.p.ref_res)) return false;
+  return true;
+}
+
+// sortNodesExplore :227-247 / sortNodesOptimize :250-268 over the first `upto` nodes
+static vector<int> sort_nodes(Oracle& o, const Pt& s, bool explore, size_t upto,
+                              vector<float>* keys_out = nullptr) {
+  vector<std::pair<int, float>> dv;
+  for (size_t i = 0; i != upto; i++) {
+    float k = explore ? dubins(s, o.tree[i], 1) : o.tree[i].costE + dubins(s, o.tree[i], 1);
+    dv.push_back(std::make_pair((int)i, k));
+  }
+  std::sort(dv.begin(), dv.end(),
+            [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; });
+  vector<int> out;
+  for (auto it = dv.begin(); it != dv.end(); ++it) {
+    if (feasible_node(o, o.tree[it->first], s)) {
+      out.push_back(it->first);
+      if (keys_out) keys_out->push_back(it->second);
+    }
+    if ((int)out.size() == o.p.sort_limit) break;
+  }
+  return out;
+}
+
+static bool feasible_goal_bias(Oracle& o, const Node& node) {  // :292-315 (cos for .y kept)
+  const double* g = o.p.goal;
+  double R1 = 4.77, R2 = R1 - 0.3;
+  Pt cl, cr;
+  cl.x = g[0] + R1 * cos(g[2] - M_PI_2);
+  cl.y = g[1] + R1 * cos(g[2] - M_PI_2);
+  cr.x = g[0] + R1 * cos(g[2] + M_PI_2);
+  cr.y = g[1] + R1 * cos(g[2] + M_PI_2);
+  bool outL = sqrt(pow(node.state[0] - cl.x, 2) + pow(node.state[1] - cl.y, 2)) > R2;
+  bool outR = sqrt(pow(node.state[0] - cr.x, 2) + pow(node.state[1] - cr.y, 2)) > R2;
+  double aRef = atan2(g[1] - node.ref.y.back(), g[0] - node.ref.x.back());
+  double h1 = std::abs(wrap_pi(g[2] - aRef));
+  double h2 = std::abs(wrap_pi(g[2] + M_PI - aRef));
+  double mn = std::min(h1, h2);
+  double sg = sgn(cos(g[2] + M_PI_2 - aRef));
+  double ang = sg * mn;
+  bool within = std::abs(ang) < (M_PI_4 / 2);
+  return outL * outR * within;
+}
+
+// Result of one expandTree iteration evaluated against the first `upto` tree nodes.
+struct IterResult {
+  bool added = false, gb_added = false;
+  Node node, gb_node;
+};
+
+static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_t upto) {
+  IterResult res;
+  vector<int> cand = sort_nodes(o, s, explore, upto);
+  for (int id : cand) {
+    Ref r = get_reference(o, s, o.tree[id], 1);
+    Sim sim = simulate(o, o.tree[id].state, r, false, o.tree[id].ref.v.back());
+    if (sim.endReached || sim.goalReached) {
+      Node n;
+      n.state = sim.rows.back(); n.parentID = id; n.ref = r; n.tra = sim.rows;
+      n.costE = sim.costE + o.tree[id].costE;
+      n.costS = sim.costS + o.tree[id].costS;
+      n.goalReached = sim.goalReached;
+      res.node = n; res.added = true;
+      break;
+    }
+  }
+  if (res.added && feasible_goal_bias(o, res.node)) {  // :163-173 on tree.back() == the new node
+    vector<double> g(o.p.goal, o.p.goal + 4);
+    Ref rg = get_goal_reference(o, res.node, g);
+    Sim sg = simulate(o, res.node.state, rg, true, res.node.ref.v.back());
+    if (sg.endReached || sg.goalReached) {
+      Node n;
+      n.state = sg.rows.back(); n.parentID = -2 /* set at append */; n.ref = rg; n.tra = sg.rows;
+      n.costE = sg.costE + res.node.costE;
+      n.costS = sg.costS + res.node.costS;
+      n.goalReached = sg.goalReached;
+      res.gb_node = n; res.gb_added = true;
+    }
+  }
+  return res;
+}
+
+static void append_result(Oracle& o, IterResult& r) {
+  if (!r.added) return;
+  o.tree.push_back(r.node);
+  if (r.gb_added) {
+    r.gb_node.parentID = (int)o.tree.size() - 1;
+    o.tree.push_back(r.gb_node);
+  }
+}
+
+// expandTree :123-174 (one iteration, 3 rand() draws)
+static void expand_tree(Oracle& o) {
+  Pt s = sample_around(o);
+  double r = static_cast<double>(rand()) / (static_cast<double>(RAND_MAX / (1)));
+  bool explore = r <= ((false * 0.3) + (!false * 0.7));  // RRT.goalReached is never set
+  IterResult res = evaluate_iteration(o, s, explore, o.tree.size());
+  append_result(o, res);
+}
+
+// addInitialNode :21-37
+static void add_initial_node(Oracle& o, const vector<double>& state) {
+  Ref r;
+  double xend = 1, yend = 0, res = 0.1;
+  int N = floor(sqrt(pow(xend, 2) + pow(yend, 2)) / res);
+  r.x = linspace(0, xend, N);
+  r.y = linspace(0, yend, N);
+  for (int i = 0; i != N; i++) r.v.push_back(state[4]);
+  r.dir = 1;
+  Node n;
+  n.state = state; n.parentID = -1; n.ref = r; n.tra.push_back(state);
+  n.costE = 0; n.costS = 0; n.goalReached = false;
+  o.tree.push_back(n);
+}
+
+}  // namespace orc
+
+// ============================================================================ C API (ctypes)
+using namespace orc;
+
+extern "C" {
+
+void* orc_create(const clrrt_params* p) {
+  Oracle* o = new Oracle();
+  o->p = *p;
+  return o;
+}
+void orc_destroy(void* h) { delete (Oracle*)h; }
+void orc_srand(unsigned seed) { srand(seed); }
+int orc_rand(void) { return rand(); }
+
+void orc_set_params(void* h, const clrrt_params* p) { ((Oracle*)h)->p = *p; }
+
+void orc_set_obstacles(void* h, const double* obs7, int m) {
+  Oracle* o = (Oracle*)h;
+  o->det.clear();
+  for (int i = 0; i < m; i++) {
+    const double* d = obs7 + 7 * i;
+    o->det.push_back(Obs{d[0], d[1], d[2], d[3], d[4], d[5], d[6]});
+  }
+}
+
+void orc_init_tree(void* h, const double* root10) {
+  Oracle* o = (Oracle*)h;
+  o->tree.clear();
+  add_initial_node(*o, std::vector<double>(root10, root10 + 10));
+}
+
+void orc_expand(void* h, long n_iters) {
+  Oracle* o = (Oracle*)h;
+  for (long i = 0; i < n_iters; i++) expand_tree(*o);
+}
+
+// Budgeted loop (motionplanner.cpp:39-43).  clock_kind 0 = CPU time (the reference's Timer),
+// 1 = wall time (steady_clock).  Returns the number of iterations performed.
+long orc_expand_budget(void* h, double budget_ms, int clock_kind) {
+  Oracle* o = (Oracle*)h;
+  long it = 0;
+  if (clock_kind == 0) {
+    clock_t t0 = clock();
+    for (;; it++) {
+      double ms = (double)(clock() - t0) / (CLOCKS_PER_SEC / 1000);
+      if (!(ms < budget_ms)) break;
+      expand_tree(*o);
+    }
+  } else {
+    auto t0 = std::chrono::steady_clock::now();
+    for (;; it++) {
+      double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (!(ms < budget_ms)) break;
+      expand_tree(*o);
+    }
+  }
+  return it;
+}
+
+// BATCH mode restatement: rounds of B iterations; every sample of a round sees only the tree
+// as it was at the start of the round; results are appended in sample order.
+void orc_expand_batch(void* h, long n_iters, int B) {
+  Oracle* o = (Oracle*)h;
+  long done = 0;
+  while (done < n_iters) {
+    int nb = (int)std::min<long>(B, n_iters - done);
+    std::vector<Pt> ss(nb);
+    std::vector<char> ex(nb);
+    for (int j = 0; j < nb; j++) {
+      ss[j] = sample_around(*o);
+      double r = static_cast<double>(rand()) / (static_cast<double>(RAND_MAX / (1)));
+      ex[j] = r <= 0.7;
+    }
+    size_t upto = o->tree.size();
+    std::vector<IterResult> rs(nb);
+    for (int j = 0; j < nb; j++) rs[j] = evaluate_iteration(*o, ss[j], ex[j], upto);
+    for (int j = 0; j < nb; j++) append_result(*o, rs[j]);
+    done += nb;
+  }
+}
+
+long orc_tree_size(void* h) { return (long)((Oracle*)h)->tree.size(); }
+
+// Export node headers in the clrrt_node layout.
+void orc_get_nodes(void* h, long first, long count, clrrt_node* out) {
+  Oracle* o = (Oracle*)h;
+  for (long k = 0; k < count; k++) {
+    const Node& n = o->tree[first + k];
+    clrrt_node& d = out[k];
+    memset(&d, 0, sizeof(d));
+    for (int i = 0; i < 10; i++) d.state[i] = at0(n.state, i);
+    d.ref_front[0] = n.ref.x.front(); d.ref_front[1] = n.ref.y.front();
+    d.ref_back[0] = n.ref.x.back(); d.ref_back[1] = n.ref.y.back();
+    d.ref_vback = n.ref.v.back();
+    d.ang_par = atan2(n.ref.y.back() - n.ref.y.front(), n.ref.x.back() - n.ref.x.front());
+    d.parent = n.parentID;
+    d.costE = n.costE; d.costS = n.costS;
+    d.goal = n.goalReached;
+    d.nrows = (int)n.tra.size();
+    d.owner = 0; d.row_offset = 0;
+  }
+}
+
+long orc_node_ref_len(void* h, long i) { return (long)((Oracle*)h)->tree[i].ref.x.size(); }
+
+void orc_get_ref(void* h, long i, double* x, double* y, double* v) {
+  const Node& n = ((Oracle*)h)->tree[i];
+  for (size_t k = 0; k < n.ref.x.size(); k++) {
+    x[k] = n.ref.x[k]; y[k] = n.ref.y[k]; v[k] = at0(n.ref.v, (long)k);
+  }
+}
+
+void orc_get_rows(void* h, long i, double* out) {
+  const Node& n = ((Oracle*)h)->tree[i];
+  for (size_t r = 0; r < n.tra.size(); r++)
+    for (int c = 0; c < 10; c++) out[r * 10 + c] = at0(n.tra[r], c);
+}
+
+void orc_counters(void* h, long* out5) {
+  Oracle* o = (Oracle*)h;
+  out5[0] = o->sim_count; out5[1] = o->fail_collision; out5[2] = o->fail_acclimit;
+  out5[3] = o->fail_iterlimit; out5[4] = o->rollouts;
+}
+void orc_reset_counters(void* h) {
+  Oracle* o = (Oracle*)h;
+  o->sim_count = o->fail_collision = o->fail_acclimit = o->fail_iterlimit = o->rollouts = 0;
+}
+
+// Load a tree from node headers (refs rebuilt as 2-point references carrying front/back/vback —
+// all the expansion reads from a node's ref).  Trajectories are 1 row (the node state).
+void orc_load_tree(void* h, const clrrt_node* nodes, long n) {
+  Oracle* o = (Oracle*)h;
+  o->tree.clear();
+  for (long k = 0; k < n; k++) {
+    const clrrt_node& d = nodes[k];
+    Node nd;
+    nd.state.assign(d.state, d.state + 10);
+    nd.parentID = d.parent;
+    nd.ref.x = {d.ref_front[0], d.ref_back[0]};
+    nd.ref.y = {d.ref_front[1], d.ref_back[1]};
+    nd.ref.v = {d.ref_vback, d.ref_vback};
+    nd.costE = d.costE; nd.costS = d.costS; nd.goalReached = d.goal;
+    nd.tra.push_back(nd.state);
+    o->tree.push_back(nd);
+  }
+}
+
+// One Simulation from tree node `parent` (gb=0: toward sample; gb=1: goal-biased).
+// rows_out may be null; returns the number of rows.
+int orc_simulate(void* h, int parent, int gb, double sx, double sy, int* outcome, double* costs2,
+                 double* final10, double* ref_back3, int* ref_n, double* rows_out, int rows_cap) {
+  Oracle* o = (Oracle*)h;
+  Node par = o->tree[parent];
+  Ref r;
+  if (gb) {
+    std::vector<double> g(o->p.goal, o->p.goal + 4);
+    r = get_goal_reference(*o, par, g);
+  } else {
+    Pt s; s.x = sx; s.y = sy;
+    r = get_reference(*o, s, par, 1);
+  }
+  Sim sim = simulate(*o, par.state, r, gb != 0, par.ref.v.back());
+  *outcome = sim.outcome;
+  costs2[0] = sim.costE; costs2[1] = sim.costS;
+  for (int i = 0; i < 10; i++) final10[i] = at0(sim.rows.back(), i);
+  ref_back3[0] = r.x.back(); ref_back3[1] = r.y.back(); ref_back3[2] = r.v.back();
+  *ref_n = (int)r.x.size();
+  if (rows_out) {
+    for (size_t k = 0; k < sim.rows.size() && (int)k < rows_cap; k++)
+      for (int c = 0; c < 10; c++) rows_out[k * 10 + c] = at0(sim.rows[k], c);
+  }
+  return (int)sim.rows.size();
+}
+
+int orc_feasible_goal_bias(void* h, long node) {
+  Oracle* o = (Oracle*)h;
+  return feasible_goal_bias(*o, o->tree[node]) ? 1 : 0;
+}
+
+// Candidate list of the nearest-node search (ids + keys), count returned.
+int orc_sort_nodes(void* h, double sx, double sy, int explore, int* ids, float* keys) {
+  Oracle* o = (Oracle*)h;
+  Pt s; s.x = sx; s.y = sy;
+  std::vector<float> k;
+  std::vector<int> c = sort_nodes(*o, s, explore != 0, o->tree.size(), &k);
+  for (size_t i = 0; i < c.size(); i++) { ids[i] = c[i]; keys[i] = k[i]; }
+  return (int)c.size();
+}
+
+float orc_dubins(void* h, double sx, double sy, long node) {
+  Oracle* o = (Oracle*)h;
+  Pt s; s.x = sx; s.y = sy;
+  return dubins(s, o->tree[node], 1);
+}
+
+// getOBBdist known-answer hook: boxes given as (px, py, w, h, o) with float w/h/o.
+double orc_obb_dist(double apx, double apy, float aw, float ah, float ao, double bpx, double bpy,
+                    float bw, float bh, float bo) {
+  Box a(apx, apy, aw, ah, ao), b(bpx, bpy, bw, bh, bo);
+  return box_gap(a, b);
+}
+
+double orc_check_obs(void* h, const double* x10) {
+  Oracle* o = (Oracle*)h;
+  std::vector<double> x(x10, x10 + 10);
+  return obs_distance(*o, x);
+}
+
+// Draw `n` iterations' samples from glibc rand() in the reference order (rLong, rLat, r).
+void orc_draw_samples(void* h, int n, double* xy, int* explore) {
+  Oracle* o = (Oracle*)h;
+  for (int j = 0; j < n; j++) {
+    Pt s = sample_around(*o);
+    double r = static_cast<double>(rand()) / (static_cast<double>(RAND_MAX / (1)));
+    xy[2 * j] = s.x; xy[2 * j + 1] = s.y;
+    explore[j] = r <= 0.7;
+  }
+}
+
+// Evaluate one iteration for a given sample against the whole tree without appending.
+// Returns the number of nodes it would append (0..2); fills headers (parent of the GB node = -2).
+int orc_eval_iteration(void* h, double sx, double sy, int explore, clrrt_node* out2) {
+  Oracle* o = (Oracle*)h;
+  Pt s; s.x = sx; s.y = sy;
+  IterResult r = evaluate_iteration(*o, s, explore != 0, o->tree.size());
+  int n = 0;
+  Oracle tmp;
+  if (r.added) { tmp.tree.push_back(r.node); n++; }
+  if (r.gb_added) { tmp.tree.push_back(r.gb_node); n++; }
+  if (n) orc_get_nodes(&tmp, 0, n, out2);
+  return n;
+}
+
+}  // extern "C"
