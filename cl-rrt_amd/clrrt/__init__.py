@@ -1,1 +1,282 @@
-"""clrrt — host-side Python binding of libclrrt (the MI355X closed-loop RRT engine)."""
+"""clrrt — Python binding of libclrrt (the MI355X closed-loop RRT tree-expansion engine).
+
+The product is the C-ABI shared library `cl-rrt_amd/libclrrt.so` (HIP kernels for gfx950 + host
+orchestration).  This module only marshals arguments through ctypes; it never computes any part of
+the hot path itself, and it raises if the library (or a GPU, for device entry points) is missing.
+
+The class names mirror the reference's planner objects (vdBerg93/cl-rrt):
+  Planner.expand_tree(...)  <- expandTree           rrt/src/rrtplanner.cpp:123-174
+  Planner.plan(budget_ms)   <- MotionPlanner::planMotion's Timer loop  rrt/src/motionplanner.cpp:39-43
+  Planner.simulate(...)     <- Simulation            rrt/src/simulation.cpp:36-143
+  Planner.sort_nodes(...)   <- sortNodesExplore/Optimize  rrt/src/rrtplanner.cpp:227-268
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import (CLRRT_COLLISION_OBB, CLRRT_COLLISION_STUB, CLRRT_MODE_BATCH,  # noqa: F401
+                  CLRRT_MODE_EXACT, ROLL_NAMES)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libclrrt.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "clrrt.h")
+
+_lib = None
+P = C.POINTER
+
+_SIGS = {
+    "clrrt_abi_version": (C.c_int, []),
+    "clrrt_params_default": (C.c_int, [P(abi.Params), C.c_double, P(C.c_double), C.c_double]),
+    "clrrt_rng_seed": (None, [P(abi.Rng), C.c_uint32]),
+    "clrrt_rng_next": (C.c_int32, [P(abi.Rng)]),
+    "clrrt_draw_samples": (C.c_int, [P(abi.Params), P(abi.Rng), C.c_int32, P(abi.Sample)]),
+    "clrrt_create": (C.c_int, [P(abi.Params), P(abi.Capacity), C.c_int, P(C.c_void_p)]),
+    "clrrt_destroy": (None, [C.c_void_p]),
+    "clrrt_last_error": (C.c_char_p, [C.c_void_p]),
+    "clrrt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "clrrt_set_params": (C.c_int, [C.c_void_p, P(abi.Params)]),
+    "clrrt_set_obstacles": (C.c_int, [C.c_void_p, P(abi.Obstacle), C.c_int32]),
+    "clrrt_set_rank": (C.c_int, [C.c_void_p, C.c_int32]),
+    "clrrt_tree_init": (C.c_int, [C.c_void_p, P(C.c_double)]),
+    "clrrt_tree_load": (C.c_int, [C.c_void_p, P(abi.Node), C.c_int64]),
+    "clrrt_tree_size": (C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64)]),
+    "clrrt_tree_download": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(abi.Node)]),
+    "clrrt_tree_rows": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(C.c_double)]),
+    "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
+    "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
+    "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "clrrt_rollout_batch": (C.c_int, [C.c_void_p, P(abi.RolloutJob), C.c_int32, P(abi.RolloutResult),
+                                      P(C.c_double), C.c_int32]),
+    "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, P(C.c_int32), P(C.c_float)]),
+    "clrrt_get_counters": (C.c_int, [C.c_void_p, P(abi.Counters)]),
+    "clrrt_reset_counters": (C.c_int, [C.c_void_p]),
+    "clrrt_kernel_time": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_int64)]),
+    "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+}
+
+
+class ClrrtError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libclrrt.so (raises loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ClrrtError(f"libclrrt.so not built at {LIB_PATH}: run `make -C cl-rrt_amd/csrc` "
+                             "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+# ----------------------------------------------------------------------------- host-only helpers
+def default_params(v0=0.0, goal=(40.0, 0.0, 0.0, 0.0), vmax=5.0, collision_mode=CLRRT_COLLISION_STUB):
+    p = abi.Params()
+    g = (C.c_double * 4)(*goal)
+    rc = lib().clrrt_params_default(C.byref(p), v0, g, vmax)
+    if rc != 0:
+        raise ClrrtError(f"clrrt_params_default -> {rc}")
+    p.collision_mode = collision_mode
+    return p
+
+
+class Rng:
+    """glibc rand() stream (TYPE_3 additive feedback), srand(seed) semantics."""
+
+    def __init__(self, seed=1):
+        self.state = abi.Rng()
+        lib().clrrt_rng_seed(C.byref(self.state), seed)
+
+    def next(self):
+        return lib().clrrt_rng_next(C.byref(self.state))
+
+    def draw_samples(self, params, n):
+        out = (abi.Sample * n)()
+        rc = lib().clrrt_draw_samples(C.byref(params), C.byref(self.state), n, out)
+        if rc != 0:
+            raise ClrrtError(f"clrrt_draw_samples -> {rc}")
+        return out
+
+
+def samples_to_numpy(samples):
+    xy = np.array([(s.x, s.y) for s in samples], dtype=np.float64).reshape(-1, 2)
+    ex = np.array([s.explore for s in samples], dtype=np.int32)
+    return xy, ex
+
+
+def nodes_to_numpy(nodes):
+    n = len(nodes)
+    raw = np.frombuffer(bytes(nodes), dtype=np.uint8).reshape(n, C.sizeof(abi.Node))
+    f64 = lambda a, b: raw[:, a:b].copy().view(np.float64)  # noqa: E731
+    i32 = lambda a, b: raw[:, a:b].copy().view(np.int32).reshape(-1)  # noqa: E731
+    f32 = lambda a, b: raw[:, a:b].copy().view(np.float32).reshape(-1)  # noqa: E731
+    return {
+        "state": f64(0, 80).reshape(-1, 10), "ref_front": f64(80, 96).reshape(-1, 2),
+        "ref_back": f64(96, 112).reshape(-1, 2), "ref_vback": f64(112, 120).reshape(-1),
+        "ang_par": f64(120, 128).reshape(-1), "parent": i32(128, 132), "costE": f32(132, 136),
+        "costS": f32(136, 140), "goal": i32(140, 144), "nrows": i32(144, 148), "owner": i32(148, 152),
+        "row_offset": raw[:, 152:160].copy().view(np.int64).reshape(-1),
+    }
+
+
+# ----------------------------------------------------------------------------- device planner
+class Planner:
+    """One libclrrt context on one GPU: a MyRRT tree plus the query's parameters and obstacles."""
+
+    def __init__(self, params, device=0, max_nodes=1 << 20, max_rows=1 << 24, max_batch=4096,
+                 max_obstacles=4096):
+        self.L = lib()
+        self.params = params
+        cap = abi.Capacity(max_nodes, max_rows, max_batch, max_obstacles)
+        h = C.c_void_p()
+        rc = self.L.clrrt_create(C.byref(params), C.byref(cap), device, C.byref(h))
+        if rc != 0:
+            raise ClrrtError(f"clrrt_create failed ({rc}): no usable HIP device {device}?")
+        self.h = h
+        self.max_batch = max_batch
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.clrrt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.L.clrrt_last_error(self.h)
+            raise ClrrtError(f"{what} -> {rc}: {msg.decode() if msg else ''}")
+
+    def set_stream(self, stream_ptr):
+        self._chk(self.L.clrrt_set_stream(self.h, C.c_void_p(stream_ptr)), "set_stream")
+
+    def set_params(self, params):
+        self.params = params
+        self._chk(self.L.clrrt_set_params(self.h, C.byref(params)), "set_params")
+
+    def set_rank(self, rank):
+        self._chk(self.L.clrrt_set_rank(self.h, rank), "set_rank")
+
+    def set_obstacles(self, obs):
+        obs = np.ascontiguousarray(obs, dtype=np.float64).reshape(-1, 7)
+        arr = (abi.Obstacle * max(1, len(obs)))()
+        C.memmove(arr, obs.ctypes.data, obs.nbytes)
+        self._chk(self.L.clrrt_set_obstacles(self.h, arr, len(obs)), "set_obstacles")
+
+    def tree_init(self, root=None):
+        root = np.zeros(10) if root is None else np.ascontiguousarray(root, dtype=np.float64)
+        self._chk(self.L.clrrt_tree_init(self.h, root.ctypes.data_as(P(C.c_double))), "tree_init")
+
+    def tree_load(self, nodes_raw):
+        self._chk(self.L.clrrt_tree_load(self.h, nodes_raw, len(nodes_raw)), "tree_load")
+
+    def size(self):
+        n, r = C.c_int64(), C.c_int64()
+        self._chk(self.L.clrrt_tree_size(self.h, C.byref(n), C.byref(r)), "tree_size")
+        return n.value, r.value
+
+    def nodes_raw(self, first=0, count=None):
+        n = self.size()[0] - first if count is None else count
+        arr = (abi.Node * max(1, n))()
+        if n:
+            self._chk(self.L.clrrt_tree_download(self.h, first, n, arr), "tree_download")
+        return arr if n else (abi.Node * 0)()
+
+    def nodes(self):
+        return nodes_to_numpy(self.nodes_raw())
+
+    def rows(self, row_offset, nrows):
+        out = np.zeros((nrows, 10))
+        self._chk(self.L.clrrt_tree_rows(self.h, row_offset, nrows, out.ctypes.data_as(P(C.c_double))), "tree_rows")
+        return out
+
+    def expand(self, rng, n_iters=0, budget_ms=0.0, mode=CLRRT_MODE_EXACT, batch=0):
+        st = abi.Stats()
+        self._chk(self.L.clrrt_expand(self.h, C.byref(rng.state), n_iters, budget_ms, mode, batch, C.byref(st)),
+                  "expand")
+        return {k: getattr(st, k) for k, _ in abi.Stats._fields_}
+
+    # reference-named conveniences
+    def expand_tree(self, rng, n_iters=1):
+        """n_iters sequential expandTree iterations (EXACT semantics)."""
+        return self.expand(rng, n_iters=n_iters, mode=CLRRT_MODE_EXACT)
+
+    def plan(self, rng, budget_ms=200.0, mode=CLRRT_MODE_BATCH, batch=0):
+        """The planMotion budget loop: expand until budget_ms of wall time has elapsed."""
+        return self.expand(rng, n_iters=0, budget_ms=budget_ms, mode=mode, batch=batch)
+
+    def round_eval(self, samples, dev_out_ptr):
+        n_out = C.c_int32()
+        self._chk(self.L.clrrt_round_eval(self.h, samples, len(samples), C.c_void_p(dev_out_ptr), C.byref(n_out)),
+                  "round_eval")
+        return n_out.value
+
+    def round_commit(self, dev_nodes_ptr, n, local_first=0, local_count=0):
+        self._chk(self.L.clrrt_round_commit(self.h, C.c_void_p(dev_nodes_ptr), n, local_first, local_count),
+                  "round_commit")
+
+    def simulate_batch(self, jobs, rows=False):
+        """jobs: list of (parent, gb, sx, sy).  Returns a list of result dicts (+ rows)."""
+        n = len(jobs)
+        arr = (abi.RolloutJob * n)()
+        for i, (par, gb, sx, sy) in enumerate(jobs):
+            arr[i].parent, arr[i].gb = par, gb
+            arr[i].sample[0], arr[i].sample[1] = sx, sy
+        out = (abi.RolloutResult * n)()
+        cap = 512
+        buf = np.zeros((n, cap, 10)) if rows else None
+        self._chk(self.L.clrrt_rollout_batch(self.h, arr, n, out,
+                                             buf.ctypes.data_as(P(C.c_double)) if rows else None, cap),
+                  "rollout_batch")
+        res = []
+        for i in range(n):
+            o = out[i]
+            d = {"outcome": o.outcome, "nrows": o.nrows, "costE": o.costE, "costS": o.costS,
+                 "final": np.array(o.final_state[:]), "ref_back": np.array(o.ref_back[:]),
+                 "ref_vback": o.ref_vback, "ref_n": o.ref_n}
+            if rows:
+                d["rows"] = buf[i, :o.nrows].copy()
+            res.append(d)
+        return res
+
+    def sort_nodes_batch(self, samples):
+        """Candidate lists (ids, keys) for a list of abi.Sample."""
+        n = len(samples)
+        arr = (abi.Sample * n)(*samples)
+        ids = np.zeros((n, 10), dtype=np.int32)
+        keys = np.zeros((n, 10), dtype=np.float32)
+        self._chk(self.L.clrrt_nn_batch(self.h, arr, n, ids.ctypes.data_as(P(C.c_int32)),
+                                        keys.ctypes.data_as(P(C.c_float))), "nn_batch")
+        return ids, keys
+
+    def counters(self):
+        c = abi.Counters()
+        self._chk(self.L.clrrt_get_counters(self.h, C.byref(c)), "get_counters")
+        return {k: getattr(c, k) for k, _ in abi.Counters._fields_}
+
+    def reset_counters(self):
+        self._chk(self.L.clrrt_reset_counters(self.h), "reset_counters")
+
+    def enable_timing(self, on=True):
+        self._chk(self.L.clrrt_enable_timing(self.h, 1 if on else 0), "enable_timing")
+
+    def kernel_time(self, which):
+        ms, n = C.c_double(), C.c_int64()
+        self._chk(self.L.clrrt_kernel_time(self.h, which, C.byref(ms), C.byref(n)), "kernel_time")
+        return ms.value, n.value

@@ -1,0 +1,783 @@
+// clrrt_capi.hip — host side of libclrrt: the C-ABI of include/clrrt.h.
+//
+// Round structure of one batch of expandTree iterations (rrtplanner.cpp:123-174) on the GPU:
+//   1. nearest-node search for every sample against the frozen tree        (k_nn_partial/merge)
+//   2. every candidate rollout of every sample, speculatively in parallel    (k_rollout SPEC)
+//   3. first success per sample -> regular node, goal-bias gate              (k_select)
+//   4. goal-biased rollout from each new node                                (k_rollout GB, k_gb_select)
+//   5. EXACT mode only: first sample whose candidate list a node of an earlier sample of the round
+//      would reorder (k_conflict) -> commit the prefix before it, re-draw nothing, retry the rest
+//   6. scan committed samples -> node records, arena offsets, counters       (k_compact)
+//   7. replay the accepted rollouts writing stateArray rows into the arena   (k_rollout LIST)
+//   8. append the records to the tree                                        (k_append)
+// Failed candidates never write rows: only accepted rollouts are replayed with row output.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/clrrt.h"
+#include "clrrt_dev.hpp"
+#include "clrrt_internal.hpp"
+
+using namespace clrrt;
+
+#define CAND_K 10
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct clrrt_ctx {
+  int device = 0;
+  int rank = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  clrrt_params params;
+  DevParams dp;
+  clrrt_capacity cap;
+  std::string err;
+  // tree
+  clrrt_node* tree = nullptr;
+  NnRec* nn = nullptr;
+  double* arena = nullptr;
+  int64_t n_nodes = 0, n_rows = 0;
+  // obstacles
+  BakedObs* obs = nullptr;
+  int n_obs = 0;
+  // round buffers (capacity cap.max_batch samples)
+  clrrt_sample* d_samples = nullptr;
+  float* pk = nullptr;
+  int* pi = nullptr;
+  int64_t partial_cap = 0;  // entries (samples * chunks * K)
+  int* cand = nullptr;
+  float* ckey = nullptr;
+  int* ncand = nullptr;
+  RollRes* res_spec = nullptr;
+  clrrt_node* regnodes = nullptr;
+  int* gbflag = nullptr;
+  RollRes* res_gb = nullptr;
+  clrrt_node* gbnodes = nullptr;
+  SampleOut* so = nullptr;
+  int* first_conflict = nullptr;
+  clrrt_node* out_nodes = nullptr;
+  Job* jobs = nullptr;
+  RollRes* res_replay = nullptr;
+  int64_t* totals = nullptr;
+  // host staging (pinned)
+  clrrt_sample* h_samples = nullptr;
+  int64_t* h_totals = nullptr;
+  int* h_int = nullptr;
+  // last round_eval bookkeeping
+  int64_t last_eval_rows = 0;
+  // counters
+  clrrt_counters counters{};
+  // timing
+  bool timing = false;
+  double kt_ms[3] = {0, 0, 0};
+  int64_t kt_n[3] = {0, 0, 0};
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+};
+
+// ------------------------------------------------------------------------------------------ util
+static int fail(clrrt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPC(c, call)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (call);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return fail((c), CLRRT_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+template <typename T>
+static hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc((void**)p, count * sizeof(T));
+}
+
+static hipEvent_t ev_get(clrrt_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct KTimer {
+  clrrt_ctx* c;
+  int which;
+  hipEvent_t a = nullptr, b = nullptr;
+  KTimer(clrrt_ctx* c_, int w) : c(c_), which(w) {
+    if (!c->timing) return;
+    a = ev_get(c);
+    b = ev_get(c);
+    if (a) hipEventRecord(a, c->stream);
+  }
+  ~KTimer() {
+    if (!c->timing || !a || !b) return;
+    hipEventRecord(b, c->stream);
+    c->ev_pending.push_back({which, {a, b}});
+  }
+};
+
+static void drain_timers(clrrt_ctx* c) {
+  for (auto& pe : c->ev_pending) {
+    float ms = 0;
+    hipEventSynchronize(pe.second.second);
+    if (hipEventElapsedTime(&ms, pe.second.first, pe.second.second) == hipSuccess) {
+      c->kt_ms[pe.first] += ms;
+      c->kt_n[pe.first] += 1;
+    }
+    c->ev_pool.push_back(pe.second.first);
+    c->ev_pool.push_back(pe.second.second);
+  }
+  c->ev_pending.clear();
+}
+
+// ------------------------------------------------------------------------------------------ params
+static void derive(const clrrt_params& q, DevParams& d, int n_obs) {
+  memset(&d, 0, sizeof(d));
+  d.dmax = q.veh.dmax; d.ddmax = q.veh.ddmax; d.Td = q.veh.Td; d.Ta = q.veh.Ta;
+  d.amin = q.veh.amin; d.amax = q.veh.amax; d.L = q.veh.L; d.Vch = q.veh.Vch; d.Kus = q.veh.Kus;
+  d.dt = q.sim_dt; d.tla = q.ctrl_tla; d.mindla = q.ctrl_mindla;
+  d.dla_c = q.ctrl_mindla - q.ctrl_tla * q.ctrl_dlavmin;  // controller.cpp:14
+  d.Kp = q.ctrl_Kp; d.Ki = q.ctrl_Ki; d.ref_res = q.ref_res; d.vmax = q.vmax; d.ay_road_max = q.ay_road_max;
+  d.g0 = q.goal[0]; d.g1 = q.goal[1]; d.g2 = q.goal[2]; d.g3 = q.goal[3];
+  d.W0 = q.Wcost[0]; d.W1 = q.Wcost[1]; d.W2 = q.Wcost[2]; d.W3 = q.Wcost[3]; d.W4 = q.Wcost[4];
+  d.lane_shift0 = q.lane_shift0; d.Cxy1 = q.Cxy[1]; d.Cxy2 = q.Cxy[2];
+  d.feas_len = 2.1 * q.ref_res;
+  // getGoalReference reference.cpp:27-50 (query constants)
+  double dla_end = std::max(q.ctrl_mindla, d.dla_c + q.ctrl_tla * std::abs(q.goal[3]));
+  double Dext = dla_end, Dal = 1;
+  const double* g = q.goal;
+  d.gbP1x = g[0] + Dal * cos(g[2]); d.gbP1y = g[1] + Dal * sin(g[2]);
+  d.gbP2x = g[0] - Dal * cos(g[2]); d.gbP2y = g[1] - Dal * sin(g[2]);
+  d.gbF1x = d.gbP1x + (Dext + Dal) * cos(g[2]); d.gbF1y = d.gbP1y + (Dext + Dal) * sin(g[2]);
+  d.gbF2x = d.gbP2x + (Dext + Dal) * cos(g[2]); d.gbF2y = d.gbP2y + (Dext + Dal) * sin(g[2]);
+  // feasibleGoalBias rrtplanner.cpp:294-299 (the .y coordinates use cos, as the reference does)
+  double R1 = 4.77;
+  d.gbR2 = R1 - 0.3;
+  d.gbLx = g[0] + R1 * cos(g[2] - M_PI_2); d.gbLy = g[1] + R1 * cos(g[2] - M_PI_2);
+  d.gbRx = g[0] + R1 * cos(g[2] + M_PI_2); d.gbRy = g[1] + R1 * cos(g[2] + M_PI_2);
+  d.bend = q.bend; d.obs_use_pred = q.obs_use_pred; d.sort_limit = std::min(q.sort_limit, CAND_K);
+  d.coll_mode = q.collision_mode;
+  int n = 0;
+  while (n < (20 / q.sim_dt)) n++;  // `for(int i = 0; i<(20/sim_dt); i++)` simulation.cpp:58
+  d.n_steps_max = n;
+  d.use_exp = !(q.Wcost[2] == 0.0 && q.Wcost[3] >= 0.0);  // W2*exp(-W3*Dobs) is exactly +0 otherwise
+  d.n_obs = n_obs;
+  d.need_gap = (q.collision_mode == CLRRT_COLLISION_OBB) && d.use_exp;
+}
+
+// ------------------------------------------------------------------------------------------ C-ABI
+extern "C" {
+
+int clrrt_abi_version(void) { return CLRRT_ABI_VERSION; }
+
+int clrrt_params_default(clrrt_params* p, double v0, const double goal[4], double vmax) {
+  if (!p) return CLRRT_EINVAL;
+  memset(p, 0, sizeof(*p));
+  // Vehicle::setPrius vehicle.h:39-60
+  p->veh.dmax = 0.52; p->veh.ddmax = 0.3294; p->veh.Td = 0.3; p->veh.Ta = 0.3;
+  p->veh.amin = -6; p->veh.amax = 2; p->veh.L = 2.7;
+  double lf = 1.0868, lr = 1.6132, Cf = 22201, Cr = 22201, m = 950 + 640;
+  p->veh.Kus = (m / p->veh.L) * (lr / Cf - lf / Cr);
+  p->veh.Vch = 20;
+  // parameters.launch:3-20
+  p->ctrl_tla = 1.4; p->ctrl_mindla = 3.2; p->ctrl_dlavmin = 3; p->ref_int = 0.02; p->ref_mindist = 0.2;
+  p->sim_dt = 0.04; p->ctrl_Kp = 8; p->ctrl_Ki = 0.05;
+  p->Wcost[0] = 10; p->Wcost[1] = 5; p->Wcost[2] = 0; p->Wcost[3] = 4; p->Wcost[4] = 1;
+  // updateReferenceResolution controller.cpp:18-21 at the query's start velocity
+  p->ref_res = std::max(std::abs(v0) * p->ref_int, p->ref_mindist);
+  p->vmax = vmax;
+  p->ay_road_max = 0;  // rrt_node.cpp:16, never assigned
+  for (int i = 0; i < 4; i++) p->goal[i] = goal ? goal[i] : 0.0;
+  p->bend = 0;
+  p->obs_use_pred = 1;  // rrt_node.cpp:11
+  p->sort_limit = 10;   // rrtplanner.cpp:13
+  p->collision_mode = CLRRT_COLLISION_STUB;
+  return CLRRT_OK;
+}
+
+// glibc random_r TYPE_3 (degree 31, separation 3), seeded like srandom_r: r[0..30] = state,
+// r[31] = front index, r[32] = rear index.
+void clrrt_rng_seed(clrrt_rng* g, uint32_t seed) {
+  int32_t* s = g->r;
+  int32_t word = (int32_t)(seed == 0 ? 1 : seed);
+  s[0] = word;
+  for (int i = 1; i < 31; i++) {
+    int32_t hi = word / 127773, lo = word % 127773;
+    word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    s[i] = word;
+  }
+  s[31] = 3;
+  s[32] = 0;
+  s[33] = 0;
+  g->pos = 0;
+  for (int i = 0; i < 310; i++) clrrt_rng_next(g);
+}
+
+int32_t clrrt_rng_next(clrrt_rng* g) {
+  int32_t* s = g->r;
+  int f = s[31], r = s[32];
+  uint32_t v = (uint32_t)s[f] + (uint32_t)s[r];
+  s[f] = (int32_t)v;
+  int32_t out = (int32_t)(v >> 1);
+  f = f + 1 == 31 ? 0 : f + 1;
+  r = r + 1 == 31 ? 0 : r + 1;
+  s[31] = f;
+  s[32] = r;
+  return out;
+}
+
+// sampleAroundVehicle rrtplanner.cpp:187-201 (rLong, rLat) + heuristic draw :142-143 (r).
+int clrrt_draw_samples(const clrrt_params* p, clrrt_rng* rng, int32_t n, clrrt_sample* out) {
+  if (!p || !rng || (n > 0 && !out)) return CLRRT_EINVAL;
+  const double* g = p->goal;
+  const double RM = 2147483647.0;  // RAND_MAX
+  double dGoal = sqrt(g[0] * g[0] + g[1] * g[1]);
+  double hd = atan2(g[1], g[0]);
+  double latMin = -7, latMax = 7;
+  float fl = (float)(RM / (dGoal + 10));
+  float fw = (float)(RM / (latMax - latMin));
+  double ch = cos(hd), sh = sin(hd), cq = cos(hd + M_PI / 2), sq = sin(hd + M_PI / 2);
+  for (int j = 0; j < n; j++) {
+    double rLong = (float)clrrt_rng_next(rng) / fl;
+    double rLat = latMin + (float)clrrt_rng_next(rng) / fw;
+    out[j].x = rLong * ch + rLat * cq;
+    out[j].y = rLong * sh + rLat * sq;
+    double r = (double)clrrt_rng_next(rng) / (double)(2147483647 / 1);
+    out[j].explore = r <= ((0 * 0.3) + (1 * 0.7));  // RRT.goalReached is never set
+    out[j].pad = 0;
+  }
+  return CLRRT_OK;
+}
+
+const char* clrrt_last_error(const clrrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+static void free_all(clrrt_ctx* c) {
+  void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
+                  c->res_spec, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so, c->first_conflict,
+                  c->out_nodes, c->jobs, c->res_replay, c->totals};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  if (c->h_samples) hipHostFree(c->h_samples);
+  if (c->h_totals) hipHostFree(c->h_totals);
+  if (c->h_int) hipHostFree(c->h_int);
+  for (auto& pe : c->ev_pending) { hipEventDestroy(pe.second.first); hipEventDestroy(pe.second.second); }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+}
+
+int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, clrrt_ctx** out) {
+  if (!p || !out) return CLRRT_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CLRRT_EHIP;
+  if (device < 0 || device >= ndev) return CLRRT_EINVAL;
+  clrrt_ctx* c = new clrrt_ctx();
+  c->device = device;
+  c->params = *p;
+  clrrt_capacity dc;
+  dc.max_nodes = 1 << 20;
+  dc.max_rows = 1 << 24;
+  dc.max_batch = 4096;
+  dc.max_obstacles = 4096;
+  c->cap = cap ? *cap : dc;
+  if (c->cap.max_nodes < 2 || c->cap.max_rows < 2 || c->cap.max_batch < 1 || c->cap.max_obstacles < 0) {
+    delete c;
+    return CLRRT_EINVAL;
+  }
+  derive(c->params, c->dp, 0);
+  int rc = CLRRT_OK;
+  auto chk = [&](hipError_t e) {
+    if (e != hipSuccess && rc == CLRRT_OK) { rc = CLRRT_EHIP; c->err = hipGetErrorString(e); }
+  };
+  chk(hipSetDevice(device));
+  chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->own_stream = true;
+  const int64_t B = c->cap.max_batch;
+  chk(dalloc(&c->tree, c->cap.max_nodes));
+  chk(dalloc(&c->nn, c->cap.max_nodes));
+  chk(dalloc(&c->arena, (size_t)c->cap.max_rows * 10));
+  chk(dalloc(&c->obs, std::max<int64_t>(1, c->cap.max_obstacles)));
+  chk(dalloc(&c->d_samples, B));
+  c->partial_cap = std::max<int64_t>(B * 16, 4096) * CAND_K;
+  chk(dalloc(&c->pk, c->partial_cap));
+  chk(dalloc(&c->pi, c->partial_cap));
+  chk(dalloc(&c->cand, B * CAND_K));
+  chk(dalloc(&c->ckey, B * CAND_K));
+  chk(dalloc(&c->ncand, B));
+  chk(dalloc(&c->res_spec, B * CAND_K));
+  chk(dalloc(&c->regnodes, B));
+  chk(dalloc(&c->gbflag, B));
+  chk(dalloc(&c->res_gb, B));
+  chk(dalloc(&c->gbnodes, B));
+  chk(dalloc(&c->so, B));
+  chk(dalloc(&c->first_conflict, 1));
+  chk(dalloc(&c->out_nodes, 2 * B));
+  chk(dalloc(&c->jobs, 2 * B));
+  chk(dalloc(&c->res_replay, 2 * B));
+  chk(dalloc(&c->totals, 8));
+  chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
+  chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
+  chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
+  if (rc != CLRRT_OK) {
+    fprintf(stderr, "clrrt_create: %s\n", c->err.c_str());
+    free_all(c);
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return CLRRT_OK;
+}
+
+void clrrt_destroy(clrrt_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  free_all(c);
+  delete c;
+}
+
+int clrrt_set_stream(clrrt_ctx* c, void* s) {
+  if (!c) return CLRRT_EINVAL;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  if (s) {
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+  } else {
+    HIPC(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return CLRRT_OK;
+}
+
+int clrrt_set_rank(clrrt_ctx* c, int32_t rank) {
+  if (!c || rank < 0) return CLRRT_EINVAL;
+  c->rank = rank;
+  return CLRRT_OK;
+}
+
+int clrrt_set_params(clrrt_ctx* c, const clrrt_params* p) {
+  if (!c || !p) return CLRRT_EINVAL;
+  c->params = *p;
+  derive(c->params, c->dp, c->n_obs);
+  return CLRRT_OK;
+}
+
+// getOBBvector old_collisioncheck.cpp:6-22, evaluated once per query instead of once per step.
+int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
+  if (!c || m < 0 || (m > 0 && !o)) return CLRRT_EINVAL;
+  if (m > c->cap.max_obstacles) return fail(c, CLRRT_ECAPACITY, "too many obstacles");
+  std::vector<BakedObs> b(m);
+  for (int i = 0; i < m; i++) {
+    BakedObs& d = b[i];
+    memset(&d, 0, sizeof(d));
+    float w = (float)(o[i].size_x / 2), h = (float)(o[i].size_y / 2), th = (float)o[i].theta;
+    float cf = std::cos(th), sf = std::sin(th);
+    float hh = h / 2, ww = w / 2;
+    d.P = cf * hh; d.Q = sf * ww; d.R = sf * hh; d.S = cf * ww;
+    d.cx = o[i].cx; d.cy = o[i].cy; d.vlx = o[i].vx; d.vly = o[i].vy;
+    d.moving = (o[i].vx != 0.0 || o[i].vy != 0.0);
+    // static geometry: centre + 0*t (t >= 0) == centre + 0.0
+    double px = o[i].cx + 0.0, py = o[i].cy + 0.0;
+    d.vx[0] = (float)((px + (double)d.P) - (double)d.Q);
+    d.vy[0] = (float)((py + (double)d.R) + (double)d.S);
+    d.vx[1] = (float)((px + (double)d.P) - (double)(-d.Q));
+    d.vy[1] = (float)((py + (double)d.R) + (double)(-d.S));
+    d.vx[2] = (float)((px + (double)(-d.P)) - (double)(-d.Q));
+    d.vy[2] = (float)((py + (double)(-d.R)) + (double)(-d.S));
+    d.vx[3] = (float)((px + (double)(-d.P)) - (double)d.Q);
+    d.vy[3] = (float)((py + (double)(-d.R)) + (double)d.S);
+    for (int k = 0; k < 3; k++) {
+      d.nx[k] = d.vy[k + 1] - d.vy[k];
+      d.ny[k] = -(d.vx[k + 1] - d.vx[k]);
+    }
+    d.nx[3] = d.vy[0] - d.vy[3];
+    d.ny[3] = -(d.vx[0] - d.vx[3]);
+    d.bcx = (float)o[i].cx; d.bcy = (float)o[i].cy;
+    d.brad = std::sqrt(hh * hh + ww * ww);
+  }
+  HIPC(c, hipSetDevice(c->device));
+  if (m > 0) {
+    HIPC(c, hipMemcpyAsync(c->obs, b.data(), sizeof(BakedObs) * m, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+  }
+  c->n_obs = m;
+  derive(c->params, c->dp, m);
+  return CLRRT_OK;
+}
+
+int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
+  if (!c || !root_state) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  double* d_state = nullptr;
+  HIPC(c, hipMalloc((void**)&d_state, 10 * sizeof(double)));
+  hipError_t e = hipMemcpyAsync(d_state, root_state, 10 * sizeof(double), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_init_root(c->stream, d_state, c->tree, c->nn, c->arena);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d_state);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("tree_init: ") + hipGetErrorString(e));
+  c->n_nodes = 1;
+  c->n_rows = 1;
+  return CLRRT_OK;
+}
+
+int clrrt_tree_load(clrrt_ctx* c, const clrrt_node* nodes, int64_t n) {
+  if (!c || n < 0 || (n > 0 && !nodes)) return CLRRT_EINVAL;
+  if (n > c->cap.max_nodes) return fail(c, CLRRT_ECAPACITY, "tree_load: too many nodes");
+  HIPC(c, hipSetDevice(c->device));
+  if (n > 0) {
+    clrrt_node* tmp = nullptr;
+    HIPC(c, hipMalloc((void**)&tmp, sizeof(clrrt_node) * n));
+    hipError_t e = hipMemcpyAsync(tmp, nodes, sizeof(clrrt_node) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_append(c->stream, tmp, (int)n, 0, c->tree, c->nn);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipFree(tmp);
+    if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("tree_load: ") + hipGetErrorString(e));
+  }
+  c->n_nodes = n;
+  c->n_rows = 0;
+  return CLRRT_OK;
+}
+
+int clrrt_tree_size(clrrt_ctx* c, int64_t* n_nodes, int64_t* n_rows) {
+  if (!c) return CLRRT_EINVAL;
+  if (n_nodes) *n_nodes = c->n_nodes;
+  if (n_rows) *n_rows = c->n_rows;
+  return CLRRT_OK;
+}
+
+int clrrt_tree_download(clrrt_ctx* c, int64_t first, int64_t count, clrrt_node* out) {
+  if (!c || first < 0 || count < 0 || first + count > c->n_nodes || (count > 0 && !out)) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (count == 0) return CLRRT_OK;
+  HIPC(c, hipMemcpyAsync(out, c->tree + first, sizeof(clrrt_node) * count, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_tree_rows(clrrt_ctx* c, int64_t row_offset, int64_t nrows, double* out) {
+  if (!c || row_offset < 0 || nrows < 0 || row_offset + nrows > c->n_rows || (nrows > 0 && !out))
+    return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (nrows == 0) return CLRRT_OK;
+  HIPC(c, hipMemcpyAsync(out, c->arena + row_offset * 10, sizeof(double) * 10 * nrows, hipMemcpyDeviceToHost,
+                         c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_get_counters(clrrt_ctx* c, clrrt_counters* out) {
+  if (!c || !out) return CLRRT_EINVAL;
+  *out = c->counters;
+  return CLRRT_OK;
+}
+
+int clrrt_reset_counters(clrrt_ctx* c) {
+  if (!c) return CLRRT_EINVAL;
+  memset(&c->counters, 0, sizeof(c->counters));
+  return CLRRT_OK;
+}
+
+int clrrt_enable_timing(clrrt_ctx* c, int32_t on) {
+  if (!c) return CLRRT_EINVAL;
+  drain_timers(c);
+  c->timing = on != 0;
+  for (int i = 0; i < 3; i++) { c->kt_ms[i] = 0; c->kt_n[i] = 0; }
+  return CLRRT_OK;
+}
+
+int clrrt_kernel_time(clrrt_ctx* c, int32_t which, double* ms, int64_t* launches) {
+  if (!c || which < 0 || which > 2) return CLRRT_EINVAL;
+  drain_timers(c);
+  if (ms) *ms = c->kt_ms[which];
+  if (launches) *launches = c->kt_n[which];
+  return CLRRT_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------ rounds
+static RollArgs roll_args(clrrt_ctx* c, int njobs) {
+  RollArgs a;
+  memset(&a, 0, sizeof(a));
+  a.p = c->dp;
+  a.tree = c->tree;
+  a.samples = c->d_samples;
+  a.cand = c->cand;
+  a.regnodes = c->regnodes;
+  a.gbflag = c->gbflag;
+  a.jobs = c->jobs;
+  a.obs = c->obs;
+  a.arena = c->arena;
+  a.njobs = njobs;
+  return a;
+}
+
+// Stages 1-4 (+5 in EXACT mode) for n samples already in c->d_samples.  Returns the number of
+// samples to commit (n in BATCH mode).
+static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
+  hipStream_t st = c->stream;
+  {
+    KTimer kt(c, 0);
+    int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * CAND_K));
+    HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
+                      c->ncand, max_chunks));
+  }
+  {
+    KTimer kt(c, 1);
+    RollArgs a = roll_args(c, n * CAND_K);
+    a.res = c->res_spec;
+    HIPC(c, launch_rollout(st, SRC_SPEC, a));
+  }
+  SelArgs s;
+  s.p = c->dp; s.tree = c->tree; s.cand = c->cand; s.ckey = c->ckey; s.ncand = c->ncand; s.res = c->res_spec;
+  s.regnodes = c->regnodes; s.gbflag = c->gbflag; s.so = c->so; s.B = n;
+  {
+    KTimer kt(c, 2);
+    HIPC(c, launch_select(st, s));
+  }
+  {
+    KTimer kt(c, 1);
+    RollArgs a = roll_args(c, n);
+    a.res = c->res_gb;
+    HIPC(c, launch_rollout(st, SRC_GB, a));
+  }
+  {
+    KTimer kt(c, 2);
+    HIPC(c, launch_gb_select(st, n, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so));
+  }
+  int L = n;
+  if (exact && n > 1) {
+    c->h_int[0] = n;
+    HIPC(c, hipMemcpyAsync(c->first_conflict, c->h_int, sizeof(int), hipMemcpyHostToDevice, st));
+    {
+      KTimer kt(c, 2);
+      HIPC(c, launch_conflict(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->first_conflict));
+    }
+    HIPC(c, hipMemcpyAsync(c->h_int + 1, c->first_conflict, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(c, hipStreamSynchronize(st));
+    L = std::max(1, std::min(n, c->h_int[1]));
+  }
+  *L_out = L;
+  return CLRRT_OK;
+}
+
+// Stages 6-7: compact the first L samples into node records (c->out_nodes), reserve arena rows,
+// replay accepted rollouts into the arena.  *n_out = records.
+static int compact_and_replay(clrrt_ctx* c, int L, int* n_out) {
+  hipStream_t st = c->stream;
+  {
+    KTimer kt(c, 2);
+    HIPC(c, launch_compact(st, L, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
+                           c->out_nodes, c->jobs, c->totals));
+  }
+  HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 7, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  int64_t nn = c->h_totals[0], nr = c->h_totals[1];
+  if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
+  c->counters.sim_count += c->h_totals[2];
+  c->counters.fail_collision += c->h_totals[3];
+  c->counters.fail_acclimit += c->h_totals[4];
+  c->counters.fail_iterlimit += c->h_totals[5];
+  c->counters.rollouts += c->h_totals[6];
+  {
+    KTimer kt(c, 1);
+    RollArgs a = roll_args(c, (int)nn);
+    a.res = c->res_replay;
+    HIPC(c, launch_rollout(st, SRC_LIST, a));
+  }
+  c->n_rows += nr;
+  c->last_eval_rows = nr;
+  *n_out = (int)nn;
+  return CLRRT_OK;
+}
+
+static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n) {
+  if (c->n_nodes + n > c->cap.max_nodes) return fail(c, CLRRT_ECAPACITY, "tree full");
+  {
+    KTimer kt(c, 2);
+    HIPC(c, launch_append(c->stream, dev_nodes, n, c->n_nodes, c->tree, c->nn));
+  }
+  c->n_nodes += n;
+  return CLRRT_OK;
+}
+
+extern "C" {
+
+int clrrt_round_eval(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, void* dev_out, int32_t* n_out) {
+  if (!c || n < 0 || (n > 0 && !samples) || !n_out) return CLRRT_EINVAL;
+  if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
+  if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
+  HIPC(c, hipSetDevice(c->device));
+  *n_out = 0;
+  if (n == 0) return CLRRT_OK;
+  memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
+  HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
+  int L = n, rc;
+  if ((rc = eval_samples(c, n, false, &L)) != CLRRT_OK) return rc;
+  int nn = 0;
+  if ((rc = compact_and_replay(c, L, &nn)) != CLRRT_OK) return rc;
+  if (dev_out && nn > 0)
+    HIPC(c, hipMemcpyAsync(dev_out, c->out_nodes, sizeof(clrrt_node) * nn, hipMemcpyDeviceToDevice, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  *n_out = nn;
+  return CLRRT_OK;
+}
+
+int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t local_first, int32_t local_count) {
+  (void)local_first;
+  (void)local_count;  // rows of local records were written to the arena by clrrt_round_eval
+  if (!c || n < 0 || (n > 0 && !dev_nodes)) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  int rc = append_nodes(c, (const clrrt_node*)dev_nodes, n);
+  if (rc != CLRRT_OK) return rc;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
+                 clrrt_stats* out) {
+  if (!c || !rng || n_iters < 0 || (mode != CLRRT_MODE_EXACT && mode != CLRRT_MODE_BATCH)) return CLRRT_EINVAL;
+  if (n_iters == 0 && !(budget_ms > 0)) return CLRRT_EINVAL;
+  if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
+  HIPC(c, hipSetDevice(c->device));
+  batch = std::max(1, std::min<int32_t>(batch > 0 ? batch : c->cap.max_batch, c->cap.max_batch));
+  clrrt_stats st{};
+  auto t0 = std::chrono::steady_clock::now();
+  clrrt_rng work = *rng;       // draws ahead (speculative samples)
+  clrrt_rng committed = *rng;  // state after exactly `iterations` iterations
+  std::deque<clrrt_sample> pending;
+  const bool exact = mode == CLRRT_MODE_EXACT;
+  int cur = exact ? std::min(batch, 16) : batch;
+  int64_t nodes_before = c->n_nodes;
+  int rc = CLRRT_OK;
+  for (;;) {
+    if (n_iters > 0 && st.iterations >= n_iters) break;
+    if (n_iters == 0) {
+      double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (!(ms < budget_ms)) break;
+    }
+    int nb = cur;
+    if (n_iters > 0) nb = (int)std::min<int64_t>(nb, n_iters - st.iterations);
+    while ((int)pending.size() < nb) {
+      clrrt_sample smp;
+      clrrt_draw_samples(&c->params, &work, 1, &smp);
+      pending.push_back(smp);
+    }
+    for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
+    HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
+    int L = nb, nn = 0;
+    if ((rc = eval_samples(c, nb, exact, &L)) != CLRRT_OK) break;
+    if ((rc = compact_and_replay(c, L, &nn)) != CLRRT_OK) break;
+    if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
+    for (int j = 0; j < L; j++) {
+      pending.pop_front();
+      for (int k = 0; k < 3; k++) clrrt_rng_next(&committed);
+    }
+    st.iterations += L;
+    st.speculated += nb;
+    st.rounds++;
+    if (exact) cur = std::max(8, std::min(batch, L == nb ? 2 * nb : 2 * L));
+  }
+  HIPC(c, hipStreamSynchronize(c->stream));
+  st.nodes_added = c->n_nodes - nodes_before;
+  st.elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *rng = committed;
+  if (out) *out = st;
+  return rc;
+}
+
+int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, clrrt_rollout_result* out,
+                        double* rows_out, int32_t rows_cap) {
+  if (!c || n < 0 || (n > 0 && (!jobs || !out))) return CLRRT_EINVAL;
+  if (rows_out && rows_cap < c->dp.n_steps_max + 1) return fail(c, CLRRT_EINVAL, "rows_cap < max steps + 1");
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  for (int j = 0; j < n; j++)
+    if (jobs[j].parent < 0 || jobs[j].parent >= c->n_nodes) return fail(c, CLRRT_EINVAL, "job parent out of range");
+  std::vector<Job> hj(n);
+  for (int j = 0; j < n; j++) {
+    hj[j].parent = jobs[j].parent; hj[j].from_reg = 0; hj[j].gb = jobs[j].gb; hj[j].pad = 0;
+    hj[j].sx = jobs[j].sample[0]; hj[j].sy = jobs[j].sample[1];
+    hj[j].row_off = rows_out ? (int64_t)j * rows_cap : -1;
+  }
+  Job* dj = nullptr;
+  RollRes* dr = nullptr;
+  double* drows = nullptr;
+  hipError_t e = hipMalloc((void**)&dj, sizeof(Job) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&dr, sizeof(RollRes) * n);
+  if (e == hipSuccess && rows_out) e = hipMalloc((void**)&drows, sizeof(double) * 10 * (size_t)rows_cap * n);
+  if (e == hipSuccess) e = hipMemcpyAsync(dj, hj.data(), sizeof(Job) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    RollArgs a = roll_args(c, n);
+    a.jobs = dj;
+    a.arena = drows;
+    a.res = dr;
+    KTimer kt(c, 1);
+    e = launch_rollout(c->stream, SRC_LIST, a);
+  }
+  std::vector<RollRes> hr(n);
+  if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), dr, sizeof(RollRes) * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && rows_out)
+    e = hipMemcpyAsync(rows_out, drows, sizeof(double) * 10 * (size_t)rows_cap * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(dj);
+  hipFree(dr);
+  if (drows) hipFree(drows);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("rollout_batch: ") + hipGetErrorString(e));
+  for (int j = 0; j < n; j++) {
+    clrrt_rollout_result& o = out[j];
+    memset(&o, 0, sizeof(o));
+    o.outcome = hr[j].outcome;
+    o.nrows = hr[j].nrows;
+    o.costE = hr[j].costE;
+    o.costS = hr[j].costS;
+    for (int k = 0; k < 10; k++) o.final_state[k] = hr[j].st[k];
+    o.ref_back[0] = hr[j].bx; o.ref_back[1] = hr[j].by;
+    o.ref_vback = hr[j].vback;
+    o.ref_n = hr[j].refN;
+  }
+  return CLRRT_OK;
+}
+
+int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t* out_ids, float* out_keys) {
+  if (!c || n < 0 || (n > 0 && (!samples || !out_ids))) return CLRRT_EINVAL;
+  if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
+  HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
+  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * CAND_K));
+  {
+    KTimer kt(c, 0);
+    HIPC(c, launch_nn(c->stream, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
+                      c->ncand, max_chunks));
+  }
+  HIPC(c, hipMemcpyAsync(out_ids, c->cand, sizeof(int) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));
+  if (out_keys)
+    HIPC(c, hipMemcpyAsync(out_keys, c->ckey, sizeof(float) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+}  // extern "C"

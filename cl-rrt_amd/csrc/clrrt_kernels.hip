@@ -1,0 +1,636 @@
+// clrrt_kernels.hip — gfx950 kernels of the expandTree hot path.
+//
+//   k_nn_partial / k_nn_merge : nearest-node search (sortNodesExplore/Optimize, rrtplanner.cpp:227-268)
+//                               lanes = samples, loop over a node chunk with wave-uniform (scalar)
+//                               node loads, per-lane top-K in registers, Euclidean prune (key >= |q|)
+//   k_rollout                 : closed-loop rollouts (Simulation, simulation.cpp:36-143), one lane per
+//                               rollout job; obstacle bounding circles staged in LDS
+//   k_select / k_gb_select    : first successful candidate per sample (expandTree :150-160), goal-bias
+//                               gate (feasibleGoalBias :292-315) and node construction (:156,170)
+//   k_conflict                : EXACT mode — does a node appended earlier in the round reorder a
+//                               later sample's candidate list?
+//   k_compact                 : prefix scan over committed samples -> node records + arena offsets +
+//                               replay jobs (wave ballot / block scan)
+//   k_append                  : RRT.addNode for a batch of records (rrtplanner.h:111-113)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "clrrt_dev.hpp"
+#include "clrrt_internal.hpp"
+
+namespace clrrt {
+
+#define CAND_K 10
+static_assert(CAND_K == 10, "sortLimit");
+
+// --------------------------------------------------------------------------------------------
+// nearest-node search
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool lex_less(float ka, int ia, float kb, int ib) {
+  return (ka < kb) || (ka == kb && ia < ib);
+}
+
+// Insert (k, i) into the ascending register list (static indices only: stays in VGPRs).
+__device__ __forceinline__ void topk_insert(float (&keys)[CAND_K], int (&ids)[CAND_K], float k, int i) {
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) {
+    bool sw = lex_less(k, i, keys[j], ids[j]);
+    float tk = keys[j];
+    int ti = ids[j];
+    keys[j] = sw ? k : tk;
+    ids[j] = sw ? i : ti;
+    k = sw ? tk : k;
+    i = sw ? ti : i;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
+                                                    const NnRec* __restrict__ nodes, int N, int chunk,
+                                                    int nchunks, DevParams p, float* __restrict__ pk,
+                                                    int* __restrict__ pi) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  const int n0 = c * chunk;
+  const int n1 = min(N, n0 + chunk);
+  const bool act = s < B;
+  double sx = 0, sy = 0;
+  int ex = 1;
+  if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
+  float keys[CAND_K];
+  int ids[CAND_K];
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  for (int n = n0; n < n1; n++) {
+    const NnRec rec = nodes[n];
+    float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
+    float lb = sqrtf(qx * qx + qy * qy) * 0.99999f - 1e-4f;
+    if (!ex) lb = rec.costE + lb;
+    if (act && lb <= keys[CAND_K - 1]) {
+      float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+      if (!ex) k = rec.costE + k;
+      if (lex_less(k, n, keys[CAND_K - 1], ids[CAND_K - 1]) &&
+          feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
+        topk_insert(keys, ids, k, n);
+    }
+  }
+  if (act) {
+    size_t base = ((size_t)s * nchunks + c) * CAND_K;
+#pragma unroll
+    for (int j = 0; j < CAND_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
+  }
+}
+
+__global__ void k_nn_merge(int B, int nchunks, int limit, const float* __restrict__ pk,
+                           const int* __restrict__ pi, int* __restrict__ cand, float* __restrict__ ckey,
+                           int* __restrict__ ncand) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B) return;
+  float keys[CAND_K];
+  int ids[CAND_K];
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  for (int c = 0; c < nchunks; c++) {
+    size_t base = ((size_t)s * nchunks + c) * CAND_K;
+    for (int j = 0; j < CAND_K; j++) {
+      int id = pi[base + j];
+      if (id == 0x7fffffff) break;
+      float k = pk[base + j];
+      if (lex_less(k, id, keys[CAND_K - 1], ids[CAND_K - 1])) topk_insert(keys, ids, k, id);
+      else break;  // chunk lists are sorted
+    }
+  }
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) {
+    bool v = ids[j] != 0x7fffffff && j < limit;
+    cand[s * CAND_K + j] = v ? ids[j] : -1;
+    ckey[s * CAND_K + j] = keys[j];
+    n += v;
+  }
+  ncand[s] = n;
+}
+
+// --------------------------------------------------------------------------------------------
+// rollouts
+// --------------------------------------------------------------------------------------------
+struct ObsView {
+  const BakedObs* __restrict__ g;  // global baked records
+  const float4* cv;                // LDS: (cx, cy, vx, vy) float
+  const float* rad;                // LDS: bounding radius + vehicle radius + margin
+  int n;
+};
+
+#define VEH_RAD 2.6220219f  /* sqrt(2.424^2 + 1^2), vehicle half-diagonal */
+#define CULL_MARGIN 0.05f
+
+// checkObsDistance (stub collisioncheck.cpp:6-8 | OBB old_collisioncheck.cpp:24-51).
+template <bool NEED_GAP>
+__device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p, const ObsView& ov) {
+  if (p.coll_mode == CLRRT_COLLISION_STUB) return 100.0;
+  const double t = p.obs_use_pred ? r.x6 : 0.0;
+  const double vpx = r.x0 + 1.424 * r.c2, vpy = r.x1 + 1.424 * r.s2;
+  const float of = (float)r.x2;
+  const float cf = cosf(of), sf = sinf(of);
+  const float hh = 4.848f / 2, ww = 2.0f / 2;
+  Box4 veh;
+  box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
+  const float fvx = (float)vpx, fvy = (float)vpy, ft = (float)t;
+  double best = 10000;
+  for (int j = 0; j < ov.n; j++) {
+    if (!NEED_GAP) {
+      float4 q = ov.cv[j];
+      float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
+      float rr = ov.rad[j];
+      if (dx * dx + dy * dy > rr * rr) continue;  // bounding circles apart: no overlap possible
+    }
+    const BakedObs& o = ov.g[j];
+    float D;
+    if (!o.moving) {
+      D = sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
+    } else {
+      float bvx[4], bvy[4], bnx[4], bny[4];
+      box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
+      D = sat_gap(veh, bvx, bvy, bnx, bny);
+    }
+    if (D == 0) return 0.0;
+    if (NEED_GAP && (double)D < best) best = D;
+  }
+  return best;
+}
+
+// One Euler step of Simulation::propagate (simulation.cpp:58-137).  Fills the logged row columns
+// 7..9 and returns CLRRT_ROLL_* or -1 to continue.
+template <bool NEED_GAP>
+__device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
+                                         double& col8, double& col9) {
+  double Px, Py;
+  // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
+  double dla = update_waypoint(r, p, Px, Py, false);
+  double ym = lateral_error(r, Px, Py);
+  double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
+  double dc = satd(-p.dmax, p.dmax, cmd);
+  double E = prof_v(r.P, r.wp + 2) - r.x4;
+  r.iE = r.iE + E * p.dt;
+  double ac = satd(p.amin, p.amax, p.Kp * E + p.Ki * r.iE);
+  // VehicleODE (simulation.cpp:11-25)
+  double q = r.x4 / p.Vch;
+  double Gss = 1 / (1 + q * q);
+  double d0 = r.x4 * r.c2, d1 = r.x4 * r.s2;
+  double d2 = (r.x4 / p.L) * r.t3 * Gss;
+  double d3 = (1 / p.Td) * (dc - r.x3);
+  double d4 = r.x5;
+  double d5 = (1 / p.Ta) * (ac - r.x5);
+  d4 = satd(p.amin, p.amax, d4);
+  d3 = satd(-p.ddmax, p.ddmax, d3);
+  // IntegrateEuler (simulation.cpp:27-34)
+  r.x0 = r.x0 + d0 * p.dt;
+  r.x1 = r.x1 + d1 * p.dt;
+  r.x2 = r.x2 + d2 * p.dt;
+  r.x3 = r.x3 + d3 * p.dt;
+  r.x4 = r.x4 + d4 * p.dt;
+  r.x5 = r.x5 + d5 * p.dt;
+  r.x6 = r.x6 + 1.0 * p.dt;
+  r.x3 = satd(-p.dmax, p.dmax, r.x3);
+  r.c2 = cos(r.x2);
+  r.s2 = sin(r.x2);
+  r.t3 = tan(r.x3);
+  col7 = (double)r.wp;
+  col8 = prof_v(r.P, r.wp + 2);
+  col9 = dc;
+  // collision (simulation.cpp:83-86)
+  double Dobs = obs_distance<NEED_GAP>(r, p, ov);
+  if (Dobs == 0) return CLRRT_ROLL_COLLISION;
+  // costs (simulation.cpp:89-95)
+  r.costE += r.x4 * p.dt;
+  double kappa = r.t3 / p.L;
+  double term = p.W0 * r.x4 * p.dt + p.W1 * fabs(kappa);
+  if (p.use_exp) term = term + p.W2 * exp(-p.W3 * Dobs);
+  r.costS += term;
+  if (p.bend) r.costS += p.W4 * dist_to_lane(r.x0, r.x1, p.lane_shift0, p.Cxy1, p.Cxy2);
+  // lateral acceleration limit (simulation.cpp:98-104)
+  double ay = fabs(r.x4 * d2);
+  if (ay + p.ay_road_max > 3) return CLRRT_ROLL_ACCLIMIT;
+  // end / goal (simulation.cpp:110-133)
+  double ex = r.x0 - p.g0, ey = r.x1 - p.g1;
+  double dg = sqrt(ex * ex + ey * ey);
+  double he = fabs(angle_diff(r.x2, p.g2));
+  double Ve = (r.x4 - r.vback);
+  if (r.endr && (Ve < 0.1)) return CLRRT_ROLL_END;
+  if ((dg <= 1) && (he < 0.05)) return CLRRT_ROLL_GOAL;
+  return -1;
+}
+
+__device__ __forceinline__ void store_row(double* __restrict__ row, const Roll& r, double c7, double c8,
+                                          double c9) {
+  row[0] = r.x0; row[1] = r.x1; row[2] = r.x2; row[3] = r.x3; row[4] = r.x4;
+  row[5] = r.x5; row[6] = r.x6; row[7] = c7; row[8] = c8; row[9] = c9;
+}
+
+// One whole rollout.  `ps` = parent state (10 doubles), (pbx, pby) = parent ref.back(),
+// pvb = parent ref.v.back().  rows (nullable) receives stateArray.
+template <bool NEED_GAP>
+__device__ void run_rollout(const double* ps, double pbx, double pby, double pvb, int gb, double sx,
+                            double sy, const DevParams& p, const ObsView& ov, double* __restrict__ rows,
+                            RollRes& out) {
+  RefD R = gb ? make_goal_ref(pbx, pby, p) : make_ref(pbx, pby, sx, sy, p);
+  Roll r;
+  roll_init(r, ps, R, pvb, gb != 0, p);
+  double c7 = (double)r.wp, c8 = ps[8], c9 = ps[9];
+  if (rows) {
+    for (int k = 0; k < 10; k++) rows[k] = ps[k];
+    rows[7] = c7;
+  }
+  int outcome = CLRRT_ROLL_ITERLIMIT;
+  int steps = 0;
+  for (int i = 0; i < p.n_steps_max; i++) {
+    steps++;
+    int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9);
+    if (rows) store_row(rows + (size_t)steps * 10, r, c7, c8, c9);
+    if (o >= 0) { outcome = o; break; }
+  }
+  out.st[0] = r.x0; out.st[1] = r.x1; out.st[2] = r.x2; out.st[3] = r.x3; out.st[4] = r.x4;
+  out.st[5] = r.x5; out.st[6] = r.x6; out.st[7] = c7; out.st[8] = c8; out.st[9] = c9;
+  out.costE = r.costE;
+  out.costS = r.costS;
+  out.bx = r.R.bx; out.by = r.R.by;
+  out.fx = r.R.a1x; out.fy = r.R.a1y;
+  out.vback = r.vback;
+  out.outcome = outcome;
+  out.nrows = steps + 1;
+  out.refN = r.R.N;
+}
+
+
+template <int SRC, bool NEED_GAP>
+__global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
+  extern __shared__ float4 lds[];
+  float4* cv = lds;
+  float* rad = (float*)(lds + a.p.n_obs);
+  if (a.p.coll_mode == CLRRT_COLLISION_OBB && !NEED_GAP) {
+    for (int j = threadIdx.x; j < a.p.n_obs; j += blockDim.x) {
+      const BakedObs& o = a.obs[j];
+      cv[j] = make_float4((float)o.cx, (float)o.cy, (float)o.vlx, (float)o.vly);
+      float rr = o.brad + VEH_RAD + CULL_MARGIN;
+      rad[j] = rr;
+    }
+    __syncthreads();
+  }
+  ObsView ov{a.obs, cv, rad, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0};
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.njobs) return;
+  const double* ps;
+  double pbx, pby, pvb, sx = 0, sy = 0;
+  int gb = 0;
+  double* rows = nullptr;
+  if (SRC == SRC_SPEC) {
+    int s = j / CAND_K;
+    int id = a.cand[j];
+    if (id < 0) { a.res[j].outcome = -1; return; }
+    const clrrt_node& n = a.tree[id];
+    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+    sx = a.samples[s].x; sy = a.samples[s].y;
+  } else if (SRC == SRC_GB) {
+    if (!a.gbflag[j]) { a.res[j].outcome = -1; return; }
+    const clrrt_node& n = a.regnodes[j];
+    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+    gb = 1;
+  } else {
+    const Job& jb = a.jobs[j];
+    const clrrt_node& n = jb.from_reg ? a.regnodes[jb.parent] : a.tree[jb.parent];
+    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+    gb = jb.gb; sx = jb.sx; sy = jb.sy;
+    if (jb.row_off >= 0) rows = a.arena + (size_t)jb.row_off * 10;
+  }
+  RollRes out;
+  run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, out);
+  a.res[j] = out;
+}
+
+// --------------------------------------------------------------------------------------------
+// selection, goal bias, conflicts
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const double* st, double bx,
+                                                   double by) {
+  bool outL = sqrt((st[0] - p.gbLx) * (st[0] - p.gbLx) + (st[1] - p.gbLy) * (st[1] - p.gbLy)) > p.gbR2;
+  bool outR = sqrt((st[0] - p.gbRx) * (st[0] - p.gbRx) + (st[1] - p.gbRy) * (st[1] - p.gbRy)) > p.gbR2;
+  double aRef = atan2(p.g1 - by, p.g0 - bx);
+  double h1 = fabs(wrap_pi(p.g2 - aRef));
+  double h2 = fabs(wrap_pi(p.g2 + M_PI - aRef));
+  double m = mn(h1, h2);
+  double cv = cos(p.g2 + M_PI_2 - aRef);
+  double sg = (double)((0.0 < cv) - (cv < 0.0));
+  double ang = sg * m;
+  bool within = fabs(ang) < (M_PI_4 / 2);
+  return outL && outR && within;
+}
+
+__device__ __forceinline__ void fill_node(clrrt_node& n, const RollRes& r, int parent, float pcE,
+                                          float pcS) {
+  for (int k = 0; k < 10; k++) n.state[k] = r.st[k];
+  n.ref_front[0] = r.fx; n.ref_front[1] = r.fy;
+  n.ref_back[0] = r.bx; n.ref_back[1] = r.by;
+  n.ref_vback = r.vback;
+  n.ang_par = atan2(r.by - r.fy, r.bx - r.fx);
+  n.parent = parent;
+  n.costE = (float)(r.costE + (double)pcE);
+  n.costS = (float)(r.costS + (double)pcS);
+  n.goal = r.outcome == CLRRT_ROLL_GOAL;
+  n.nrows = r.nrows;
+  n.owner = 0;
+  n.row_offset = -1;
+}
+
+
+__global__ void k_select(SelArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.B) return;
+  const int nc = a.ncand[s];
+  SampleOut o = {};
+  o.k = -1;
+  for (int k = 0; k < nc; k++) {
+    const RollRes& r = a.res[s * CAND_K + k];
+    o.rollouts++;
+    o.steps += r.nrows - 1;
+    o.f_col += r.outcome == CLRRT_ROLL_COLLISION;
+    o.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
+    o.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
+    if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL) { o.k = k; break; }
+  }
+  // EXACT-mode conflict threshold: the key a new node must beat (<=) to be tried before the result.
+  o.thr = o.k >= 0 ? a.ckey[s * CAND_K + o.k] : (nc == a.p.sort_limit ? a.ckey[s * CAND_K + nc - 1] : __builtin_inff());
+  int gbf = 0;
+  if (o.k >= 0) {
+    const int pid = a.cand[s * CAND_K + o.k];
+    const clrrt_node& par = a.tree[pid];
+    clrrt_node n;
+    fill_node(n, a.res[s * CAND_K + o.k], pid, par.costE, par.costS);
+    a.regnodes[s] = n;
+    o.nrows_reg = n.nrows;
+    gbf = feasible_goal_bias(a.p, n.state, n.ref_back[0], n.ref_back[1]);
+  }
+  a.gbflag[s] = gbf;
+  a.so[s] = o;
+}
+
+__global__ void k_gb_select(int B, const clrrt_node* __restrict__ regnodes, const int* __restrict__ gbflag,
+                            const RollRes* __restrict__ gbres, clrrt_node* gbnodes, SampleOut* so) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B) return;
+  SampleOut o = so[s];
+  o.gb_ok = 0;
+  if (gbflag[s]) {
+    const RollRes& r = gbres[s];
+    o.rollouts++;
+    o.steps += r.nrows - 1;
+    o.f_col += r.outcome == CLRRT_ROLL_COLLISION;
+    o.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
+    o.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
+    if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL) {
+      clrrt_node n;
+      fill_node(n, r, CLRRT_PARENT_PREV, regnodes[s].costE, regnodes[s].costS);
+      gbnodes[s] = n;
+      o.gb_ok = 1;
+      o.nrows_gb = n.nrows;
+    }
+  }
+  so[s] = o;
+}
+
+// EXACT mode: sample j conflicts when a node produced by an earlier sample of the round would sort
+// at or before j's accepted candidate (or into j's candidate window when nothing was accepted).
+__global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ S,
+                           const clrrt_node* __restrict__ regnodes, const clrrt_node* __restrict__ gbnodes,
+                           const SampleOut* __restrict__ so, int* first_conflict) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  const double sx = S[j].x, sy = S[j].y;
+  const int ex = S[j].explore;
+  const float thr = so[j].thr;
+  bool conflict = false;
+  for (int k = 0; k < j && !conflict; k++) {
+    if (so[k].k < 0) continue;
+    for (int w = 0; w < 2; w++) {
+      if (w == 1 && !so[k].gb_ok) break;
+      const clrrt_node& n = w == 0 ? regnodes[k] : gbnodes[k];
+      float c = cosf((float)(-n.state[2] - 0.0)), s = sinf((float)(-n.state[2] - 0.0));
+      float key = dubins_key(sx, sy, n.state[0], n.state[1], c, s);
+      if (!ex) key = n.costE + key;
+      if (!(key > thr) && feasible_node(n.ref_back[0], n.ref_back[1], n.ang_par, sx, sy, p.feas_len)) {
+        conflict = true;
+        break;
+      }
+    }
+  }
+  if (conflict) atomicMin(first_conflict, j);
+}
+
+// --------------------------------------------------------------------------------------------
+// compaction of committed samples (one block, sequential chunks + block scan)
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __restrict__ S,
+                                                  const int* __restrict__ cand,
+                                                  const clrrt_node* __restrict__ regnodes,
+                                                  const clrrt_node* __restrict__ gbnodes,
+                                                  const SampleOut* __restrict__ so, int64_t row_base,
+                                                  int rank, clrrt_node* __restrict__ out, Job* __restrict__ jobs,
+                                                  int64_t* __restrict__ totals) {
+  __shared__ int64_t s_nodes[1024], s_rows[1024];
+  __shared__ int64_t s_cnt[8];
+  const int t = threadIdx.x;
+  const int per = (L + blockDim.x - 1) / blockDim.x;
+  const int b0 = min(L, t * per), b1 = min(L, b0 + per);
+  int64_t nn = 0, nr = 0;
+  int64_t cnt[5] = {0, 0, 0, 0, 0};
+  for (int s = b0; s < b1; s++) {
+    const SampleOut& o = so[s];
+    if (o.k >= 0) { nn++; nr += o.nrows_reg; }
+    if (o.gb_ok) { nn++; nr += o.nrows_gb; }
+    cnt[0] += o.steps; cnt[1] += o.f_col; cnt[2] += o.f_acc; cnt[3] += o.f_it; cnt[4] += o.rollouts;
+  }
+  s_nodes[t] = nn;
+  s_rows[t] = nr;
+  if (t < 8) s_cnt[t] = 0;
+  __syncthreads();
+  for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+    int64_t vn = t >= off ? s_nodes[t - off] : 0;
+    int64_t vr = t >= off ? s_rows[t - off] : 0;
+    __syncthreads();
+    s_nodes[t] += vn;
+    s_rows[t] += vr;
+    __syncthreads();
+  }
+  for (int c = 0; c < 5; c++) atomicAdd((unsigned long long*)&s_cnt[c], (unsigned long long)cnt[c]);
+  int64_t node_off = s_nodes[t] - nn, row_off = s_rows[t] - nr;
+  for (int s = b0; s < b1; s++) {
+    const SampleOut& o = so[s];
+    if (o.k >= 0) {
+      clrrt_node n = regnodes[s];
+      n.owner = rank;
+      n.row_offset = row_base + row_off;
+      out[node_off] = n;
+      Job jb;
+      jb.parent = cand[s * CAND_K + o.k]; jb.from_reg = 0; jb.gb = 0;
+      jb.sx = S[s].x; jb.sy = S[s].y;
+      jb.row_off = row_base + row_off;
+      jobs[node_off] = jb;
+      node_off++;
+      row_off += o.nrows_reg;
+    }
+    if (o.gb_ok) {
+      clrrt_node n = gbnodes[s];
+      n.owner = rank;
+      n.row_offset = row_base + row_off;
+      out[node_off] = n;
+      Job jb;
+      jb.parent = s; jb.from_reg = 1; jb.gb = 1;
+      jb.sx = 0; jb.sy = 0;
+      jb.row_off = row_base + row_off;
+      jobs[node_off] = jb;
+      node_off++;
+      row_off += o.nrows_gb;
+    }
+  }
+  __syncthreads();
+  if (t == blockDim.x - 1) {
+    totals[0] = s_nodes[t];
+    totals[1] = s_rows[t];
+  }
+  if (t < 5) totals[2 + t] = s_cnt[t];
+}
+
+// RRT.addNode for n records: resolve GB parents (CLRRT_PARENT_PREV -> the record before) and build
+// the nearest-node mirror.
+__global__ void k_append(const clrrt_node* __restrict__ in, int n, int64_t base, clrrt_node* __restrict__ tree,
+                         NnRec* __restrict__ nn) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  clrrt_node d = in[i];
+  if (d.parent == CLRRT_PARENT_PREV) d.parent = (int32_t)(base + i - 1);
+  tree[base + i] = d;
+  NnRec r;
+  r.x = d.state[0]; r.y = d.state[1];
+  r.bx = d.ref_back[0]; r.by = d.ref_back[1];
+  r.ang_par = d.ang_par;
+  float ang = (float)(-d.state[2] - 0.0);
+  r.c = cosf(ang); r.s = sinf(ang);
+  r.costE = d.costE;
+  r.pad = 0.f;
+  nn[base + i] = r;
+}
+
+// addInitialNode rrtplanner.cpp:21-37: reference = linspace(0, 1, floor(1/0.1)) at v = state[4].
+__global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnRec* nn, double* arena) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int N = (int)floor(sqrt(1.0 * 1.0 + 0.0 * 0.0) / 0.1);
+  double h = (1.0 - 0.0) / (double)(uint64_t)(N - 1);
+  double x = 0.0;
+  for (int i = 1; i < N; i++) x += h;
+  clrrt_node n;
+  for (int k = 0; k < 10; k++) { n.state[k] = st[k]; arena[k] = st[k]; }
+  n.ref_front[0] = 0.0; n.ref_front[1] = 0.0;
+  n.ref_back[0] = x; n.ref_back[1] = 0.0;
+  n.ref_vback = st[4];
+  n.ang_par = atan2(0.0 - 0.0, x - 0.0);
+  n.parent = -1;
+  n.costE = 0.f; n.costS = 0.f;
+  n.goal = 0;
+  n.nrows = 1;
+  n.owner = 0;
+  n.row_offset = 0;
+  tree[0] = n;
+  NnRec r;
+  r.x = n.state[0]; r.y = n.state[1]; r.bx = x; r.by = 0.0; r.ang_par = n.ang_par;
+  float ang = (float)(-n.state[2] - 0.0);
+  r.c = cosf(ang); r.s = sinf(ang); r.costE = 0.f; r.pad = 0.f;
+  nn[0] = r;
+}
+
+// ============================================================================================
+// launch wrappers (host)
+// ============================================================================================
+#define LAUNCH_CHECK()                                   \
+  do {                                                   \
+    hipError_t e__ = hipGetLastError();                  \
+    if (e__ != hipSuccess) return e__;                   \
+  } while (0)
+
+hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                     const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
+                     int max_chunks) {
+  int groups = (B + 255) / 256;
+  int nchunks = (N + 255) / 256;
+  int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
+  nchunks = max(1, min(nchunks, min(want, max_chunks)));
+  int chunk = (N + nchunks - 1) / nchunks;
+  nchunks = (N + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
+                     p, pk, pi);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
+                     cand, ckey, ncand);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+template <int SRC>
+static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
+  if (a.njobs <= 0) return hipSuccess;
+  size_t lds = (a.p.coll_mode == CLRRT_COLLISION_OBB) ? (size_t)a.p.n_obs * (sizeof(float4) + sizeof(float)) : 0;
+  dim3 grid((a.njobs + 255) / 256), block(256);
+  if (a.p.need_gap)
+    hipLaunchKernelGGL((k_rollout<SRC, true>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((k_rollout<SRC, false>), grid, block, lds, st, a);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
+  if (src == SRC_SPEC) return launch_roll_t<SRC_SPEC>(st, a);
+  if (src == SRC_GB) return launch_roll_t<SRC_GB>(st, a);
+  return launch_roll_t<SRC_LIST>(st, a);
+}
+
+hipError_t launch_select(hipStream_t st, const SelArgs& a) {
+  hipLaunchKernelGGL(k_select, dim3((a.B + 255) / 256), dim3(256), 0, st, a);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const int* gbflag,
+                            const RollRes* gbres, clrrt_node* gbnodes, SampleOut* so) {
+  hipLaunchKernelGGL(k_gb_select, dim3((B + 255) / 256), dim3(256), 0, st, B, reg, gbflag, gbres, gbnodes, so);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
+                           const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, int* first) {
+  hipLaunchKernelGGL(k_conflict, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, first);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
+                          const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
+                          clrrt_node* out, Job* jobs, int64_t* totals) {
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, L, S, cand, reg, gbn, so, row_base, rank, out, jobs,
+                     totals);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_append, dim3((n + 255) / 256), dim3(256), 0, st, in, n, base, tree, nn);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_init_root(hipStream_t st, const double* state, clrrt_node* tree, NnRec* nn, double* arena) {
+  hipLaunchKernelGGL(k_init_root, dim3(1), dim3(64), 0, st, state, tree, nn, arena);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+}  // namespace clrrt

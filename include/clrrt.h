@@ -54,6 +54,9 @@ extern "C" {
 #define CLRRT_MODE_EXACT 0
 #define CLRRT_MODE_BATCH 1
 
+/* parent id of a goal-biased record in a round's node batch: "the record just before me" */
+#define CLRRT_PARENT_PREV (-2)
+
 /* ---- collision modes ---- */
 #define CLRRT_COLLISION_STUB 0 /* checkObsDistance returns 100 (rrt/src/collisioncheck.cpp:6-8) */
 #define CLRRT_COLLISION_OBB 1  /* OBB separating-axis test (rrt/src/old_collisioncheck.cpp:6-148) */
