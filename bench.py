@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X closed-loop RRT expansion engine (BASELINE.json metric:
+nodes expanded/sec + feasible-paths/sec, 200-obstacle scene, 1/2/4/8 GPU).
+
+A step is one planning query (MotionPlanner::planMotion, rrt/src/motionplanner.cpp:8-77 of the
+reference): a fresh tree from the root, then expansion rounds of `batch` samples per GPU (BATCH mode:
+every round evaluates its samples against the tree as it was at the round's start and appends all
+accepted nodes) until the query's wall-clock horizon is spent.  Default workload: config 3 of
+BASELINE.json — 200 static obstacles, 16384 samples per batch per GPU, 2 s horizon.
+
+N > 1: one process per GPU (torch.distributed, RCCL); each round every rank evaluates its own
+`batch` samples (weak scaling), the accepted-node records are all-gathered and every rank appends
+the union in global sample order, so the trees stay identical.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
+
+CONFIGS = {
+    # name: static obstacles, moving obstacles, samples per batch (per GPU), horizon ms
+    "cfg2": dict(obstacles=50, moving=0, batch=4096, horizon_ms=200.0,
+                 desc="cfg2: 50-obstacle static urban scene, 4096 samples/batch, 0.2 s horizon"),
+    "cfg3": dict(obstacles=200, moving=0, batch=16384, horizon_ms=2000.0,
+                 desc="cfg3: 200-obstacle static urban scene, 16384 samples/batch per GPU, 2 s horizon"),
+    "cfg5": dict(obstacles=200, moving=20, batch=16384, horizon_ms=200.0,
+                 desc="cfg5-scene: 200 static + 20 moving obstacles, 16384 samples/batch per GPU, 0.2 s (5 Hz) horizon"),
+}
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP32_VALU_TF = 157.3
+PEAK_FP64_VALU_TF = 78.6
+PEAK_HBM_GBS = 8000.0
+# Algorithmic FLOP per unit: FP64 per simulated step = 160 + 6 per reference
+# point scanned by findClosestPoint; FP32 per OBB box test = 36.
+FLOP_STEP, FLOP_SCAN, FLOP_BOX = 160, 6, 36
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="samples per round per GPU (default: config)")
+    ap.add_argument("--horizon-ms", type=float, default=0.0, help="per-query budget (default: config)")
+    ap.add_argument("--max-nodes", type=int, default=6 << 20)
+    ap.add_argument("--rows-per-node", type=int, default=64)
+    ap.add_argument("--cpu-queries", type=int, default=5, help="oracle queries timed for cpu_baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=1)
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, horizon_ms, n_queries, seed):
+    """The reference-faithful CPU restatement (oracle/, kind 'port'), 1 thread, same scene and
+    horizon: nodes appended per second of wall time, n_queries fresh queries."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from clrrt import abi, scenes
+    from oracle_binding import Oracle
+
+    obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
+    nodes = goals = 0
+    t_total = 0.0
+    for q in range(n_queries):
+        o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+        Oracle.srand(seed + q)
+        o.init_tree()
+        t0 = time.perf_counter()
+        o.expand_budget(horizon_ms, wall=True)
+        t_total += time.perf_counter() - t0
+        n = o.nodes()
+        nodes += len(n["goal"]) - 1
+        goals += int(n["goal"].sum())
+    return {
+        "value": nodes / t_total, "unit": "nodes/s", "cores": 1, "kind": "port",
+        "feasible_paths_per_s": goals / t_total,
+        "sample": f"{n_queries} planMotion queries x {horizon_ms:.0f} ms wall budget, {cfg['obstacles']}+"
+                  f"{cfg['moving']} obstacles, srand({seed}..{seed + n_queries - 1}), 1 thread, {cpu_model()}",
+    }
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    B = args.batch or cfg["batch"]
+    horizon = args.horizon_ms or cfg["horizon_ms"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import clrrt
+    from clrrt import abi, scenes
+
+    obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
+    params = clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
+    max_nodes = args.max_nodes
+    max_rows = max_nodes * args.rows_per_node
+    pl = clrrt.Planner(params, device=local, max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
+                       max_obstacles=max(1, len(obs)))
+    pl.set_obstacles(obs)
+    pl.set_rank(rank)
+    stream = torch.cuda.current_stream()
+    pl.set_stream(stream.cuda_stream)
+
+    rec_bytes = 160
+    if world > 1:
+        out_buf = torch.empty((2 * B, rec_bytes), dtype=torch.uint8, device="cuda")
+        gathered = torch.empty((world, 2 * B, rec_bytes), dtype=torch.uint8, device="cuda")
+        meta = torch.zeros(2, dtype=torch.float64, device="cuda")
+        meta_all = torch.zeros((world, 2), dtype=torch.float64, device="cuda")
+
+    def query(seed):
+        """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""
+        pl.tree_init()
+        rng = clrrt.Rng(seed)
+        if world == 1:
+            st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+            return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
+        nodes = goals = 0
+        cap_stop = 0
+        t0 = time.perf_counter()
+        while True:
+            n_now = pl.size()[0]
+            if n_now + 2 * world * B > max_nodes:
+                cap_stop = 1
+                break
+            allsmp = rng.draw_samples(params, world * B)
+            mine = (abi.Sample * B).from_buffer(allsmp, rank * B * C_SAMPLE)
+            n_local = pl.round_eval(mine, out_buf.data_ptr())
+            meta[0] = float(n_local)
+            meta[1] = (time.perf_counter() - t0) * 1e3
+            dist.all_gather_into_tensor(meta_all.view(-1), meta)
+            dist.all_gather_into_tensor(gathered.view(-1), out_buf.view(-1))
+            counts = meta_all[:, 0].to(torch.int64).tolist()
+            parts = [gathered[r, :counts[r]] for r in range(world)]
+            cat = torch.cat(parts, 0).contiguous()
+            total = cat.shape[0]
+            first = sum(counts[:rank])
+            pl.round_commit(cat.data_ptr(), total, first, counts[rank])
+            nodes += total
+            goals += int(cat[:, 140:144].contiguous().view(torch.int32).sum().item()) if total else 0
+            if float(meta_all[:, 1].max().item()) >= horizon:
+                break
+        return nodes, goals, cap_stop
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for w in range(args.warmup):
+        query(args.seed + 1000 + w)
+    pl.enable_timing(True)
+    pl.reset_counters()
+    barrier_sync()
+    t0 = time.perf_counter()
+    tot_nodes = tot_goals = cap_stops = 0
+    for k in range(args.steps):
+        n, g, c = query(args.seed + k)
+        tot_nodes += n
+        tot_goals += g
+        cap_stops += c
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roll_ms, roll_n = pl.kernel_time(1)
+    nn_ms, nn_n = pl.kernel_time(0)
+    other_ms, other_n = pl.kernel_time(2)
+    work = pl.work_counters()
+    cnt = pl.counters()
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    fp64 = FLOP_STEP * work["steps"] + FLOP_SCAN * work["scan_points"]
+    fp32 = FLOP_BOX * work["box_tests"]
+    achieved_tf = (fp64 + fp32) / (roll_ms * 1e-3) / 1e12 if roll_ms > 0 else 0.0
+    t_mix = fp64 / PEAK_FP64_VALU_TF + fp32 / PEAK_FP32_VALU_TF
+    peak_tf = (fp64 + fp32) / t_mix if t_mix > 0 else PEAK_FP32_VALU_TF
+    value = tot_nodes / elapsed
+    line = {
+        "metric": "nodes expanded/sec (200-obstacle scene)",
+        "value": value,
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "feasible_paths_per_s": tot_goals / elapsed,
+        "config": {
+            "workload": cfg["desc"],
+            "samples_per_batch": B,
+            "obstacles": cfg["obstacles"] + cfg["moving"],
+            "horizon_ms": horizon,
+            "mode": "BATCH",
+            "parallelism": f"dp{world}",
+            "capacity_stops": cap_stops,
+        },
+        "roofline": {
+            "bound": "valu",
+            "kernel": "k_rollout (speculative candidates + goal-bias + row replay)",
+            "achieved": achieved_tf,
+            "peak": peak_tf,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / peak_tf if peak_tf else 0.0,
+            "traffic": None,
+            "launches": roll_n,
+            "avg_launch_ms": roll_ms / roll_n if roll_n else 0.0,
+            "flop_per_launch": (fp64 + fp32) / roll_n if roll_n else 0.0,
+            "fp64_flop": fp64,
+            "fp32_flop": fp32,
+            "peak_note": "mix-weighted VALU peak: FP64 78.6 TF/s, FP32 157.3 TF/s (MI355X_MICROARCH.md)",
+        },
+        "kernel_ms": {"rollout": roll_ms, "nn": nn_ms, "select_commit": other_ms,
+                      "launches": {"rollout": roll_n, "nn": nn_n, "other": other_n}},
+        "work": {**work, **cnt},
+    }
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(cfg, horizon, args.cpu_queries, args.seed)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+C_SAMPLE = 24
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,7 @@ _SIGS = {
     "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, P(C.c_int32), P(C.c_float)]),
     "clrrt_get_counters": (C.c_int, [C.c_void_p, P(abi.Counters)]),
     "clrrt_reset_counters": (C.c_int, [C.c_void_p]),
+    "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_kernel_time": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_int64)]),
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
 }
@@ -65,6 +66,12 @@ def lib():
     """Load libclrrt.so (raises loudly when it has not been built)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: when PyTorch is present its bundled libamdhip64.so.7 must be
+        # the one loaded (same soname), so import it before libclrrt pulls /opt/rocm's copy in.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ClrrtError(f"libclrrt.so not built at {LIB_PATH}: run `make -C cl-rrt_amd/csrc` "
                              "(or __graft_entry__.build())")
@@ -269,6 +276,11 @@ class Planner:
         c = abi.Counters()
         self._chk(self.L.clrrt_get_counters(self.h, C.byref(c)), "get_counters")
         return {k: getattr(c, k) for k, _ in abi.Counters._fields_}
+
+    def work_counters(self):
+        out = (C.c_int64 * 3)()
+        self._chk(self.L.clrrt_work_counters(self.h, out), "work_counters")
+        return {"steps": out[0], "scan_points": out[1], "box_tests": out[2]}
 
     def reset_counters(self):
         self._chk(self.L.clrrt_reset_counters(self.h), "reset_counters")

@@ -61,7 +61,8 @@ class Counters(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("iterations", C.c_int64), ("nodes_added", C.c_int64), ("goal_nodes_added", C.c_int64),
-                ("rounds", C.c_int64), ("speculated", C.c_int64), ("elapsed_ms", C.c_double)]
+                ("rounds", C.c_int64), ("speculated", C.c_int64), ("elapsed_ms", C.c_double),
+                ("capacity_stop", C.c_int64)]
 
 
 class Capacity(C.Structure):

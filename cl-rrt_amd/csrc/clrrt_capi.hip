@@ -30,6 +30,7 @@
 using namespace clrrt;
 
 #define CAND_K 10
+#define NN_K 11
 
 struct DevBuf {
   void* p = nullptr;
@@ -61,6 +62,9 @@ struct clrrt_ctx {
   int* cand = nullptr;
   float* ckey = nullptr;
   int* ncand = nullptr;
+  int* ctie = nullptr;
+  KeyId* sort_scratch = nullptr;
+  int64_t sort_cap = 0;  // KeyId entries
   RollRes* res_spec = nullptr;
   clrrt_node* regnodes = nullptr;
   int* gbflag = nullptr;
@@ -72,12 +76,14 @@ struct clrrt_ctx {
   Job* jobs = nullptr;
   RollRes* res_replay = nullptr;
   int64_t* totals = nullptr;
+  unsigned long long* work_ctr = nullptr;  // [3] algorithmic rollout work
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
   int* h_int = nullptr;
   // last round_eval bookkeeping
   int64_t last_eval_rows = 0;
+  int64_t last_goal_nodes = 0;
   // counters
   clrrt_counters counters{};
   // timing
@@ -273,8 +279,8 @@ const char* clrrt_last_error(const clrrt_ctx* c) { return c ? c->err.c_str() : "
 
 static void free_all(clrrt_ctx* c) {
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
-                  c->res_spec, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so, c->first_conflict,
-                  c->out_nodes, c->jobs, c->res_replay, c->totals};
+                  c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so, c->first_conflict,
+                  c->out_nodes, c->jobs, c->res_replay, c->totals, c->work_ctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -318,12 +324,13 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->arena, (size_t)c->cap.max_rows * 10));
   chk(dalloc(&c->obs, std::max<int64_t>(1, c->cap.max_obstacles)));
   chk(dalloc(&c->d_samples, B));
-  c->partial_cap = std::max<int64_t>(B * 16, 4096) * CAND_K;
+  c->partial_cap = std::max<int64_t>(B * 16, 4096) * NN_K;
   chk(dalloc(&c->pk, c->partial_cap));
   chk(dalloc(&c->pi, c->partial_cap));
   chk(dalloc(&c->cand, B * CAND_K));
   chk(dalloc(&c->ckey, B * CAND_K));
   chk(dalloc(&c->ncand, B));
+  chk(dalloc(&c->ctie, B));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->gbflag, B));
@@ -335,6 +342,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->jobs, 2 * B));
   chk(dalloc(&c->res_replay, 2 * B));
   chk(dalloc(&c->totals, 8));
+  chk(dalloc(&c->work_ctr, 4));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 4 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
@@ -495,6 +504,19 @@ int clrrt_get_counters(clrrt_ctx* c, clrrt_counters* out) {
 int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_work_counters(clrrt_ctx* c, int64_t out[3]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  unsigned long long h[4];
+  HIPC(c, hipMemcpyAsync(h, c->work_ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < 3; i++) out[i] = (int64_t)h[i];
   return CLRRT_OK;
 }
 
@@ -529,19 +551,38 @@ static RollArgs roll_args(clrrt_ctx* c, int njobs) {
   a.jobs = c->jobs;
   a.obs = c->obs;
   a.arena = c->arena;
+  a.ctr = c->work_ctr;
   a.njobs = njobs;
   return a;
+}
+
+static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
+  if (entries <= c->sort_cap) return CLRRT_OK;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->sort_scratch) HIPC(c, hipFree(c->sort_scratch));
+  c->sort_scratch = nullptr;
+  c->sort_cap = 0;
+  int64_t want = std::max<int64_t>(entries, 1 << 20);
+  HIPC(c, hipMalloc((void**)&c->sort_scratch, sizeof(KeyId) * want));
+  c->sort_cap = want;
+  return CLRRT_OK;
 }
 
 // Stages 1-4 (+5 in EXACT mode) for n samples already in c->d_samples.  Returns the number of
 // samples to commit (n in BATCH mode).
 static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
   hipStream_t st = c->stream;
+  KeyId* scratch = nullptr;
+  if (exact) {
+    int rc = ensure_sort_scratch(c, (int64_t)n * c->n_nodes);
+    if (rc != CLRRT_OK) return rc;
+    scratch = c->sort_scratch;
+  }
   {
     KTimer kt(c, 0);
-    int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * CAND_K));
+    int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
     HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                      c->ncand, max_chunks));
+                      c->ncand, c->ctie, max_chunks, scratch));
   }
   {
     KTimer kt(c, 1);
@@ -591,7 +632,7 @@ static int compact_and_replay(clrrt_ctx* c, int L, int* n_out) {
     HIPC(c, launch_compact(st, L, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
                            c->out_nodes, c->jobs, c->totals));
   }
-  HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 7, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
@@ -600,6 +641,7 @@ static int compact_and_replay(clrrt_ctx* c, int L, int* n_out) {
   c->counters.fail_acclimit += c->h_totals[4];
   c->counters.fail_iterlimit += c->h_totals[5];
   c->counters.rollouts += c->h_totals[6];
+  c->last_goal_nodes = c->h_totals[7];
   {
     KTimer kt(c, 1);
     RollArgs a = roll_args(c, (int)nn);
@@ -679,6 +721,13 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     }
     int nb = cur;
     if (n_iters > 0) nb = (int)std::min<int64_t>(nb, n_iters - st.iterations);
+    // a round appends at most 2 nodes and 2 full-horizon trajectories per sample
+    if (c->n_nodes + 2 * (int64_t)nb > c->cap.max_nodes ||
+        c->n_rows + 2 * (int64_t)nb * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+      if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
+      st.capacity_stop = 1;
+      break;
+    }
     while ((int)pending.size() < nb) {
       clrrt_sample smp;
       clrrt_draw_samples(&c->params, &work, 1, &smp);
@@ -695,6 +744,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
       for (int k = 0; k < 3; k++) clrrt_rng_next(&committed);
     }
     st.iterations += L;
+    st.goal_nodes_added += c->last_goal_nodes;
     st.speculated += nb;
     st.rounds++;
     if (exact) cur = std::max(8, std::min(batch, L == nb ? 2 * nb : 2 * L));
@@ -767,11 +817,13 @@ int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t
   if (n == 0) return CLRRT_OK;
   memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
   HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
-  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * CAND_K));
+  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
+  int rc = ensure_sort_scratch(c, (int64_t)n * c->n_nodes);
+  if (rc != CLRRT_OK) return rc;
   {
     KTimer kt(c, 0);
     HIPC(c, launch_nn(c->stream, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                      c->ncand, max_chunks));
+                      c->ncand, c->ctie, max_chunks, c->sort_scratch));
   }
   HIPC(c, hipMemcpyAsync(out_ids, c->cand, sizeof(int) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));
   if (out_keys)

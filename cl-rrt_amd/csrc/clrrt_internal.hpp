@@ -5,6 +5,7 @@
 
 #include "../../include/clrrt.h"
 #include "clrrt_dev.hpp"
+#include "clrrt_stdsort.hpp"
 
 namespace clrrt {
 
@@ -19,6 +20,12 @@ struct RollRes {
   int32_t nrows;       // stateArray.size()
   int32_t refN;
   int32_t pad;
+};
+
+// Algorithmic work of rollouts (SURVEY §8(d) roofline basis): simulated steps, reference points
+// scanned by findClosestPoint, OBB box tests.
+struct WorkCtr {
+  uint32_t steps, scan, box;
 };
 
 // Explicit rollout job (parity entry, row replay).
@@ -57,6 +64,7 @@ struct RollArgs {
   const BakedObs* __restrict__ obs;
   double* __restrict__ arena;              // rows destination (LIST with row_off >= 0)
   RollRes* __restrict__ res;
+  unsigned long long* ctr;  // [3] steps, scan points, box tests (nullable)
   int njobs;
 };
 
@@ -73,8 +81,11 @@ struct SelArgs {
   int B;
 };
 
+// Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
+// selection involves equal keys are re-sorted with the replay of std::sort.
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                     const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int max_chunks);
+                     const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
+                     int max_chunks, KeyId* exact_scratch);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const int* gbflag,

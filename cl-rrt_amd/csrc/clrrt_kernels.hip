@@ -17,10 +17,12 @@
 
 #include "clrrt_dev.hpp"
 #include "clrrt_internal.hpp"
+#include "clrrt_stdsort.hpp"
 
 namespace clrrt {
 
 #define CAND_K 10
+#define NN_K (CAND_K + 1)  // one extra entry reveals a key tie at the selection boundary
 static_assert(CAND_K == 10, "sortLimit");
 
 // --------------------------------------------------------------------------------------------
@@ -31,9 +33,9 @@ __device__ __forceinline__ bool lex_less(float ka, int ia, float kb, int ib) {
 }
 
 // Insert (k, i) into the ascending register list (static indices only: stays in VGPRs).
-__device__ __forceinline__ void topk_insert(float (&keys)[CAND_K], int (&ids)[CAND_K], float k, int i) {
+__device__ __forceinline__ void topk_insert(float (&keys)[NN_K], int (&ids)[NN_K], float k, int i) {
 #pragma unroll
-  for (int j = 0; j < CAND_K; j++) {
+  for (int j = 0; j < NN_K; j++) {
     bool sw = lex_less(k, i, keys[j], ids[j]);
     float tk = keys[j];
     int ti = ids[j];
@@ -56,58 +58,98 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   double sx = 0, sy = 0;
   int ex = 1;
   if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
-  float keys[CAND_K];
-  int ids[CAND_K];
+  float keys[NN_K];
+  int ids[NN_K];
 #pragma unroll
-  for (int j = 0; j < CAND_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
   for (int n = n0; n < n1; n++) {
     const NnRec rec = nodes[n];
     float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
     float lb = sqrtf(qx * qx + qy * qy) * 0.99999f - 1e-4f;
     if (!ex) lb = rec.costE + lb;
-    if (act && lb <= keys[CAND_K - 1]) {
+    if (act && lb <= keys[NN_K - 1]) {
       float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
       if (!ex) k = rec.costE + k;
-      if (lex_less(k, n, keys[CAND_K - 1], ids[CAND_K - 1]) &&
+      if (lex_less(k, n, keys[NN_K - 1], ids[NN_K - 1]) &&
           feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
         topk_insert(keys, ids, k, n);
     }
   }
   if (act) {
-    size_t base = ((size_t)s * nchunks + c) * CAND_K;
+    size_t base = ((size_t)s * nchunks + c) * NN_K;
 #pragma unroll
-    for (int j = 0; j < CAND_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
+    for (int j = 0; j < NN_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
   }
 }
 
 __global__ void k_nn_merge(int B, int nchunks, int limit, const float* __restrict__ pk,
                            const int* __restrict__ pi, int* __restrict__ cand, float* __restrict__ ckey,
-                           int* __restrict__ ncand) {
+                           int* __restrict__ ncand, int* __restrict__ ctie) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= B) return;
-  float keys[CAND_K];
-  int ids[CAND_K];
+  float keys[NN_K];
+  int ids[NN_K];
 #pragma unroll
-  for (int j = 0; j < CAND_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
   for (int c = 0; c < nchunks; c++) {
-    size_t base = ((size_t)s * nchunks + c) * CAND_K;
-    for (int j = 0; j < CAND_K; j++) {
+    size_t base = ((size_t)s * nchunks + c) * NN_K;
+    for (int j = 0; j < NN_K; j++) {
       int id = pi[base + j];
       if (id == 0x7fffffff) break;
       float k = pk[base + j];
-      if (lex_less(k, id, keys[CAND_K - 1], ids[CAND_K - 1])) topk_insert(keys, ids, k, id);
+      if (lex_less(k, id, keys[NN_K - 1], ids[NN_K - 1])) topk_insert(keys, ids, k, id);
       else break;  // chunk lists are sorted
     }
   }
-  int n = 0;
+  int n = 0, valid = 0;
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) valid += ids[j] != 0x7fffffff;
+  const int sel = min(limit, valid);
+  int tie = 0;
 #pragma unroll
   for (int j = 0; j < CAND_K; j++) {
-    bool v = ids[j] != 0x7fffffff && j < limit;
+    bool v = j < sel;
     cand[s * CAND_K + j] = v ? ids[j] : -1;
     ckey[s * CAND_K + j] = keys[j];
     n += v;
+    // equal keys among the selected entries or across the selection boundary: the order std::sort
+    // gives them is algorithm-defined (EXACT mode replays it in k_nn_exact)
+    tie |= (j < sel && j + 1 < valid && keys[j] == keys[j + 1]);
   }
   ncand[s] = n;
+  ctie[s] = tie;
+}
+
+// EXACT mode, samples whose candidate selection involves equal keys: rebuild the full (id, key)
+// sequence in node order and replay libstdc++'s std::sort on it (one lane per sample), then walk it
+// exactly as sortNodesExplore/Optimize do (rrtplanner.cpp:237-243).
+__global__ void k_nn_exact(const clrrt_sample* __restrict__ S, int B, const NnRec* __restrict__ nodes, int N,
+                           DevParams p, const int* __restrict__ ctie, KeyId* __restrict__ scratch,
+                           int* __restrict__ cand, float* __restrict__ ckey, int* __restrict__ ncand) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B || !ctie[s]) return;
+  const double sx = S[s].x, sy = S[s].y;
+  const int ex = S[s].explore;
+  KeyId* a = scratch + (size_t)s * N;
+  for (int n = 0; n < N; n++) {
+    const NnRec& rec = nodes[n];
+    float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+    if (!ex) k = rec.costE + k;
+    a[n].id = n;
+    a[n].key = k;
+  }
+  std_sort(a, N);
+  int cnt = 0;
+  for (int i = 0; i < N && cnt < p.sort_limit; i++) {
+    const NnRec& rec = nodes[a[i].id];
+    if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
+      cand[s * CAND_K + cnt] = a[i].id;
+      ckey[s * CAND_K + cnt] = a[i].key;
+      cnt++;
+    }
+  }
+  for (int j = cnt; j < CAND_K; j++) cand[s * CAND_K + j] = -1;
+  ncand[s] = cnt;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -125,7 +167,8 @@ struct ObsView {
 
 // checkObsDistance (stub collisioncheck.cpp:6-8 | OBB old_collisioncheck.cpp:24-51).
 template <bool NEED_GAP>
-__device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p, const ObsView& ov) {
+__device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p, const ObsView& ov,
+                                               uint32_t& tests) {
   if (p.coll_mode == CLRRT_COLLISION_STUB) return 100.0;
   const double t = p.obs_use_pred ? r.x6 : 0.0;
   const double vpx = r.x0 + 1.424 * r.c2, vpy = r.x1 + 1.424 * r.s2;
@@ -152,9 +195,10 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
       D = sat_gap(veh, bvx, bvy, bnx, bny);
     }
-    if (D == 0) return 0.0;
+    if (D == 0) { tests += j + 1; return 0.0; }
     if (NEED_GAP && (double)D < best) best = D;
   }
+  tests += ov.n;  // the reference tests every obstacle until the first overlap
   return best;
 }
 
@@ -162,9 +206,10 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
 // 7..9 and returns CLRRT_ROLL_* or -1 to continue.
 template <bool NEED_GAP>
 __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
-                                         double& col8, double& col9) {
+                                         double& col8, double& col9, WorkCtr& w) {
   double Px, Py;
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
+  w.scan += (uint32_t)(r.R.N - r.wp);
   double dla = update_waypoint(r, p, Px, Py, false);
   double ym = lateral_error(r, Px, Py);
   double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
@@ -198,7 +243,7 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   col8 = prof_v(r.P, r.wp + 2);
   col9 = dc;
   // collision (simulation.cpp:83-86)
-  double Dobs = obs_distance<NEED_GAP>(r, p, ov);
+  double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);
   if (Dobs == 0) return CLRRT_ROLL_COLLISION;
   // costs (simulation.cpp:89-95)
   r.costE += r.x4 * p.dt;
@@ -231,7 +276,7 @@ __device__ __forceinline__ void store_row(double* __restrict__ row, const Roll& 
 template <bool NEED_GAP>
 __device__ void run_rollout(const double* ps, double pbx, double pby, double pvb, int gb, double sx,
                             double sy, const DevParams& p, const ObsView& ov, double* __restrict__ rows,
-                            RollRes& out) {
+                            RollRes& out, WorkCtr& w) {
   RefD R = gb ? make_goal_ref(pbx, pby, p) : make_ref(pbx, pby, sx, sy, p);
   Roll r;
   roll_init(r, ps, R, pvb, gb != 0, p);
@@ -244,7 +289,7 @@ __device__ void run_rollout(const double* ps, double pbx, double pby, double pvb
   int steps = 0;
   for (int i = 0; i < p.n_steps_max; i++) {
     steps++;
-    int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9);
+    int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9, w);
     if (rows) store_row(rows + (size_t)steps * 10, r, c7, c8, c9);
     if (o >= 0) { outcome = o; break; }
   }
@@ -258,6 +303,7 @@ __device__ void run_rollout(const double* ps, double pbx, double pby, double pvb
   out.outcome = outcome;
   out.nrows = steps + 1;
   out.refN = r.R.N;
+  w.steps += (uint32_t)steps;
 }
 
 
@@ -277,33 +323,58 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
   }
   ObsView ov{a.obs, cv, rad, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0};
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.njobs) return;
-  const double* ps;
-  double pbx, pby, pvb, sx = 0, sy = 0;
+  WorkCtr w{0, 0, 0};
+  bool act = j < a.njobs;
+  const double* ps = nullptr;
+  double pbx = 0, pby = 0, pvb = 0, sx = 0, sy = 0;
   int gb = 0;
   double* rows = nullptr;
-  if (SRC == SRC_SPEC) {
-    int s = j / CAND_K;
-    int id = a.cand[j];
-    if (id < 0) { a.res[j].outcome = -1; return; }
-    const clrrt_node& n = a.tree[id];
-    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
-    sx = a.samples[s].x; sy = a.samples[s].y;
-  } else if (SRC == SRC_GB) {
-    if (!a.gbflag[j]) { a.res[j].outcome = -1; return; }
-    const clrrt_node& n = a.regnodes[j];
-    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
-    gb = 1;
-  } else {
-    const Job& jb = a.jobs[j];
-    const clrrt_node& n = jb.from_reg ? a.regnodes[jb.parent] : a.tree[jb.parent];
-    ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
-    gb = jb.gb; sx = jb.sx; sy = jb.sy;
-    if (jb.row_off >= 0) rows = a.arena + (size_t)jb.row_off * 10;
+  if (act) {
+    if (SRC == SRC_SPEC) {
+      int s = j / CAND_K;
+      int id = a.cand[j];
+      if (id < 0) {
+        a.res[j].outcome = -1;
+        act = false;
+      } else {
+        const clrrt_node& n = a.tree[id];
+        ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+        sx = a.samples[s].x; sy = a.samples[s].y;
+      }
+    } else if (SRC == SRC_GB) {
+      if (!a.gbflag[j]) {
+        a.res[j].outcome = -1;
+        act = false;
+      } else {
+        const clrrt_node& n = a.regnodes[j];
+        ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+        gb = 1;
+      }
+    } else {
+      const Job& jb = a.jobs[j];
+      const clrrt_node& n = jb.from_reg ? a.regnodes[jb.parent] : a.tree[jb.parent];
+      ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+      gb = jb.gb; sx = jb.sx; sy = jb.sy;
+      if (jb.row_off >= 0) rows = a.arena + (size_t)jb.row_off * 10;
+    }
   }
-  RollRes out;
-  run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, out);
-  a.res[j] = out;
+  if (act) {
+    RollRes out;
+    run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, out, w);
+    a.res[j] = out;
+  }
+  if (a.ctr) {  // algorithmic work counters (roofline): block reduction, one atomic per block
+    __shared__ __attribute__((aligned(16))) unsigned long long s_ctr[4];
+    if (threadIdx.x < 3) s_ctr[threadIdx.x] = 0;
+    __syncthreads();
+    if (w.steps) {
+      atomicAdd(&s_ctr[0], (unsigned long long)w.steps);
+      atomicAdd(&s_ctr[1], (unsigned long long)w.scan);
+      atomicAdd(&s_ctr[2], (unsigned long long)w.box);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -440,11 +511,11 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
   const int per = (L + blockDim.x - 1) / blockDim.x;
   const int b0 = min(L, t * per), b1 = min(L, b0 + per);
   int64_t nn = 0, nr = 0;
-  int64_t cnt[5] = {0, 0, 0, 0, 0};
+  int64_t cnt[6] = {0, 0, 0, 0, 0, 0};
   for (int s = b0; s < b1; s++) {
     const SampleOut& o = so[s];
-    if (o.k >= 0) { nn++; nr += o.nrows_reg; }
-    if (o.gb_ok) { nn++; nr += o.nrows_gb; }
+    if (o.k >= 0) { nn++; nr += o.nrows_reg; cnt[5] += regnodes[s].goal; }
+    if (o.gb_ok) { nn++; nr += o.nrows_gb; cnt[5] += gbnodes[s].goal; }
     cnt[0] += o.steps; cnt[1] += o.f_col; cnt[2] += o.f_acc; cnt[3] += o.f_it; cnt[4] += o.rollouts;
   }
   s_nodes[t] = nn;
@@ -459,7 +530,7 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
     s_rows[t] += vr;
     __syncthreads();
   }
-  for (int c = 0; c < 5; c++) atomicAdd((unsigned long long*)&s_cnt[c], (unsigned long long)cnt[c]);
+  for (int c = 0; c < 6; c++) atomicAdd((unsigned long long*)&s_cnt[c], (unsigned long long)cnt[c]);
   int64_t node_off = s_nodes[t] - nn, row_off = s_rows[t] - nr;
   for (int s = b0; s < b1; s++) {
     const SampleOut& o = so[s];
@@ -495,7 +566,7 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
     totals[0] = s_nodes[t];
     totals[1] = s_rows[t];
   }
-  if (t < 5) totals[2 + t] = s_cnt[t];
+  if (t < 6) totals[2 + t] = s_cnt[t];
 }
 
 // RRT.addNode for n records: resolve GB parents (CLRRT_PARENT_PREV -> the record before) and build
@@ -555,8 +626,8 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   } while (0)
 
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                     const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
-                     int max_chunks) {
+                     const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
+                     int max_chunks, KeyId* exact_scratch) {
   int groups = (B + 255) / 256;
   int nchunks = (N + 255) / 256;
   int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
@@ -567,8 +638,13 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
                      p, pk, pi);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
-                     cand, ckey, ncand);
+                     cand, ckey, ncand, ctie);
   LAUNCH_CHECK();
+  if (exact_scratch) {
+    hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, exact_scratch,
+                       cand, ckey, ncand);
+    LAUNCH_CHECK();
+  }
   return hipSuccess;
 }
 

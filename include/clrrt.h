@@ -159,6 +159,7 @@ typedef struct clrrt_stats {
   int64_t rounds;
   int64_t speculated;   /* samples evaluated (>= iterations in EXACT mode) */
   double elapsed_ms;
+  int64_t capacity_stop; /* 1 when the loop ended because the next round could overflow capacity */
 } clrrt_stats;
 
 typedef struct clrrt_capacity {
@@ -240,6 +241,10 @@ int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32
 
 int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);
 int clrrt_reset_counters(clrrt_ctx* ctx);
+/* Algorithmic work done by rollout kernels since the last reset (SURVEY §8(d) roofline basis):
+ * out[0] = simulated steps (incl. speculative candidates and row replays), out[1] = reference
+ * points scanned by findClosestPoint, out[2] = OBB box tests (first overlap ends a step's scan). */
+int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 
 /* Launch-time profile of the last clrrt_expand / round call: device milliseconds per kernel
  * family measured with HIP events on the context stream.  which: 0 = nn, 1 = rollout,

@@ -447,15 +447,18 @@ static bool feasible_node(Oracle& o, const Node& n, const Pt& s) {  // :271-289
 }
 
 // sortNodesExplore :227-247 / sortNodesOptimize :250-268 over the first `upto` nodes
+// stable = true: ties ordered by node id (std::stable_sort) -- the BATCH-mode semantics of the GPU
+// engine; stable = false: std::sort exactly as the reference.
 static vector<int> sort_nodes(Oracle& o, const Pt& s, bool explore, size_t upto,
-                              vector<float>* keys_out = nullptr) {
+                              vector<float>* keys_out = nullptr, bool stable = false) {
   vector<std::pair<int, float>> dv;
   for (size_t i = 0; i != upto; i++) {
     float k = explore ? dubins(s, o.tree[i], 1) : o.tree[i].costE + dubins(s, o.tree[i], 1);
     dv.push_back(std::make_pair((int)i, k));
   }
-  std::sort(dv.begin(), dv.end(),
-            [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; });
+  auto by_key = [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; };
+  if (stable) std::stable_sort(dv.begin(), dv.end(), by_key);
+  else std::sort(dv.begin(), dv.end(), by_key);
   vector<int> out;
   for (auto it = dv.begin(); it != dv.end(); ++it) {
     if (feasible_node(o, o.tree[it->first], s)) {
@@ -493,9 +496,9 @@ struct IterResult {
   Node node, gb_node;
 };
 
-static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_t upto) {
+static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_t upto, bool stable = false) {
   IterResult res;
-  vector<int> cand = sort_nodes(o, s, explore, upto);
+  vector<int> cand = sort_nodes(o, s, explore, upto, nullptr, stable);
   for (int id : cand) {
     Ref r = get_reference(o, s, o.tree[id], 1);
     Sim sim = simulate(o, o.tree[id].state, r, false, o.tree[id].ref.v.back());
@@ -620,8 +623,9 @@ long orc_expand_budget(void* h, double budget_ms, int clock_kind) {
 }
 
 // BATCH mode restatement: rounds of B iterations; every sample of a round sees only the tree
-// as it was at the start of the round; results are appended in sample order.
-void orc_expand_batch(void* h, long n_iters, int B) {
+// as it was at the start of the round; results are appended in sample order; equal keys are
+// ordered by node id (stable = 1, the GPU engine's BATCH semantics) or as std::sort (stable = 0).
+void orc_expand_batch(void* h, long n_iters, int B, int stable) {
   Oracle* o = (Oracle*)h;
   long done = 0;
   while (done < n_iters) {
@@ -635,7 +639,7 @@ void orc_expand_batch(void* h, long n_iters, int B) {
     }
     size_t upto = o->tree.size();
     std::vector<IterResult> rs(nb);
-    for (int j = 0; j < nb; j++) rs[j] = evaluate_iteration(*o, ss[j], ex[j], upto);
+    for (int j = 0; j < nb; j++) rs[j] = evaluate_iteration(*o, ss[j], ex[j], upto, stable != 0);
     for (int j = 0; j < nb; j++) append_result(*o, rs[j]);
     done += nb;
   }
@@ -740,11 +744,11 @@ int orc_feasible_goal_bias(void* h, long node) {
 }
 
 // Candidate list of the nearest-node search (ids + keys), count returned.
-int orc_sort_nodes(void* h, double sx, double sy, int explore, int* ids, float* keys) {
+int orc_sort_nodes(void* h, double sx, double sy, int explore, int stable, int* ids, float* keys) {
   Oracle* o = (Oracle*)h;
   Pt s; s.x = sx; s.y = sy;
   std::vector<float> k;
-  std::vector<int> c = sort_nodes(*o, s, explore != 0, o->tree.size(), &k);
+  std::vector<int> c = sort_nodes(*o, s, explore != 0, o->tree.size(), &k, stable != 0);
   for (size_t i = 0; i < c.size(); i++) { ids[i] = c[i]; keys[i] = k[i]; }
   return (int)c.size();
 }
@@ -781,10 +785,10 @@ void orc_draw_samples(void* h, int n, double* xy, int* explore) {
 
 // Evaluate one iteration for a given sample against the whole tree without appending.
 // Returns the number of nodes it would append (0..2); fills headers (parent of the GB node = -2).
-int orc_eval_iteration(void* h, double sx, double sy, int explore, clrrt_node* out2) {
+int orc_eval_iteration(void* h, double sx, double sy, int explore, int stable, clrrt_node* out2) {
   Oracle* o = (Oracle*)h;
   Pt s; s.x = sx; s.y = sy;
-  IterResult r = evaluate_iteration(*o, s, explore != 0, o->tree.size());
+  IterResult r = evaluate_iteration(*o, s, explore != 0, o->tree.size(), stable != 0);
   int n = 0;
   Oracle tmp;
   if (r.added) { tmp.tree.push_back(r.node); n++; }

@@ -34,7 +34,7 @@ def lib():
             "orc_init_tree": (None, [vp, P(d)]),
             "orc_expand": (None, [vp, l]),
             "orc_expand_budget": (l, [vp, d, i]),
-            "orc_expand_batch": (None, [vp, l, i]),
+            "orc_expand_batch": (None, [vp, l, i, i]),
             "orc_tree_size": (l, [vp]),
             "orc_get_nodes": (None, [vp, l, l, P(abi.Node)]),
             "orc_node_ref_len": (l, [vp, l]),
@@ -45,12 +45,12 @@ def lib():
             "orc_load_tree": (None, [vp, P(abi.Node), l]),
             "orc_simulate": (i, [vp, i, i, d, d, P(i), P(d), P(d), P(d), P(i), P(d), i]),
             "orc_feasible_goal_bias": (i, [vp, l]),
-            "orc_sort_nodes": (i, [vp, d, d, i, P(i), P(f)]),
+            "orc_sort_nodes": (i, [vp, d, d, i, i, P(i), P(f)]),
             "orc_dubins": (f, [vp, d, d, l]),
             "orc_obb_dist": (d, [d, d, f, f, f, d, d, f, f, f]),
             "orc_check_obs": (d, [vp, P(d)]),
             "orc_draw_samples": (None, [vp, i, P(d), P(i)]),
-            "orc_eval_iteration": (i, [vp, d, d, i, P(abi.Node)]),
+            "orc_eval_iteration": (i, [vp, d, d, i, i, P(abi.Node)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -113,8 +113,8 @@ class Oracle:
     def expand(self, n):
         self.L.orc_expand(self.h, n)
 
-    def expand_batch(self, n, batch):
-        self.L.orc_expand_batch(self.h, n, batch)
+    def expand_batch(self, n, batch, stable=True):
+        self.L.orc_expand_batch(self.h, n, batch, 1 if stable else 0)
 
     def expand_budget(self, ms, wall=True):
         return self.L.orc_expand_budget(self.h, ms, 1 if wall else 0)
@@ -167,10 +167,10 @@ class Oracle:
             out["rows"] = buf[:nr].copy()
         return out
 
-    def sort_nodes(self, sx, sy, explore):
+    def sort_nodes(self, sx, sy, explore, stable=False):
         ids = (C.c_int * 64)()
         keys = (C.c_float * 64)()
-        n = self.L.orc_sort_nodes(self.h, sx, sy, 1 if explore else 0, ids, keys)
+        n = self.L.orc_sort_nodes(self.h, sx, sy, 1 if explore else 0, 1 if stable else 0, ids, keys)
         return list(ids[:n]), list(keys[:n])
 
     def dubins(self, sx, sy, node):
@@ -189,9 +189,9 @@ class Oracle:
         self.L.orc_draw_samples(self.h, n, _dp(xy), ex)
         return xy.reshape(n, 2), np.array(list(ex), dtype=np.int32)
 
-    def eval_iteration(self, sx, sy, explore):
+    def eval_iteration(self, sx, sy, explore, stable=False):
         out = (abi.Node * 2)()
-        n = self.L.orc_eval_iteration(self.h, sx, sy, 1 if explore else 0, out)
+        n = self.L.orc_eval_iteration(self.h, sx, sy, 1 if explore else 0, 1 if stable else 0, out)
         return [out[i] for i in range(n)]
 
 

@@ -88,7 +88,7 @@ def test_batch_mode_b1_equals_sequential():
     obs = scenes.urban_scene(50)
     a, b = Oracle(p, obs), Oracle(p, obs)
     Oracle.srand(5); a.init_tree(); a.expand(60)
-    Oracle.srand(5); b.init_tree(); b.expand_batch(60, 1)
+    Oracle.srand(5); b.init_tree(); b.expand_batch(60, 1, stable=False)
     na, nb = a.nodes(), b.nodes()
     assert a.size() == b.size()
     assert np.array_equal(na["state"], nb["state"]) and np.array_equal(na["parent"], nb["parent"])
