@@ -50,6 +50,8 @@ _SIGS = {
     "clrrt_rollout_batch": (C.c_int, [C.c_void_p, P(abi.RolloutJob), C.c_int32, P(abi.RolloutResult),
                                       P(C.c_double), C.c_int32]),
     "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, P(C.c_int32), P(C.c_float)]),
+    "clrrt_selftest_math": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double), C.c_int32,
+                                      P(C.c_double)]),
     "clrrt_get_counters": (C.c_int, [C.c_void_p, P(abi.Counters)]),
     "clrrt_reset_counters": (C.c_int, [C.c_void_p]),
     "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
@@ -276,6 +278,15 @@ class Planner:
         c = abi.Counters()
         self._chk(self.L.clrrt_get_counters(self.h, C.byref(c)), "get_counters")
         return {k: getattr(c, k) for k, _ in abi.Counters._fields_}
+
+    def selftest_math(self, fn, a, b=None):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        b = np.zeros_like(a) if b is None else np.ascontiguousarray(b, dtype=np.float64)
+        out = np.zeros_like(a)
+        self._chk(self.L.clrrt_selftest_math(self.h, fn, a.ctypes.data_as(P(C.c_double)),
+                                             b.ctypes.data_as(P(C.c_double)), len(a),
+                                             out.ctypes.data_as(P(C.c_double))), "selftest_math")
+        return out
 
     def work_counters(self):
         out = (C.c_int64 * 3)()

@@ -12,6 +12,7 @@
 //   8. append the records to the tree                                        (k_append)
 // Failed candidates never write rows: only accepted rollouts are replayed with row output.
 #include <hip/hip_runtime.h>
+#include <math.h>
 
 #include <algorithm>
 #include <chrono>
@@ -171,10 +172,12 @@ static void derive(const clrrt_params& q, DevParams& d, int n_obs) {
   double dla_end = std::max(q.ctrl_mindla, d.dla_c + q.ctrl_tla * std::abs(q.goal[3]));
   double Dext = dla_end, Dal = 1;
   const double* g = q.goal;
-  d.gbP1x = g[0] + Dal * cos(g[2]); d.gbP1y = g[1] + Dal * sin(g[2]);
-  d.gbP2x = g[0] - Dal * cos(g[2]); d.gbP2y = g[1] - Dal * sin(g[2]);
-  d.gbF1x = d.gbP1x + (Dext + Dal) * cos(g[2]); d.gbF1y = d.gbP1y + (Dext + Dal) * sin(g[2]);
-  d.gbF2x = d.gbP2x + (Dext + Dal) * cos(g[2]); d.gbF2y = d.gbP2y + (Dext + Dal) * sin(g[2]);
+  double sg2, cg2;
+  ::sincos(g[2], &sg2, &cg2);  // getGoalReference: cos and sin of one argument -> glibc sincos
+  d.gbP1x = g[0] + Dal * cg2; d.gbP1y = g[1] + Dal * sg2;
+  d.gbP2x = g[0] - Dal * cg2; d.gbP2y = g[1] - Dal * sg2;
+  d.gbF1x = d.gbP1x + (Dext + Dal) * cg2; d.gbF1y = d.gbP1y + (Dext + Dal) * sg2;
+  d.gbF2x = d.gbP2x + (Dext + Dal) * cg2; d.gbF2y = d.gbP2y + (Dext + Dal) * sg2;
   // feasibleGoalBias rrtplanner.cpp:294-299 (the .y coordinates use cos, as the reference does)
   double R1 = 4.77;
   d.gbR2 = R1 - 0.3;
@@ -262,7 +265,9 @@ int clrrt_draw_samples(const clrrt_params* p, clrrt_rng* rng, int32_t n, clrrt_s
   double latMin = -7, latMax = 7;
   float fl = (float)(RM / (dGoal + 10));
   float fw = (float)(RM / (latMax - latMin));
-  double ch = cos(hd), sh = sin(hd), cq = cos(hd + M_PI / 2), sq = sin(hd + M_PI / 2);
+  double ch, sh, cq, sq;
+  ::sincos(hd, &sh, &ch);  // sampleAroundVehicle: cos/sin pairs of one argument -> glibc sincos
+  ::sincos(hd + M_PI / 2, &sq, &cq);
   for (int j = 0; j < n; j++) {
     double rLong = (float)clrrt_rng_next(rng) / fl;
     double rLat = latMin + (float)clrrt_rng_next(rng) / fw;
@@ -401,7 +406,8 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
     BakedObs& d = b[i];
     memset(&d, 0, sizeof(d));
     float w = (float)(o[i].size_x / 2), h = (float)(o[i].size_y / 2), th = (float)o[i].theta;
-    float cf = std::cos(th), sf = std::sin(th);
+    float cf, sf;
+    ::sincosf(th, &sf, &cf);  // OBB::setVertices: float cos/sin of one argument -> glibc sincosf
     float hh = h / 2, ww = w / 2;
     d.P = cf * hh; d.Q = sf * ww; d.R = sf * hh; d.S = cf * ww;
     d.cx = o[i].cx; d.cy = o[i].cy; d.vlx = o[i].vx; d.vly = o[i].vy;
@@ -613,7 +619,8 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
     HIPC(c, hipMemcpyAsync(c->first_conflict, c->h_int, sizeof(int), hipMemcpyHostToDevice, st));
     {
       KTimer kt(c, 2);
-      HIPC(c, launch_conflict(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->first_conflict));
+      HIPC(c, launch_conflict(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie,
+                              c->first_conflict));
     }
     HIPC(c, hipMemcpyAsync(c->h_int + 1, c->first_conflict, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPC(c, hipStreamSynchronize(st));
@@ -807,6 +814,26 @@ int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, 
     o.ref_vback = hr[j].vback;
     o.ref_n = hr[j].refN;
   }
+  return CLRRT_OK;
+}
+
+int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double* b, int32_t n, double* out) {
+  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 17) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  double *da = nullptr, *db = nullptr, *dout = nullptr;
+  hipError_t e = hipMalloc((void**)&da, sizeof(double) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&db, sizeof(double) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * n);
+  if (e == hipSuccess) e = hipMemcpyAsync(da, a, sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(db, b, sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_selftest_math(c->stream, fn, da, db, n, dout);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(da);
+  hipFree(db);
+  hipFree(dout);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("selftest_math: ") + hipGetErrorString(e));
   return CLRRT_OK;
 }
 

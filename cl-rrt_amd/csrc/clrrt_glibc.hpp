@@ -1,0 +1,310 @@
+// clrrt_glibc.hpp — glibc 2.35's double sin, cos and tan restated for gfx950 (and the host tests).
+//
+// The reference computes its closed-loop rollouts with glibc's libm (rrt/src/simulation.cpp:13-16,
+// controller.cpp:56-57,115-132).  Its goal-biased rollouts are ill-conditioned: getGoalReference
+// duplicates the joint point of its two segments (reference.cpp:56-63), so the 3-point Lagrange
+// interpolation of getLateralError divides by ~0 there (controller.cpp:134-148) and the sign of the
+// saturated steering command depends on the last bit of every earlier sin/cos/tan.  Matching the
+// reference's trees therefore needs these three functions bit for bit.  On x86-64 CPUs with
+// FMA+AVX2 (the oracle's and the GPU box's hosts), libm's ifunc runs the FMA-compiled variants of
+// sysdeps/ieee754/dbl-64/s_sin.c and s_tan.c (IBM Accurate Mathematical Library); this file follows
+// their algorithm — table-driven do_sin/do_cos with the Cody-Waite reduce_sincos, and tan's xfg
+// table path — and fuses exactly the multiply-adds that build fuses, so every rounding is identical.
+//
+// Domain restated: |x| < 105414350 for sin/cos (beyond that glibc switches to __branred: we fall
+// back to the GPU libm, outside anything the planner evaluates); |x| <= 0.787 for tan (steering
+// angles are clamped to +-0.52 rad; larger arguments fall back likewise).  NaN/Inf propagate.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <cmath>
+
+#include "clrrt_glibc_data.hpp"
+
+#ifndef CLRRT_HD
+#if defined(__HIPCC__)
+#define CLRRT_HD __host__ __device__
+#else
+#define CLRRT_HD
+#endif
+#endif
+
+namespace clrrt {
+namespace glibc {
+
+#if defined(__HIPCC__)
+static __device__ __constant__ double d_sincostab[SINCOSTAB_N] = CLRRT_GLIBC_SINCOSTAB;
+static __device__ __constant__ double d_xfg[XFG_ROWS * 4] = CLRRT_GLIBC_XFG;
+#endif
+static const double h_sincostab[SINCOSTAB_N] = CLRRT_GLIBC_SINCOSTAB;
+static const double h_xfg[XFG_ROWS * 4] = CLRRT_GLIBC_XFG;
+
+CLRRT_HD inline const double* sincostab() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return d_sincostab;
+#else
+  return h_sincostab;
+#endif
+}
+CLRRT_HD inline const double* xfg() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return d_xfg;
+#else
+  return h_xfg;
+#endif
+}
+
+CLRRT_HD inline uint64_t bits(double x) {
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  return u;
+}
+CLRRT_HD inline uint32_t hi_word(double x) { return (uint32_t)(bits(x) >> 32); }
+CLRRT_HD inline int32_t lo_word(double x) { return (int32_t)(uint32_t)bits(x); }
+CLRRT_HD inline double fma_(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(a, b, c);
+#else
+  return std::fma(a, b, c);
+#endif
+}
+CLRRT_HD inline double copysign_(double m, double s) {
+  uint64_t u = (bits(m) & 0x7fffffffffffffffull) | (bits(s) & 0x8000000000000000ull);
+  double r;
+  memcpy(&r, &u, 8);
+  return r;
+}
+
+// TAYLOR_SIN (s_sin.c): a + ((poly(xx)*a - 0.5*da)*xx + da)
+CLRRT_HD inline double taylor_sin(double a, double da) {
+  double xx = a * a;
+  double t = fma_(xx, s5, s4);
+  t = fma_(xx, t, s3);
+  t = fma_(xx, t, s2);
+  t = fma_(xx, t, s1);
+  double u = fma_(t, a, -(0.5 * da));
+  double w = fma_(xx, u, da);
+  return w + a;
+}
+
+// do_sin (s_sin.c) for |x| >= taylor_lim: sin(x + dx) from the sin/cos table at k/128.
+CLRRT_HD inline double do_sin_tab(double x, double dx) {
+  if (x <= 0) dx = -dx;
+  double ax = fabs(x);
+  double u = ax + big;
+  int k = lo_word(u) << 2;
+  double xr = ax - (u - big);
+  double xx = xr * xr;
+  double s = xr + fma_(xr * xx, fma_(xx, sn5, sn3), dx);
+  double c = fma_(xr, dx, xx * fma_(xx, fma_(xx, cs6, cs4), cs2));
+  const double* T = sincostab();
+  double sn = T[k], ssn = T[k + 1], cs = T[k + 2], ccs = T[k + 3];
+  double cor = fma_(s, ccs, ssn);
+  cor = fma_(-c, sn, cor);
+  cor = fma_(s, cs, cor);
+  return copysign_(sn + cor, x);
+}
+
+CLRRT_HD inline double do_sin(double x, double dx) {
+  if (fabs(x) < taylor_lim) return taylor_sin(x, dx);
+  return do_sin_tab(x, dx);
+}
+
+// do_cos (s_sin.c): cos(x + dx) from the sin/cos table at k/128.
+CLRRT_HD inline double do_cos(double x, double dx) {
+  if (x < 0) dx = -dx;
+  double ax = fabs(x);
+  double u = ax + big;
+  int k = lo_word(u) << 2;
+  double xr = (ax - (u - big)) + dx;
+  double xx = xr * xr;
+  double s = fma_(xr * xx, fma_(xx, sn5, sn3), xr);
+  double c = xx * fma_(xx, fma_(xx, cs6, cs4), cs2);
+  const double* T = sincostab();
+  double sn = T[k], ssn = T[k + 1], cs = T[k + 2], ccs = T[k + 3];
+  double cor = fma_(-s, ssn, ccs);
+  cor = fma_(-c, cs, cor);
+  cor = fma_(-s, sn, cor);
+  return cs + cor;
+}
+
+// reduce_sincos (s_sin.c): x = n*pi/2 + (a + da), |a| <= pi/4.
+CLRRT_HD inline int reduce_sincos(double x, double& a, double& da) {
+  double t = fma_(x, hpinv, toint);
+  double xn = t - toint;
+  int n = lo_word(t) & 3;
+  double y = fma_(-xn, mp1, x);
+  y = fma_(-xn, mp2, y);
+  double t2 = fma_(-xn, pp3, y);
+  double db = fma_(-pp3, xn, y - t2);
+  double b = fma_(-xn, pp4, t2);
+  double db2 = fma_(-xn, pp4, t2 - b);
+  a = b;
+  da = db + db2;
+  return n;
+}
+
+CLRRT_HD inline double do_sincos(double a, double da, int n) {
+  double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+  return (n & 2) ? -r : r;
+}
+
+CLRRT_HD inline double sin(double x) {
+  uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (k < 0x3e500000u) return x;
+  if (k < 0x3feb6000u) return do_sin(x, 0.0);
+  if (k < 0x400368fdu) {
+    double t = hp0 - fabs(x);
+    return copysign_(do_cos(t, hp1), x);
+  }
+  if (k < 0x419921fbu) {
+    double a, da;
+    int n = reduce_sincos(x, a, da);
+    return do_sincos(a, da, n);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ::sin(x);  // |x| >= 105414350 or non-finite: outside the restated domain
+#else
+  return std::sin(x);
+#endif
+}
+
+CLRRT_HD inline double cos(double x) {
+  uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (k < 0x3e400000u) return 1.0;
+  if (k < 0x3feb6000u) return do_cos(x, 0.0);
+  if (k < 0x400368fdu) {
+    double y = hp0 - fabs(x);
+    double a = y + hp1;
+    double da = (y - a) + hp1;
+    return do_sin(a, da);
+  }
+  if (k < 0x419921fbu) {
+    double a, da;
+    int n = reduce_sincos(x, a, da);
+    return do_sincos(a, da, n + 1);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ::cos(x);
+#else
+  return std::cos(x);
+#endif
+}
+
+// s_tan.c cases (I) |x| <= g1, (II) |x| < g2 polynomial, (III) |x| <= g3 xfg table.
+CLRRT_HD inline double tan(double x) {
+  double w = (x < 0.0) ? -x : x;
+  if (w <= tan_g1) return x;
+  if (w <= tan_g2) {
+    double x2 = x * x;
+    double t = fma_(x2, d11, d9);
+    t = fma_(x2, t, d7);
+    t = fma_(x2, t, d5);
+    t = fma_(x2, t, d3);
+    return fma_(x * x2, t, x);
+  }
+  if (w <= tan_g3) {
+    int i = (int)fma_(w, two8, mfftnhf);
+    const double* row = xfg() + 4 * i;
+    double z = w - row[0];
+    double z2 = z * z;
+    double pz = fma_(z * z2, fma_(z2, e1, e0), z);
+    double fi = row[1], gi = row[2];
+    double y = ((fi + gi) * pz) / (gi - pz) + fi;
+    return (x >= 0.0 ? 1.0 : -1.0) * y;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ::tan(x);  // outside the restated domain (steering angles never get here)
+#else
+  return std::tan(x);
+#endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// sincos: glibc's __sincos (s_sincos.c) is NOT ifunc-dispatched; libm ships only its generic SSE2
+// build, so its do_sin/do_cos/TAYLOR_SIN/reduce_sincos round every product and sum separately.
+// GCC merges a sin(x) and a cos(x) of the same argument in one function into a sincos(x) call, which
+// is how the reference evaluates the vehicle heading (controller.cpp:56-57,115-132,
+// simulation.cpp:14-15, old_collisioncheck.cpp:34) — so the rollouts need this variant.
+namespace nofma {
+CLRRT_HD inline double taylor_sin(double a, double da) {
+  double xx = a * a;
+  double p = ((((s5 * xx + s4) * xx + s3) * xx + s2) * xx) + s1;
+  double t = ((p * a - 0.5 * da) * xx + da);
+  return a + t;
+}
+CLRRT_HD inline double do_sin(double x, double dx) {
+  double xold = x;
+  if (fabs(x) < taylor_lim) return taylor_sin(x, dx);
+  if (x <= 0) dx = -dx;
+  double u = big + fabs(x);
+  int k = lo_word(u) << 2;
+  x = fabs(x) - (u - big);
+  double xx = x * x;
+  double s = x + (dx + x * xx * (sn3 + xx * sn5));
+  double c = x * dx + xx * (cs2 + xx * (cs4 + xx * cs6));
+  const double* T = sincostab();
+  double sn = T[k], ssn = T[k + 1], cs = T[k + 2], ccs = T[k + 3];
+  double cor = (ssn + s * ccs - sn * c) + cs * s;
+  return copysign_(sn + cor, xold);
+}
+CLRRT_HD inline double do_cos(double x, double dx) {
+  if (x < 0) dx = -dx;
+  double u = big + fabs(x);
+  int k = lo_word(u) << 2;
+  x = fabs(x) - (u - big) + dx;
+  double xx = x * x;
+  double s = x + x * xx * (sn3 + xx * sn5);
+  double c = xx * (cs2 + xx * (cs4 + xx * cs6));
+  const double* T = sincostab();
+  double sn = T[k], ssn = T[k + 1], cs = T[k + 2], ccs = T[k + 3];
+  double cor = (ccs - s * ssn - cs * c) - sn * s;
+  return cs + cor;
+}
+CLRRT_HD inline int reduce_sincos(double x, double& a, double& da) {
+  double t = (x * hpinv + toint);
+  double xn = t - toint;
+  int n = lo_word(t) & 3;
+  double y = (x - xn * mp1) - xn * mp2;
+  double t1 = xn * pp3;
+  double t2 = y - t1;
+  double db = (y - t2) - t1;
+  t1 = xn * pp4;
+  double b = t2 - t1;
+  db += (t2 - b) - t1;
+  a = b;
+  da = db;
+  return n;
+}
+CLRRT_HD inline double do_sincos(double a, double da, int n) {
+  double r = (n & 1) ? do_cos(a, da) : do_sin(a, da);
+  return (n & 2) ? -r : r;
+}
+}  // namespace nofma
+
+CLRRT_HD inline void sincos(double x, double& sx, double& cx) {
+  uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (k < 0x400368fdu) {
+    if (k < 0x3e400000u) { sx = x; cx = 1.0; return; }
+    if (k < 0x3feb6000u) { sx = nofma::do_sin(x, 0); cx = nofma::do_cos(x, 0); return; }
+    double y = hp0 - fabs(x);
+    double a = y + hp1;
+    double da = (y - a) + hp1;
+    sx = copysign_(nofma::do_cos(a, da), x);
+    cx = nofma::do_sin(a, da);
+    return;
+  }
+  if (k < 0x419921fbu) {
+    double a, da;
+    int n = nofma::reduce_sincos(x, a, da);
+    sx = nofma::do_sincos(a, da, n);
+    cx = nofma::do_sincos(a, da, n + 1);
+    return;
+  }
+  sx = sin(x);  // outside the restated domain
+  cx = cos(x);
+}
+
+}  // namespace glibc
+}  // namespace clrrt

@@ -91,11 +91,13 @@ hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const int* gbflag,
                             const RollRes* gbres, clrrt_node* gbnodes, SampleOut* so);
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
-                           const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, int* first);
+                           const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
+                           int* first);
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
                           clrrt_node* out, Job* jobs, int64_t* totals);
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn);
+hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out);
 hipError_t launch_init_root(hipStream_t st, const double* state, clrrt_node* tree, NnRec* nn, double* arena);
 
 }  // namespace clrrt

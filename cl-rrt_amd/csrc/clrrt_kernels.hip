@@ -236,9 +236,8 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   r.x5 = r.x5 + d5 * p.dt;
   r.x6 = r.x6 + 1.0 * p.dt;
   r.x3 = satd(-p.dmax, p.dmax, r.x3);
-  r.c2 = cos(r.x2);
-  r.s2 = sin(r.x2);
-  r.t3 = tan(r.x3);
+  glibc::sincos(r.x2, r.s2, r.c2);
+  r.t3 = glibc::tan(r.x3);
   col7 = (double)r.wp;
   col8 = prof_v(r.P, r.wp + 2);
   col9 = dc;
@@ -388,7 +387,7 @@ __device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const dou
   double h1 = fabs(wrap_pi(p.g2 - aRef));
   double h2 = fabs(wrap_pi(p.g2 + M_PI - aRef));
   double m = mn(h1, h2);
-  double cv = cos(p.g2 + M_PI_2 - aRef);
+  double cv = glibc::cos(p.g2 + M_PI_2 - aRef);
   double sg = (double)((0.0 < cv) - (cv < 0.0));
   double ang = sg * m;
   bool within = fabs(ang) < (M_PI_4 / 2);
@@ -469,17 +468,21 @@ __global__ void k_gb_select(int B, const clrrt_node* __restrict__ regnodes, cons
 
 // EXACT mode: sample j conflicts when a node produced by an earlier sample of the round would sort
 // at or before j's accepted candidate (or into j's candidate window when nothing was accepted).
+// A sample whose selection involves equal keys conflicts with ANY node appended before it in the
+// round: std::sort orders equal keys by its partitioning of the whole (grown) array.
 __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ S,
                            const clrrt_node* __restrict__ regnodes, const clrrt_node* __restrict__ gbnodes,
-                           const SampleOut* __restrict__ so, int* first_conflict) {
+                           const SampleOut* __restrict__ so, const int* __restrict__ ctie, int* first_conflict) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B) return;
   const double sx = S[j].x, sy = S[j].y;
   const int ex = S[j].explore;
   const float thr = so[j].thr;
+  const bool tie = ctie[j] != 0;
   bool conflict = false;
   for (int k = 0; k < j && !conflict; k++) {
     if (so[k].k < 0) continue;
+    if (tie) { conflict = true; break; }
     for (int w = 0; w < 2; w++) {
       if (w == 1 && !so[k].gb_ok) break;
       const clrrt_node& n = w == 0 ? regnodes[k] : gbnodes[k];
@@ -616,6 +619,38 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   nn[0] = r;
 }
 
+// Elementary functions as the kernels evaluate them (test hook: bit-compared with the host libm).
+__global__ void k_selftest_math(int fn, const double* __restrict__ a, const double* __restrict__ b, int n,
+                                double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = a[i], y = b[i];
+  const float xf = (float)x, yf = (float)y;
+  double r;
+  switch (fn) {
+    case 0: r = glibc::sin(x); break;
+    case 1: r = glibc::cos(x); break;
+    case 2: r = glibc::tan(x); break;
+    case 3: r = sqrt(x); break;
+    case 4: r = fmod(x, y); break;
+    case 5: r = atan2(x, y); break;
+    case 6: r = exp(x); break;
+    case 7: r = x / y; break;
+    case 8: r = (double)cosf(xf); break;
+    case 9: r = (double)sinf(xf); break;
+    case 10: r = (double)atan2f(xf, yf); break;
+    case 11: r = (double)acosf(xf); break;
+    case 12: r = (double)asinf(xf); break;
+    case 13: r = (double)sqrtf(xf); break;
+    case 14: r = (double)(xf / yf); break;
+    case 15: r = round(x); break;
+    case 16: { double sx, cx; glibc::sincos(x, sx, cx); r = sx; } break;
+    case 17: { double sx, cx; glibc::sincos(x, sx, cx); r = cx; } break;
+    default: r = 0.0; break;
+  }
+  out[i] = r;
+}
+
 // ============================================================================================
 // launch wrappers (host)
 // ============================================================================================
@@ -681,8 +716,9 @@ hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const 
 }
 
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
-                           const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, int* first) {
-  hipLaunchKernelGGL(k_conflict, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, first);
+                           const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
+                           int* first) {
+  hipLaunchKernelGGL(k_conflict, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, ctie, first);
   LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -699,6 +735,13 @@ hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const in
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_append, dim3((n + 255) / 256), dim3(256), 0, st, in, n, base, tree, nn);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, st, fn, a, b, n, out);
   LAUNCH_CHECK();
   return hipSuccess;
 }

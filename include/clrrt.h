@@ -239,6 +239,13 @@ int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n
 int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t* out_ids,
                    float* out_keys);
 
+/* Test hook: evaluates, on the device, the elementary functions exactly as the kernels call them,
+ * out[i] = f(a[i], b[i]) for fn = 0 sin, 1 cos, 2 tan (glibc restatements), 3 sqrt, 4 fmod, 5 atan2,
+ * 6 exp, 7 a/b, 8 cosf, 9 sinf, 10 atan2f, 11 acosf, 12 asinf, 13 sqrtf, 14 float a/b, 15 round,
+ * 16 sin and 17 cos of glibc's generic sincos
+ * (float functions take (float)a, (float)b and return the float widened to double). */
+int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const double* b, int32_t n, double* out);
+
 int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);
 int clrrt_reset_counters(clrrt_ctx* ctx);
 /* Algorithmic work done by rollout kernels since the last reset (SURVEY §8(d) roofline basis):

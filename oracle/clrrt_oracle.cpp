@@ -17,6 +17,9 @@
 //     proper edge normal of edge 3->0.  Decision-neutral (any separating axis proves separation).
 //
 // Pinned against the survey's golden outputs of the reference (tests/golden/survey_pins.json).
+#define _GNU_SOURCE 1
+#include <math.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -30,6 +33,20 @@
 #include "../include/clrrt.h"
 
 namespace orc {
+
+// ---------------------------------------------------------------- libm call sites
+// GCC -O2 merges sin(x) and cos(x) of one argument into glibc's sincos() where it can prove the
+// argument unchanged between the two calls, and glibc's sincos (generic build) rounds differently
+// from its sin/cos (FMA builds) in ~0.1% of arguments.  The reference's goal-biased rollouts are
+// ill-conditioned enough for that to matter, so every call site below names its libm entry point
+// explicitly (the choice GCC makes for the reference's code structure); the GPU kernels restate
+// the same entry point per site (cl-rrt_amd/csrc/clrrt_glibc.hpp).
+__attribute__((noinline)) static double lm_sin(double x) { return ::sin(x); }
+__attribute__((noinline)) static double lm_cos(double x) { return ::cos(x); }
+__attribute__((noinline)) static double lm_tan(double x) { return ::tan(x); }
+__attribute__((noinline)) static void lm_sincos(double x, double* s, double* c) { ::sincos(x, s, c); }
+__attribute__((noinline)) static void lm_sincosf(float x, float* s, float* c) { ::sincosf(x, s, c); }
+__attribute__((noinline)) static float lm_sinf(float x) { return ::sinf(x); }
 
 using std::vector;
 typedef vector<double> Row;
@@ -118,9 +135,11 @@ static double lateral_error(const Ref& r, const Row& x, int wp, const Pt& P) {  
   double yv[3] = {at0(r.y, lo), at0(r.y, lo + 1), at0(r.y, hi)};
   double X0 = P.x, X1 = P.y, X2 = x[2];
   double tx[3], ty[3];
+  double sX, cX;
+  lm_sincos(X2, &sX, &cX);  // transformToVehicle: sin/cos of one argument -> sincos
   for (int i = 0; i < 3; i++) {
-    tx[i] = xv[i] * cos(X2) - X0 * cos(X2) - yv[i] * sin(X2) + X1 * sin(X2);
-    ty[i] = yv[i] * cos(X2) - X1 * cos(X2) + xv[i] * sin(X2) - X0 * sin(X2);
+    tx[i] = xv[i] * cX - X0 * cX - yv[i] * sX + X1 * sX;
+    ty[i] = yv[i] * cX - X1 * cX + xv[i] * sX - X0 * sX;
   }
   double y = 0, L;
   for (int i = 0; i < 3; i++) {
@@ -140,8 +159,8 @@ struct Ctrl {  // class Controller controller.h:8-28
 
   void update_waypoint(Oracle& o, const Ref& r, const Row& x) {  // controller.cpp:53-68
     update_lookahead(o, x[4]);
-    P.x = x[0] + o.ctrl_dla * r.dir * std::cos(x[2]);
-    P.y = x[1] + o.ctrl_dla * r.dir * std::sin(x[2]);
+    P.x = x[0] + o.ctrl_dla * r.dir * lm_cos(x[2]);  // a store between the two calls: no sincos
+    P.y = x[1] + o.ctrl_dla * r.dir * lm_sin(x[2]);
     IDwp = closest_point(r, P, IDwp);
     if ((size_t)IDwp >= r.x.size() - 1 - 2) endreached = true;
     if (at0(r.x, IDwp) == r.x.back() && at0(r.y, IDwp) == r.y.back()) endreached = true;
@@ -181,16 +200,18 @@ static Ref get_goal_reference(Oracle& o, Node node, vector<double> g) {  // refe
   double Dext = dla_end, Dal = 1;
   Ref r;
   Pt P1, P2, Pc, Pf;
-  P1.x = g[0] + Dal * cos(g[2]); P1.y = g[1] + Dal * sin(g[2]);
-  P2.x = g[0] - Dal * cos(g[2]); P2.y = g[1] - Dal * sin(g[2]);
+  double sg2, cg2;
+  lm_sincos(g[2], &sg2, &cg2);
+  P1.x = g[0] + Dal * cg2; P1.y = g[1] + Dal * sg2;
+  P2.x = g[0] - Dal * cg2; P2.y = g[1] - Dal * sg2;
   double bx = node.ref.x.back(), by = node.ref.y.back();
   if (sqrt(pow(P1.x - bx, 2) + pow(P1.y - by, 2)) < sqrt(pow(P2.x - bx, 2) + pow(P2.y - by, 2))) {
     Pc = P1; Pf = P1;
   } else {
     Pc = P2; Pf = P2;
   }
-  Pf.x += (Dext + Dal) * cos(g[2]);
-  Pf.y += (Dext + Dal) * sin(g[2]);
+  Pf.x += (Dext + Dal) * cg2;
+  Pf.y += (Dext + Dal) * sg2;
   double N1 = round(sqrt(pow(Pc.x - bx, 2) + pow(Pc.y - by, 2)) / o.p.ref_res) + 1;
   double N2 = round(sqrt(pow(Pf.x - Pc.x, 2) + pow(Pf.y - Pc.y, 2)) / o.p.ref_res) + 1;
   vector<double> ax = linspace(bx, Pc.x, N1), bxv = linspace(Pc.x, Pf.x, N2);
@@ -264,15 +285,17 @@ struct Box {  // class OBB collision.h:16-34 (float fields)
   float w, h, o;
   float vx[4], vy[4], nx[4], ny[4], mm[2];
   Box(double _px, double _py, float _w, float _h, float _o) : px(_px), py(_py), w(_w), h(_h), o(_o) {
-    // setVertices old_collisioncheck.cpp:56-65
-    vx[0] = px + std::cos(o) * (h / 2) - std::sin(o) * (w / 2);
-    vy[0] = py + std::sin(o) * (h / 2) + std::cos(o) * (w / 2);
-    vx[1] = px + std::cos(o) * (h / 2) - std::sin(o) * (-w / 2);
-    vy[1] = py + std::sin(o) * (h / 2) + std::cos(o) * (-w / 2);
-    vx[2] = px + std::cos(o) * (-h / 2) - std::sin(o) * (-w / 2);
-    vy[2] = py + std::sin(o) * (-h / 2) + std::cos(o) * (-w / 2);
-    vx[3] = px + std::cos(o) * (-h / 2) - std::sin(o) * (w / 2);
-    vy[3] = py + std::sin(o) * (-h / 2) + std::cos(o) * (w / 2);
+    // setVertices old_collisioncheck.cpp:56-65 (float cos/sin of o -> sincosf)
+    float so, co;
+    lm_sincosf(o, &so, &co);
+    vx[0] = px + co * (h / 2) - so * (w / 2);
+    vy[0] = py + so * (h / 2) + co * (w / 2);
+    vx[1] = px + co * (h / 2) - so * (-w / 2);
+    vy[1] = py + so * (h / 2) + co * (-w / 2);
+    vx[2] = px + co * (-h / 2) - so * (-w / 2);
+    vy[2] = py + so * (-h / 2) + co * (-w / 2);
+    vx[3] = px + co * (-h / 2) - so * (w / 2);
+    vy[3] = py + so * (-h / 2) + co * (w / 2);
     // setNorms :67-76, axis 3 canonicalised to the proper edge normal
     for (int i = 0; i < 3; i++) {
       nx[i] = vy[i + 1] - vy[i];
@@ -320,7 +343,9 @@ static double obs_distance(Oracle& o, const Row& x) {
     const Obs& d = o.det[i];
     boxes.push_back(Box(d.cx + d.vx * t, d.cy + d.vy * t, d.sx / 2, d.sy / 2, d.th));
   }
-  Box veh(x[0] + 1.424 * cos(x[2]), x[1] + 1.424 * sin(x[2]), 2, 4.848, x[2]);
+  double sv, cv;
+  lm_sincos(x[2], &sv, &cv);
+  Box veh(x[0] + 1.424 * cv, x[1] + 1.424 * sv, 2, 4.848, x[2]);
   double best = 10000;
   for (size_t j = 0; j != boxes.size(); j++) {
     double D = box_gap(veh, boxes[j]);
@@ -357,9 +382,11 @@ static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
     // VehicleODE :11-25
     double dx[7];
     double Gss = 1 / (1 + pow((x[4] / veh.Vch), 2));
-    dx[0] = x[4] * cos(x[2]);
-    dx[1] = x[4] * sin(x[2]);
-    dx[2] = (x[4] / veh.L) * tan(x[3]) * Gss;
+    double s2, c2;
+    lm_sincos(x[2], &s2, &c2);
+    dx[0] = x[4] * c2;
+    dx[1] = x[4] * s2;
+    dx[2] = (x[4] / veh.L) * lm_tan(x[3]) * Gss;
     dx[3] = (1 / veh.Td) * (dc - x[3]);
     dx[4] = x[5];
     dx[5] = (1 / veh.Ta) * (ac - x[5]);
@@ -376,7 +403,7 @@ static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
     double Dobs = obs_distance(o, x);
     if (Dobs == 0) { s.endReached = false; o.fail_collision++; s.outcome = CLRRT_ROLL_COLLISION; return; }
     s.costE += x[4] * dt;
-    double kappa = tan(x[3]) / veh.L;
+    double kappa = lm_tan(x[3]) / veh.L;
     s.costS += o.p.Wcost[0] * x[4] * dt + o.p.Wcost[1] * std::abs(kappa) +
                o.p.Wcost[2] * exp(-o.p.Wcost[3] * Dobs);
     if (o.p.bend) s.costS += o.p.Wcost[4] * dist_to_lane(x[0], x[1], o.p.lane_shift0, o.p.Cxy);
@@ -413,8 +440,11 @@ static Pt sample_around(Oracle& o) {  // :187-201
   Pt s;
   double rLong = static_cast<float>(rand()) / (static_cast<float>(RAND_MAX / (dGoal + 10)));
   double rLat = latMin + static_cast<float>(rand()) / (static_cast<float>(RAND_MAX / (latMax - latMin)));
-  s.x = rLong * cos(hd) + rLat * cos(hd + M_PI / 2);
-  s.y = rLong * sin(hd) + rLat * sin(hd + M_PI / 2);
+  double sh, ch, sq, cq;
+  lm_sincos(hd, &sh, &ch);
+  lm_sincos(hd + M_PI / 2, &sq, &cq);
+  s.x = rLong * ch + rLat * cq;
+  s.y = rLong * sh + rLat * sq;
   return s;
 }
 
@@ -423,8 +453,10 @@ static float dubins(Pt S, Node N, int dir) {  // dubinsDistance :371-406 (Node b
   float qx = S.x - N.state[0];
   float qy = S.y - N.state[1];
   float ang = -N.state[2] - M_PI * (dir != 1);
-  float tmp = std::cos(ang) * qx - std::sin(ang) * qy;
-  qy = std::abs(std::sin(ang) * qx + std::cos(ang) * qy);
+  float sa, ca;
+  lm_sincosf(ang, &sa, &ca);
+  float tmp = ca * qx - sa * qy;
+  qy = std::abs(sa * qx + ca * qy);
   qx = tmp;
   float dc = std::sqrt(qx * qx + (qy - rho) * (qy - rho));
   float thc = std::atan2(qx, rho - qy);
@@ -434,7 +466,7 @@ static float dubins(Pt S, Node N, int dir) {  // dubinsDistance :371-406 (Node b
   bool inside = (qx * qx + (qy + rho) * (qy + rho) <= rho * rho) |
                 (qx * qx + (qy - rho) * (qy - rho) <= rho * rho);
   if (!inside) return std::sqrt(dc * dc - rho * rho) + rho * (thc - std::acos(rho / dc));
-  return rho * (alpha + std::asin(qx / df) - std::asin(rho * std::sin(alpha) / df));
+  return rho * (alpha + std::asin(qx / df) - std::asin(rho * lm_sinf(alpha) / df));
 }
 
 static bool feasible_node(Oracle& o, const Node& n, const Pt& s) {  // :271-289
@@ -474,17 +506,17 @@ static bool feasible_goal_bias(Oracle& o, const Node& node) {  // :292-315 (cos 
   const double* g = o.p.goal;
   double R1 = 4.77, R2 = R1 - 0.3;
   Pt cl, cr;
-  cl.x = g[0] + R1 * cos(g[2] - M_PI_2);
-  cl.y = g[1] + R1 * cos(g[2] - M_PI_2);
-  cr.x = g[0] + R1 * cos(g[2] + M_PI_2);
-  cr.y = g[1] + R1 * cos(g[2] + M_PI_2);
+  cl.x = g[0] + R1 * lm_cos(g[2] - M_PI_2);
+  cl.y = g[1] + R1 * lm_cos(g[2] - M_PI_2);
+  cr.x = g[0] + R1 * lm_cos(g[2] + M_PI_2);
+  cr.y = g[1] + R1 * lm_cos(g[2] + M_PI_2);
   bool outL = sqrt(pow(node.state[0] - cl.x, 2) + pow(node.state[1] - cl.y, 2)) > R2;
   bool outR = sqrt(pow(node.state[0] - cr.x, 2) + pow(node.state[1] - cr.y, 2)) > R2;
   double aRef = atan2(g[1] - node.ref.y.back(), g[0] - node.ref.x.back());
   double h1 = std::abs(wrap_pi(g[2] - aRef));
   double h2 = std::abs(wrap_pi(g[2] + M_PI - aRef));
   double mn = std::min(h1, h2);
-  double sg = sgn(cos(g[2] + M_PI_2 - aRef));
+  double sg = sgn(lm_cos(g[2] + M_PI_2 - aRef));
   double ang = sg * mn;
   bool within = std::abs(ang) < (M_PI_4 / 2);
   return outL * outR * within;

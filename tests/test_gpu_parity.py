@@ -116,7 +116,8 @@ def _compare_trees(o, pl, label):
     return on, gn, first_bad
 
 
-@pytest.mark.parametrize("kind,seed,iters", [("empty", 1, 200), ("obb200", 3, 300)])
+@pytest.mark.parametrize("kind,seed,iters", [("empty", 1, 200), ("obb200", 3, 300), ("empty", 2, 300),
+                                             ("obb200", 5, 300), ("moving", 4, 250)])
 def test_exact_mode_tree_parity(kind, seed, iters):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
