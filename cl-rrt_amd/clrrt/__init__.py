@@ -49,7 +49,7 @@ _SIGS = {
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "clrrt_rollout_batch": (C.c_int, [C.c_void_p, P(abi.RolloutJob), C.c_int32, P(abi.RolloutResult),
                                       P(C.c_double), C.c_int32]),
-    "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, P(C.c_int32), P(C.c_float)]),
+    "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_int32, P(C.c_int32), P(C.c_float)]),
     "clrrt_selftest_math": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double), C.c_int32,
                                       P(C.c_double)]),
     "clrrt_get_counters": (C.c_int, [C.c_void_p, P(abi.Counters)]),
@@ -57,6 +57,8 @@ _SIGS = {
     "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_kernel_time": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_int64)]),
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "clrrt_set_nn_grid_threshold": (C.c_int, [C.c_void_p, C.c_int64]),
+    "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
 }
 
 
@@ -82,6 +84,8 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.clrrt_abi_version() != abi.CLRRT_ABI_VERSION:
+            raise ClrrtError(f"{LIB_PATH}: ABI version {L.clrrt_abi_version()} != {abi.CLRRT_ABI_VERSION}; rebuild")
         _lib = L
     return _lib
 
@@ -264,13 +268,15 @@ class Planner:
             res.append(d)
         return res
 
-    def sort_nodes_batch(self, samples):
-        """Candidate lists (ids, keys) for a list of abi.Sample."""
+    def sort_nodes_batch(self, samples, exact=True):
+        """Candidate lists (ids, keys) for a list of abi.Sample; exact: std::sort order of equal keys
+        (else node-index order)."""
         n = len(samples)
         arr = (abi.Sample * n)(*samples)
         ids = np.zeros((n, 10), dtype=np.int32)
         keys = np.zeros((n, 10), dtype=np.float32)
-        self._chk(self.L.clrrt_nn_batch(self.h, arr, n, ids.ctypes.data_as(P(C.c_int32)),
+        mode = CLRRT_MODE_EXACT if exact else CLRRT_MODE_BATCH
+        self._chk(self.L.clrrt_nn_batch(self.h, arr, n, mode, ids.ctypes.data_as(P(C.c_int32)),
                                         keys.ctypes.data_as(P(C.c_float))), "nn_batch")
         return ids, keys
 
@@ -298,6 +304,16 @@ class Planner:
 
     def enable_timing(self, on=True):
         self._chk(self.L.clrrt_enable_timing(self.h, 1 if on else 0), "enable_timing")
+
+    def nn_stats(self):
+        out = (C.c_int64 * 8)()
+        self._chk(self.L.clrrt_nn_stats(self.h, out), "nn_stats")
+        return {"waves": out[0], "nodes_read": out[1], "rings": out[2], "truncated_waves": out[3],
+                "last_fallback_samples": out[4]}
+
+    def set_nn_grid_threshold(self, min_nodes):
+        """Trees of >= min_nodes nodes use the spatial-grid nearest-node search (0: always)."""
+        self._chk(self.L.clrrt_set_nn_grid_threshold(self.h, int(min_nodes)), "set_nn_grid_threshold")
 
     def kernel_time(self, which):
         ms, n = C.c_double(), C.c_int64()

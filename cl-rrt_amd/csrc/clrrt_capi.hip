@@ -2,15 +2,15 @@
 //
 // Round structure of one batch of expandTree iterations (rrtplanner.cpp:123-174) on the GPU:
 //   1. nearest-node search for every sample against the frozen tree        (k_nn_partial/merge)
-//   2. every candidate rollout of every sample, speculatively in parallel    (k_rollout SPEC)
-//   3. first success per sample -> regular node, goal-bias gate              (k_select)
-//   4. goal-biased rollout from each new node                                (k_rollout GB, k_gb_select)
-//   5. EXACT mode only: first sample whose candidate list a node of an earlier sample of the round
+//   2. every candidate rollout of every sample, speculatively in parallel; a successful candidate
+//      that passes the goal-bias gate continues in the same lane with the goal-biased rollout;
+//      rows go to per-job slots                                              (k_rollout SPEC)
+//   3. first success per sample -> regular node (+ goal-biased node)         (k_select)
+//   4. EXACT mode only: first sample whose candidate list a node of an earlier sample of the round
 //      would reorder (k_conflict) -> commit the prefix before it, re-draw nothing, retry the rest
-//   6. scan committed samples -> node records, arena offsets, counters       (k_compact)
-//   7. replay the accepted rollouts writing stateArray rows into the arena   (k_rollout LIST)
-//   8. append the records to the tree                                        (k_append)
-// Failed candidates never write rows: only accepted rollouts are replayed with row output.
+//   5. scan committed samples -> node records, arena offsets, counters       (k_compact)
+//   6. copy the accepted trajectories from their slots into the arena        (k_copy_rows)
+//   7. append the records to the tree                                        (k_append)
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -55,6 +55,9 @@ struct clrrt_ctx {
   // obstacles
   BakedObs* obs = nullptr;
   int n_obs = 0;
+  ObsGrid grid{};              // device view of the static-obstacle grid
+  void* grid_buf = nullptr;    // start | items | mov
+  size_t grid_bytes = 0;
   // round buffers (capacity cap.max_batch samples)
   clrrt_sample* d_samples = nullptr;
   float* pk = nullptr;
@@ -68,16 +71,26 @@ struct clrrt_ctx {
   int64_t sort_cap = 0;  // KeyId entries
   RollRes* res_spec = nullptr;
   clrrt_node* regnodes = nullptr;
-  int* gbflag = nullptr;
   RollRes* res_gb = nullptr;
+  double* slots = nullptr;  // rollout rows of one round, [2][slot_rows][10][max_batch * CAND_K]
+  int slot_rows = 0;
   clrrt_node* gbnodes = nullptr;
   SampleOut* so = nullptr;
   int* first_conflict = nullptr;
   clrrt_node* out_nodes = nullptr;
   Job* jobs = nullptr;
-  RollRes* res_replay = nullptr;
   int64_t* totals = nullptr;
-  unsigned long long* work_ctr = nullptr;  // [3] algorithmic rollout work
+  unsigned long long* work_ctr = nullptr;  // [3] algorithmic rollout work; [8..15] nn search statistics
+  // spatial index of the tree (nearest-node search)
+  NnGridBufs nng{};
+  int* fb_list = nullptr;   // [max_batch] samples the grid search hands to brute force
+  int* fb_count = nullptr;
+  // bounding box of the tree's finite node positions (x0, y0, x1, y1), maintained on the host
+  double bbox[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  double* d_bbox = nullptr;  // [4] device result of launch_bbox
+  double* h_bbox = nullptr;  // [4] pinned
+  int64_t nng_min_nodes = INT64_MAX;  // grid search off by default (see clrrt_set_nn_grid_threshold)
+  double reg_x0 = 0, reg_y0 = 0, reg_x1 = 0, reg_y1 = 0;  // sampling region + margin
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -193,6 +206,36 @@ static void derive(const clrrt_params& q, DevParams& d, int n_obs) {
   d.need_gap = (q.collision_mode == CLRRT_COLLISION_OBB) && d.use_exp;
 }
 
+static const int64_t kNngMaxCells = 1 << 20, kNngMaxSuper = kNngMaxCells / 64;
+
+static void bbox_reset(clrrt_ctx* c) {
+  c->bbox[0] = c->bbox[1] = HUGE_VAL;
+  c->bbox[2] = c->bbox[3] = -HUGE_VAL;
+}
+static void bbox_add(clrrt_ctx* c, double x0, double y0, double x1, double y1) {
+  c->bbox[0] = std::min(c->bbox[0], x0); c->bbox[1] = std::min(c->bbox[1], y0);
+  c->bbox[2] = std::max(c->bbox[2], x1); c->bbox[3] = std::max(c->bbox[3], y1);
+}
+
+// Region holding the samples (sampleAroundVehicle rrtplanner.cpp:187-201: rLong in [0, dGoal+10],
+// rLat in [-7, 7] about the goal heading) and the goal, with a margin; nodes outside it go to the
+// index's always-scanned overflow cell.
+static void sample_region(const clrrt_params& q, double& x0, double& y0, double& x1, double& y1) {
+  const double* g = q.goal;
+  double dGoal = std::sqrt(g[0] * g[0] + g[1] * g[1]);
+  double hd = std::atan2(g[1], g[0]);
+  double ch = std::cos(hd), sh = std::sin(hd);
+  x0 = y0 = 1e300; x1 = y1 = -1e300;
+  for (double L : {0.0, dGoal + 10})
+    for (double W : {-7.0, 7.0}) {
+      double x = L * ch - W * sh, y = L * sh + W * ch;
+      x0 = std::min(x0, x); x1 = std::max(x1, x); y0 = std::min(y0, y); y1 = std::max(y1, y);
+    }
+  x0 = std::min(x0, g[0]); x1 = std::max(x1, g[0]); y0 = std::min(y0, g[1]); y1 = std::max(y1, g[1]);
+  const double m = 2.0;
+  x0 -= m; y0 -= m; x1 += m; y1 += m;
+}
+
 // ------------------------------------------------------------------------------------------ C-ABI
 extern "C" {
 
@@ -284,13 +327,17 @@ const char* clrrt_last_error(const clrrt_ctx* c) { return c ? c->err.c_str() : "
 
 static void free_all(clrrt_ctx* c) {
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
-                  c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so, c->first_conflict,
-                  c->out_nodes, c->jobs, c->res_replay, c->totals, c->work_ctr};
+                  c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
+                  c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
+                  c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
+                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->nng.scount, c->nng.sfill, c->nng.sstart,
+                  c->nng.order};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
+  if (c->h_bbox) hipHostFree(c->h_bbox);
   for (auto& pe : c->ev_pending) { hipEventDestroy(pe.second.first); hipEventDestroy(pe.second.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -338,17 +385,34 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->ctie, B));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
-  chk(dalloc(&c->gbflag, B));
-  chk(dalloc(&c->res_gb, B));
+  chk(dalloc(&c->res_gb, B * CAND_K));
+  c->slot_rows = c->dp.n_steps_max + 1;
+  chk(dalloc(&c->slots, (size_t)2 * c->slot_rows * 10 * B * CAND_K));
   chk(dalloc(&c->gbnodes, B));
   chk(dalloc(&c->so, B));
   chk(dalloc(&c->first_conflict, 1));
   chk(dalloc(&c->out_nodes, 2 * B));
   chk(dalloc(&c->jobs, 2 * B));
-  chk(dalloc(&c->res_replay, 2 * B));
   chk(dalloc(&c->totals, 8));
-  chk(dalloc(&c->work_ctr, 4));
-  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 4 * sizeof(unsigned long long)));
+  chk(dalloc(&c->nng.cellid, c->cap.max_nodes));
+  chk(dalloc(&c->nng.sorted, c->cap.max_nodes));
+  chk(dalloc(&c->nng.count, kNngMaxCells + 2));
+  chk(dalloc(&c->nng.fill, kNngMaxCells + 2));
+  chk(dalloc(&c->nng.start, kNngMaxCells + 2));
+  chk(dalloc(&c->nng.cmin, kNngMaxCells + 2));
+  chk(dalloc(&c->nng.smin, kNngMaxSuper + 2));
+  chk(dalloc(&c->nng.scount, 2 * kNngMaxSuper + 4));
+  chk(dalloc(&c->nng.sfill, 2 * kNngMaxSuper + 4));
+  chk(dalloc(&c->nng.sstart, 2 * kNngMaxSuper + 4));
+  chk(dalloc(&c->nng.order, B));
+  chk(dalloc(&c->nng.fmin, 4 * kNngMaxSuper));
+  chk(dalloc(&c->nng.fmax, 4 * kNngMaxSuper));
+  chk(dalloc(&c->fb_list, B));
+  chk(dalloc(&c->d_bbox, 4));
+  chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
+  chk(dalloc(&c->fb_count, 1));
+  chk(dalloc(&c->work_ctr, 16));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 16 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
@@ -392,15 +456,113 @@ int clrrt_set_rank(clrrt_ctx* c, int32_t rank) {
 
 int clrrt_set_params(clrrt_ctx* c, const clrrt_params* p) {
   if (!c || !p) return CLRRT_EINVAL;
+  DevParams d;
+  derive(*p, d, c->n_obs);
+  if (d.n_steps_max + 1 > c->slot_rows) {  // a smaller sim_dt needs longer rollout slots
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipFree(c->slots));
+    c->slots = nullptr;
+    c->slot_rows = 0;
+    HIPC(c, dalloc(&c->slots, (size_t)2 * (d.n_steps_max + 1) * 10 * c->cap.max_batch * CAND_K));
+    c->slot_rows = d.n_steps_max + 1;
+  }
   c->params = *p;
-  derive(c->params, c->dp, c->n_obs);
+  c->dp = d;
   return CLRRT_OK;
 }
+
+}  // extern "C"
+
+// Uniform grid over the static obstacles for the rollout's collision cull (see ObsGrid).  The
+// cell size starts near 1/1024 of the covered area and grows until the grid fits the LDS budget.
+static const float kVehRad = 2.6220219f, kCullMargin = 0.05f;  // = VEH_RAD, CULL_MARGIN (kernels)
+static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
+  std::vector<int> stat, mov;
+  for (int i = 0; i < (int)b.size(); i++) (b[i].moving ? mov : stat).push_back(i);
+  const double tol = 0.05;
+  double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300;
+  std::vector<double> rr(b.size());
+  for (int i : stat) {
+    rr[i] = (double)(b[i].brad + kVehRad + kCullMargin);
+    double cx = (double)(float)b[i].cx, cy = (double)(float)b[i].cy;
+    x0 = std::min(x0, cx - rr[i] - tol); x1 = std::max(x1, cx + rr[i] + tol);
+    y0 = std::min(y0, cy - rr[i] - tol); y1 = std::max(y1, cy + rr[i] + tol);
+  }
+  std::vector<uint32_t> start;
+  std::vector<uint16_t> items;
+  int gw = 0, gh = 0;
+  float fx0 = 0, fy0 = 0, finv = 0;
+  const size_t lds_budget = 60 * 1024 - (size_t)b.size() * 20;
+  if (!stat.empty() && std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1) &&
+      (size_t)b.size() * 20 < 48 * 1024) {
+    double W = x1 - x0, H = y1 - y0;
+    double cs = std::max(0.25, std::sqrt(W * H / 1024.0));
+    for (int attempt = 0; attempt < 40; attempt++, cs *= 1.25) {
+      finv = (float)(1.0 / cs);
+      fx0 = (float)x0; fy0 = (float)y0;
+      // effective cell size seen by the kernel's float arithmetic
+      double ecs = 1.0 / (double)finv;
+      gw = (int)std::ceil((x1 - fx0) / ecs) + 1;
+      gh = (int)std::ceil((y1 - fy0) / ecs) + 1;
+      if ((int64_t)gw * gh > 16384) continue;
+      start.assign((size_t)gw * gh + 1, 0);
+      items.clear();
+      for (int gy = 0; gy < gh; gy++)
+        for (int gx = 0; gx < gw; gx++) {
+          start[(size_t)gy * gw + gx] = (uint32_t)items.size();
+          double rx0 = fx0 + gx * ecs - tol, rx1 = fx0 + (gx + 1) * ecs + tol;
+          double ry0 = fy0 + gy * ecs - tol, ry1 = fy0 + (gy + 1) * ecs + tol;
+          for (int i : stat) {
+            double cx = (double)(float)b[i].cx, cy = (double)(float)b[i].cy;
+            double dx = std::max(0.0, std::max(rx0 - cx, cx - rx1));
+            double dy = std::max(0.0, std::max(ry0 - cy, cy - ry1));
+            if (dx * dx + dy * dy <= (rr[i] + tol) * (rr[i] + tol)) items.push_back((uint16_t)i);
+          }
+        }
+      start[(size_t)gw * gh] = (uint32_t)items.size();
+      size_t bytes = 4 * start.size() + 2 * (items.size() + mov.size());
+      if (bytes <= lds_budget) break;
+      gw = gh = 0;
+    }
+  }
+  if (gw == 0) { start.clear(); items.clear(); }
+  size_t need = 4 * start.size() + 2 * (items.size() + mov.size()) + 16;
+  if (need > c->grid_bytes) {
+    if (c->grid_buf) HIPC(c, hipFree(c->grid_buf));
+    c->grid_buf = nullptr;
+    c->grid_bytes = 0;
+    HIPC(c, hipMalloc(&c->grid_buf, need));
+    c->grid_bytes = need;
+  }
+  std::vector<uint8_t> host(need, 0);
+  size_t o_items = 4 * start.size(), o_mov = o_items + 2 * items.size();
+  if (!start.empty()) memcpy(host.data(), start.data(), 4 * start.size());
+  if (!items.empty()) memcpy(host.data() + o_items, items.data(), 2 * items.size());
+  for (size_t k = 0; k < mov.size(); k++) {
+    uint16_t v = (uint16_t)mov[k];
+    memcpy(host.data() + o_mov + 2 * k, &v, 2);
+  }
+  HIPC(c, hipMemcpyAsync(c->grid_buf, host.data(), need, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  ObsGrid& g = c->grid;
+  g.start = (const uint32_t*)c->grid_buf;
+  g.items = (const uint16_t*)((const uint8_t*)c->grid_buf + o_items);
+  g.mov = (const uint16_t*)((const uint8_t*)c->grid_buf + o_mov);
+  g.gw = gw; g.gh = gh;
+  g.nitems = (int)items.size();
+  g.nmov = (int)mov.size();
+  g.x0 = fx0; g.y0 = fy0; g.inv = finv;
+  return CLRRT_OK;
+}
+
+extern "C" {
 
 // getOBBvector old_collisioncheck.cpp:6-22, evaluated once per query instead of once per step.
 int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
   if (!c || m < 0 || (m > 0 && !o)) return CLRRT_EINVAL;
   if (m > c->cap.max_obstacles) return fail(c, CLRRT_ECAPACITY, "too many obstacles");
+  if (m > 6000) return fail(c, CLRRT_ECAPACITY, "at most 6000 obstacles (rollout LDS cull table)");
   std::vector<BakedObs> b(m);
   for (int i = 0; i < m; i++) {
     BakedObs& d = b[i];
@@ -438,7 +600,7 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
   }
   c->n_obs = m;
   derive(c->params, c->dp, m);
-  return CLRRT_OK;
+  return build_grid(c, b);
 }
 
 int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
@@ -453,6 +615,9 @@ int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
   if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("tree_init: ") + hipGetErrorString(e));
   c->n_nodes = 1;
   c->n_rows = 1;
+  bbox_reset(c);
+  if (std::isfinite(root_state[0]) && std::isfinite(root_state[1]))
+    bbox_add(c, root_state[0], root_state[1], root_state[0], root_state[1]);
   return CLRRT_OK;
 }
 
@@ -471,6 +636,10 @@ int clrrt_tree_load(clrrt_ctx* c, const clrrt_node* nodes, int64_t n) {
   }
   c->n_nodes = n;
   c->n_rows = 0;
+  bbox_reset(c);
+  for (int64_t i = 0; i < n; i++)
+    if (std::isfinite(nodes[i].state[0]) && std::isfinite(nodes[i].state[1]))
+      bbox_add(c, nodes[i].state[0], nodes[i].state[1], nodes[i].state[0], nodes[i].state[1]);
   return CLRRT_OK;
 }
 
@@ -511,7 +680,7 @@ int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 16 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return CLRRT_OK;
 }
@@ -523,6 +692,23 @@ int clrrt_work_counters(clrrt_ctx* c, int64_t out[3]) {
   HIPC(c, hipMemcpyAsync(h, c->work_ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   for (int i = 0; i < 3; i++) out[i] = (int64_t)h[i];
+  return CLRRT_OK;
+}
+
+int clrrt_nn_stats(clrrt_ctx* c, int64_t out[8]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  unsigned long long h[8];
+  HIPC(c, hipMemcpy(h, c->work_ctr + 8, sizeof(h), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 8; i++) out[i] = (int64_t)h[i];
+  out[4] &= 0xffffffff;
+  return CLRRT_OK;
+}
+
+int clrrt_set_nn_grid_threshold(clrrt_ctx* c, int64_t min_nodes) {
+  if (!c || min_nodes < 0) return CLRRT_EINVAL;
+  c->nng_min_nodes = min_nodes;
   return CLRRT_OK;
 }
 
@@ -552,12 +738,11 @@ static RollArgs roll_args(clrrt_ctx* c, int njobs) {
   a.tree = c->tree;
   a.samples = c->d_samples;
   a.cand = c->cand;
-  a.regnodes = c->regnodes;
-  a.gbflag = c->gbflag;
   a.jobs = c->jobs;
   a.obs = c->obs;
   a.arena = c->arena;
   a.ctr = c->work_ctr;
+  a.grid = c->grid;
   a.njobs = njobs;
   return a;
 }
@@ -574,6 +759,37 @@ static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
   return CLRRT_OK;
 }
 
+// Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
+static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
+  hipStream_t st = c->stream;
+  KTimer kt(c, 0);
+  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
+  NnGrid g{};
+  double x0, y0, x1, y1;
+  sample_region(c->params, x0, y0, x1, y1);
+  if (c->bbox[0] <= c->bbox[2]) {  // grid covers the samples and every finite node: no overflow
+    x0 = std::min(x0, c->bbox[0] - 1.0); y0 = std::min(y0, c->bbox[1] - 1.0);
+    x1 = std::max(x1, c->bbox[2] + 1.0); y1 = std::max(y1, c->bbox[3] + 1.0);
+  }
+  const double W = x1 - x0, H = y1 - y0;
+  const bool use_grid = c->n_nodes >= c->nng_min_nodes && std::isfinite(W * H) && W * H > 0;
+  if (use_grid) {
+    double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
+    auto supers = [&](double c) { return std::ceil(std::ceil(W / c) / 8) * std::ceil(std::ceil(H / c) / 8); };
+    while (supers(cs) * 64 > (double)kNngMaxCells) cs *= 1.1;
+    g.x0 = x0; g.y0 = y0; g.cs = cs; g.inv = 1.0 / cs;
+    g.slack = 1e-9 * (1.0 + std::fabs(x0) + std::fabs(y0) + W + H);
+    g.sw = ((int)std::ceil(W / cs) + 7) / 8; g.sh = ((int)std::ceil(H / cs) + 7) / 8;
+    g.gw = 8 * g.sw; g.gh = 8 * g.sh;
+    g.ncell = 64 * g.sw * g.sh;
+    HIPC(c, launch_nn_grid_build(st, c->nn, (int)c->n_nodes, g, c->nng));
+  }
+  HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
+                    c->ncand, c->ctie, max_chunks, scratch, use_grid ? &g : nullptr, &c->nng, c->fb_list,
+                    c->fb_count, c->work_ctr + 8));
+  return CLRRT_OK;
+}
+
 // Stages 1-4 (+5 in EXACT mode) for n samples already in c->d_samples.  Returns the number of
 // samples to commit (n in BATCH mode).
 static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
@@ -585,33 +801,25 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
     scratch = c->sort_scratch;
   }
   {
-    KTimer kt(c, 0);
-    int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
-    HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                      c->ncand, c->ctie, max_chunks, scratch));
+    int rc = run_nn(c, n, scratch);
+    if (rc != CLRRT_OK) return rc;
   }
   {
     KTimer kt(c, 1);
     RollArgs a = roll_args(c, n * CAND_K);
     a.res = c->res_spec;
+    a.res_gb = c->res_gb;
+    a.slots = c->slots;
+    a.slot_rows = c->slot_rows;
+    a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
     HIPC(c, launch_rollout(st, SRC_SPEC, a));
   }
   SelArgs s;
   s.p = c->dp; s.tree = c->tree; s.cand = c->cand; s.ckey = c->ckey; s.ncand = c->ncand; s.res = c->res_spec;
-  s.regnodes = c->regnodes; s.gbflag = c->gbflag; s.so = c->so; s.B = n;
+  s.res_gb = c->res_gb; s.regnodes = c->regnodes; s.gbnodes = c->gbnodes; s.so = c->so; s.B = n;
   {
     KTimer kt(c, 2);
     HIPC(c, launch_select(st, s));
-  }
-  {
-    KTimer kt(c, 1);
-    RollArgs a = roll_args(c, n);
-    a.res = c->res_gb;
-    HIPC(c, launch_rollout(st, SRC_GB, a));
-  }
-  {
-    KTimer kt(c, 2);
-    HIPC(c, launch_gb_select(st, n, c->regnodes, c->gbflag, c->res_gb, c->gbnodes, c->so));
   }
   int L = n;
   if (exact && n > 1) {
@@ -630,17 +838,20 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
   return CLRRT_OK;
 }
 
-// Stages 6-7: compact the first L samples into node records (c->out_nodes), reserve arena rows,
-// replay accepted rollouts into the arena.  *n_out = records.
-static int compact_and_replay(clrrt_ctx* c, int L, int* n_out) {
+// Stages 5-6: compact the first L samples into node records (c->out_nodes), reserve arena rows,
+// copy the accepted trajectories into the arena.  *n_out = records.
+static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   hipStream_t st = c->stream;
   {
     KTimer kt(c, 2);
     HIPC(c, launch_compact(st, L, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
                            c->out_nodes, c->jobs, c->totals));
+    if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
   }
   HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));
+  if (merge_bbox) HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
+  if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
   c->counters.sim_count += c->h_totals[2];
@@ -650,10 +861,9 @@ static int compact_and_replay(clrrt_ctx* c, int L, int* n_out) {
   c->counters.rollouts += c->h_totals[6];
   c->last_goal_nodes = c->h_totals[7];
   {
-    KTimer kt(c, 1);
-    RollArgs a = roll_args(c, (int)nn);
-    a.res = c->res_replay;
-    HIPC(c, launch_rollout(st, SRC_LIST, a));
+    KTimer kt(c, 2);
+    HIPC(c, launch_copy_rows(st, c->jobs, c->out_nodes, (int)nn, c->slots, c->slot_rows,
+                             (int)(c->cap.max_batch * CAND_K), c->arena));
   }
   c->n_rows += nr;
   c->last_eval_rows = nr;
@@ -685,7 +895,7 @@ int clrrt_round_eval(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, void*
   int L = n, rc;
   if ((rc = eval_samples(c, n, false, &L)) != CLRRT_OK) return rc;
   int nn = 0;
-  if ((rc = compact_and_replay(c, L, &nn)) != CLRRT_OK) return rc;
+  if ((rc = compact_and_copy(c, L, &nn, false)) != CLRRT_OK) return rc;
   if (dev_out && nn > 0)
     HIPC(c, hipMemcpyAsync(dev_out, c->out_nodes, sizeof(clrrt_node) * nn, hipMemcpyDeviceToDevice, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
@@ -700,7 +910,12 @@ int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t l
   HIPC(c, hipSetDevice(c->device));
   int rc = append_nodes(c, (const clrrt_node*)dev_nodes, n);
   if (rc != CLRRT_OK) return rc;
+  if (n > 0) {
+    HIPC(c, launch_bbox(c->stream, (const clrrt_node*)dev_nodes, nullptr, n, c->d_bbox));
+    HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPC(c, hipStreamSynchronize(c->stream));
+  if (n > 0) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   return CLRRT_OK;
 }
 
@@ -744,7 +959,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
     int L = nb, nn = 0;
     if ((rc = eval_samples(c, nb, exact, &L)) != CLRRT_OK) break;
-    if ((rc = compact_and_replay(c, L, &nn)) != CLRRT_OK) break;
+    if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     for (int j = 0; j < L; j++) {
       pending.pop_front();
@@ -837,21 +1052,18 @@ int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double*
   return CLRRT_OK;
 }
 
-int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t* out_ids, float* out_keys) {
+int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t mode, int32_t* out_ids,
+                   float* out_keys) {
   if (!c || n < 0 || (n > 0 && (!samples || !out_ids))) return CLRRT_EINVAL;
+  if (mode != CLRRT_MODE_EXACT && mode != CLRRT_MODE_BATCH) return CLRRT_EINVAL;
   if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
   memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
   HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
-  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
-  int rc = ensure_sort_scratch(c, (int64_t)n * c->n_nodes);
-  if (rc != CLRRT_OK) return rc;
-  {
-    KTimer kt(c, 0);
-    HIPC(c, launch_nn(c->stream, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                      c->ncand, c->ctie, max_chunks, c->sort_scratch));
-  }
+  int rc = CLRRT_OK;
+  if (mode == CLRRT_MODE_EXACT && (rc = ensure_sort_scratch(c, (int64_t)n * c->n_nodes)) != CLRRT_OK) return rc;
+  if ((rc = run_nn(c, n, mode == CLRRT_MODE_EXACT ? c->sort_scratch : nullptr)) != CLRRT_OK) return rc;
   HIPC(c, hipMemcpyAsync(out_ids, c->cand, sizeof(int) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));
   if (out_keys)
     HIPC(c, hipMemcpyAsync(out_keys, c->ckey, sizeof(float) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));

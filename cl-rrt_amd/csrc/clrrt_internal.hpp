@@ -28,7 +28,12 @@ struct WorkCtr {
   uint32_t steps, scan, box;
 };
 
-// Explicit rollout job (parity entry, row replay).
+// A parent state passed by value so that it stays in registers.
+struct St10 {
+  double v[10];
+};
+
+// Explicit rollout job (parity entry) or row-copy job (commit: parent = slot job, gb = pass).
 struct Job {
   int32_t parent;   // tree node id, or sample index into the regular-node buffer when from_reg
   int32_t from_reg;
@@ -48,22 +53,35 @@ struct SampleOut {
 };
 
 // Job sources:
-//   SRC_SPEC : job j -> (sample s = j / K, candidate k = j % K), parent = tree node cand[s][k]
-//   SRC_GB   : job s -> goal-biased rollout from the regular node built for sample s (gbflag[s])
-//   SRC_LIST : explicit Job records (parity entry and row replay), parent = tree node or record
-enum { SRC_SPEC = 0, SRC_GB = 1, SRC_LIST = 2 };
+//   SRC_SPEC : job j -> (sample s = j / K, candidate k = j % K), parent = tree node cand[s][k];
+//              a successful regular rollout is followed in the same lane by the goal-biased one
+//   SRC_LIST : explicit Job records (parity entry), parent = tree node
+enum { SRC_SPEC = 0, SRC_LIST = 2 };
+
+// Uniform grid over the static obstacles (built on the host by clrrt_set_obstacles): cell
+// (gx, gy) lists, ascending, every static obstacle whose inflated bounding circle (radius + vehicle
+// radius + margin, the kernel's cull test) comes within a small tolerance of the cell.
+struct ObsGrid {
+  const uint32_t* start;  // [gw*gh + 1]
+  const uint16_t* items;
+  const uint16_t* mov;    // moving obstacles (tested at every step)
+  int gw, gh, nitems, nmov;
+  float x0, y0, inv;
+};
 
 struct RollArgs {
   DevParams p;
+  ObsGrid grid;
   const clrrt_node* __restrict__ tree;     // tree headers
   const clrrt_sample* __restrict__ samples;
   const int* __restrict__ cand;            // [B][K]
-  const clrrt_node* __restrict__ regnodes; // [B] regular nodes built by k_select
-  const int* __restrict__ gbflag;          // [B]
   const Job* __restrict__ jobs;
   const BakedObs* __restrict__ obs;
   double* __restrict__ arena;              // rows destination (LIST with row_off >= 0)
-  RollRes* __restrict__ res;
+  double* __restrict__ slots;              // SPEC rows, see k_rollout
+  int slot_rows, slot_jobs;
+  RollRes* __restrict__ res;               // regular rollout of each job
+  RollRes* __restrict__ res_gb;            // SPEC: goal-biased rollout (outcome -1 = not run)
   unsigned long long* ctr;  // [3] steps, scan points, box tests (nullable)
   int njobs;
 };
@@ -75,27 +93,59 @@ struct SelArgs {
   const float* __restrict__ ckey;
   const int* __restrict__ ncand;
   const RollRes* __restrict__ res;   // [B][K]
+  const RollRes* __restrict__ res_gb; // [B][K]
   clrrt_node* regnodes;              // [B]
-  int* gbflag;                       // [B]
+  clrrt_node* gbnodes;               // [B]
   SampleOut* so;                     // [B]
   int B;
 };
+
+// Spatial index of the tree for the nearest-node search (clrrt_nngrid.hip): nodes bucketed by a
+// uniform grid of gw x gh cells (multiples of 8) of size cs from (x0, y0), numbered super-cell-major
+// (8x8 cells per super-cell, super-cell (X, Y) = cells [64 (Y sw + X), 64 (Y sw + X) + 64));
+// cell ncell collects the nodes outside the grid.
+struct NnGrid {
+  double x0, y0, cs, inv, slack;
+  int gw, gh, sw, sh, ncell;
+  const uint32_t* start;  // [ncell + 2]: cell c holds recs[start[c] .. start[c+1])
+  const NnRec* recs;      // node records ordered by cell
+  const uint32_t* cmin;   // per cell: min costE (order-preserving encoding)
+  const uint32_t* smin;   // per super-cell
+  const uint32_t* gmin;   // [1] over all super-cells
+  const uint32_t* fmin;   // per super-cell [4] (int32): floor of min ref.back() x, y [mm], ang_par [urad]
+                          // in (-pi, pi] and shifted to [0, 2pi)
+  const uint32_t* fmax;   // per super-cell [4] (int32): ceil of the maxima
+};
+struct NnGridBufs {
+  int* cellid;
+  uint32_t *count, *fill, *start, *cmin, *smin, *fmin, *fmax;
+  NnRec* sorted;
+  uint32_t *scount, *sfill, *sstart;  // sample buckets [2 * super-cells + 2]
+  int* order;                         // [max_batch] samples ordered by bucket
+};
+hipError_t launch_nn_grid_build(hipStream_t st, const NnRec* nodes, int N, NnGrid& g, NnGridBufs& b);
+hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, const DevParams& p,
+                                 int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
+                                 int* fb_count, NnGridBufs& b, unsigned long long* stats);
 
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
 // selection involves equal keys are re-sorted with the replay of std::sort.
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
-                     int max_chunks, KeyId* exact_scratch);
+                     int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
+                     int* fb_count, unsigned long long* stats);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
-hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const int* gbflag,
-                            const RollRes* gbres, clrrt_node* gbnodes, SampleOut* so);
+hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
+                            int slot_rows, int slot_jobs, double* arena);
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                            const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
                            int* first);
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
                           clrrt_node* out, Job* jobs, int64_t* totals);
+// Bounding box (x0, y0, x1, y1) of the finite positions of recs[0 .. n), n = *n_dev when non-null.
+hipError_t launch_bbox(hipStream_t st, const clrrt_node* recs, const int64_t* n_dev, int n_host, double* out4);
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn);
 hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out);
 hipError_t launch_init_root(hipStream_t st, const double* state, clrrt_node* tree, NnRec* nn, double* arena);

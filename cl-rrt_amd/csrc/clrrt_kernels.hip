@@ -46,15 +46,19 @@ __device__ __forceinline__ void topk_insert(float (&keys)[NN_K], int (&ids)[NN_K
   }
 }
 
+// sidx != nullptr: lanes t < *scount search sample sidx[t] (the grid search's over-budget samples).
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, float* __restrict__ pk,
-                                                    int* __restrict__ pi) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+                                                    int* __restrict__ pi, const int* __restrict__ sidx,
+                                                    const int* __restrict__ scount) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
   const int n0 = c * chunk;
   const int n1 = min(N, n0 + chunk);
-  const bool act = s < B;
+  if (sidx && (int)(blockIdx.x * blockDim.x) >= *scount) return;
+  const bool act = sidx ? t < *scount : t < B;
+  const int s = act && sidx ? sidx[t] : t;
   double sx = 0, sy = 0;
   int ex = 1;
   if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
@@ -76,7 +80,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
     }
   }
   if (act) {
-    size_t base = ((size_t)s * nchunks + c) * NN_K;
+    size_t base = ((size_t)t * nchunks + c) * NN_K;
 #pragma unroll
     for (int j = 0; j < NN_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
   }
@@ -84,15 +88,17 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
 
 __global__ void k_nn_merge(int B, int nchunks, int limit, const float* __restrict__ pk,
                            const int* __restrict__ pi, int* __restrict__ cand, float* __restrict__ ckey,
-                           int* __restrict__ ncand, int* __restrict__ ctie) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= B) return;
+                           int* __restrict__ ncand, int* __restrict__ ctie, const int* __restrict__ sidx,
+                           const int* __restrict__ scount) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sidx ? t >= *scount : t >= B) return;
+  const int s = sidx ? sidx[t] : t;
   float keys[NN_K];
   int ids[NN_K];
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
   for (int c = 0; c < nchunks; c++) {
-    size_t base = ((size_t)s * nchunks + c) * NN_K;
+    size_t base = ((size_t)t * nchunks + c) * NN_K;
     for (int j = 0; j < NN_K; j++) {
       int id = pi[base + j];
       if (id == 0x7fffffff) break;
@@ -159,13 +165,41 @@ struct ObsView {
   const BakedObs* __restrict__ g;  // global baked records
   const float4* cv;                // LDS: (cx, cy, vx, vy) float
   const float* rad;                // LDS: bounding radius + vehicle radius + margin
-  int n;
+  const uint32_t* gstart;          // LDS: grid cell -> first item (gw*gh + 1)
+  const uint16_t* gitems;          // LDS: static obstacle ids per cell, ascending
+  const uint16_t* gmov;            // LDS: moving obstacle ids, ascending
+  int n;                           // obstacles (0: collision checking off)
+  int gw, gh, nmov;                // grid shape (gw == 0: no grid), moving obstacles
+  float gx0, gy0, ginv;            // grid origin and 1 / cell size
 };
 
 #define VEH_RAD 2.6220219f  /* sqrt(2.424^2 + 1^2), vehicle half-diagonal */
 #define CULL_MARGIN 0.05f
 
+// One obstacle against the vehicle box: bounding-circle cull (no overlap possible when the
+// circles are apart), then the SAT gap.
+__device__ __forceinline__ float obs_gap(const Box4& veh, const ObsView& ov, int j, double t, float ft,
+                                         float fvx, float fvy, bool cull, bool& culled) {
+  culled = false;
+  if (cull) {
+    float4 q = ov.cv[j];
+    float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
+    float rr = ov.rad[j];
+    if (dx * dx + dy * dy > rr * rr) { culled = true; return 1.0f; }
+  }
+  const BakedObs& o = ov.g[j];
+  if (!o.moving) return sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
+  float bvx[4], bvy[4], bnx[4], bny[4];
+  box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
+  return sat_gap(veh, bvx, bvy, bnx, bny);
+}
+
 // checkObsDistance (stub collisioncheck.cpp:6-8 | OBB old_collisioncheck.cpp:24-51).
+// Without the gap value (NEED_GAP false) only obstacles whose inflated bounding circle can reach
+// the vehicle are tested: static ones come from the uniform grid cell of the vehicle centre (its
+// list is a superset of every obstacle whose circle test can pass anywhere in the cell), moving
+// ones from their own list; both lists ascend, and they are merged so the first overlap found is
+// the reference's first overlap in obstacle order.  `tests` counts the reference's box tests.
 template <bool NEED_GAP>
 __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p, const ObsView& ov,
                                                uint32_t& tests) {
@@ -178,27 +212,36 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
   Box4 veh;
   box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
   const float fvx = (float)vpx, fvy = (float)vpy, ft = (float)t;
+  if (!NEED_GAP && ov.gw > 0 && isfinite(fvx) && isfinite(fvy) && isfinite(ft)) {
+    int a = 0, ae = 0;
+    const int gx = (int)floorf((fvx - ov.gx0) * ov.ginv), gy = (int)floorf((fvy - ov.gy0) * ov.ginv);
+    if (gx >= 0 && gx < ov.gw && gy >= 0 && gy < ov.gh) {
+      const int cell = gy * ov.gw + gx;
+      a = ov.gstart[cell];
+      ae = ov.gstart[cell + 1];
+    }
+    int b = 0;
+    while (a < ae || b < ov.nmov) {
+      const int ja = a < ae ? (int)ov.gitems[a] : 0x7fffffff;
+      const int jb = b < ov.nmov ? (int)ov.gmov[b] : 0x7fffffff;
+      int j;
+      if (ja < jb) { j = ja; a++; } else { j = jb; b++; }
+      bool culled;
+      float D = obs_gap(veh, ov, j, t, ft, fvx, fvy, true, culled);
+      if (!culled && D == 0) { tests += j + 1; return 0.0; }
+    }
+    tests += ov.n;  // the reference tests every obstacle until the first overlap
+    return 10000;
+  }
   double best = 10000;
   for (int j = 0; j < ov.n; j++) {
-    if (!NEED_GAP) {
-      float4 q = ov.cv[j];
-      float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
-      float rr = ov.rad[j];
-      if (dx * dx + dy * dy > rr * rr) continue;  // bounding circles apart: no overlap possible
-    }
-    const BakedObs& o = ov.g[j];
-    float D;
-    if (!o.moving) {
-      D = sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
-    } else {
-      float bvx[4], bvy[4], bnx[4], bny[4];
-      box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
-      D = sat_gap(veh, bvx, bvy, bnx, bny);
-    }
+    bool culled;
+    float D = obs_gap(veh, ov, j, t, ft, fvx, fvy, !NEED_GAP, culled);
+    if (culled) continue;
     if (D == 0) { tests += j + 1; return 0.0; }
     if (NEED_GAP && (double)D < best) best = D;
   }
-  tests += ov.n;  // the reference tests every obstacle until the first overlap
+  tests += ov.n;
   return best;
 }
 
@@ -264,32 +307,36 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   return -1;
 }
 
-__device__ __forceinline__ void store_row(double* __restrict__ row, const Roll& r, double c7, double c8,
-                                          double c9) {
-  row[0] = r.x0; row[1] = r.x1; row[2] = r.x2; row[3] = r.x3; row[4] = r.x4;
-  row[5] = r.x5; row[6] = r.x6; row[7] = c7; row[8] = c8; row[9] = c9;
+// One stateArray row; es = element stride (1 for row-major rows, the job count for the slot
+// layout in which consecutive lanes' values are adjacent, so a wave's stores coalesce).
+__device__ __forceinline__ void store_row(double* __restrict__ row, int64_t es, const Roll& r, double c7,
+                                          double c8, double c9) {
+  row[0] = r.x0; row[es] = r.x1; row[2 * es] = r.x2; row[3 * es] = r.x3; row[4 * es] = r.x4;
+  row[5 * es] = r.x5; row[6 * es] = r.x6; row[7 * es] = c7; row[8 * es] = c8; row[9 * es] = c9;
 }
 
 // One whole rollout.  `ps` = parent state (10 doubles), (pbx, pby) = parent ref.back(),
-// pvb = parent ref.v.back().  rows (nullable) receives stateArray.
+// pvb = parent ref.v.back().  rows (nullable) receives stateArray: element k of row i at
+// rows[(i * 10 + k) * es].
 template <bool NEED_GAP>
-__device__ void run_rollout(const double* ps, double pbx, double pby, double pvb, int gb, double sx,
+__device__ __forceinline__ void run_rollout(const St10& ps, double pbx, double pby, double pvb, int gb, double sx,
                             double sy, const DevParams& p, const ObsView& ov, double* __restrict__ rows,
-                            RollRes& out, WorkCtr& w) {
+                            int64_t es, RollRes& out, WorkCtr& w) {
   RefD R = gb ? make_goal_ref(pbx, pby, p) : make_ref(pbx, pby, sx, sy, p);
   Roll r;
-  roll_init(r, ps, R, pvb, gb != 0, p);
-  double c7 = (double)r.wp, c8 = ps[8], c9 = ps[9];
+  roll_init(r, ps.v, R, pvb, gb != 0, p);
+  double c7 = (double)r.wp, c8 = ps.v[8], c9 = ps.v[9];
   if (rows) {
-    for (int k = 0; k < 10; k++) rows[k] = ps[k];
-    rows[7] = c7;
+#pragma unroll
+    for (int k = 0; k < 10; k++) rows[k * es] = ps.v[k];
+    rows[7 * es] = c7;
   }
   int outcome = CLRRT_ROLL_ITERLIMIT;
   int steps = 0;
   for (int i = 0; i < p.n_steps_max; i++) {
     steps++;
     int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9, w);
-    if (rows) store_row(rows + (size_t)steps * 10, r, c7, c8, c9);
+    if (rows) store_row(rows + (int64_t)steps * 10 * es, es, r, c7, c8, c9);
     if (o >= 0) { outcome = o; break; }
   }
   out.st[0] = r.x0; out.st[1] = r.x1; out.st[2] = r.x2; out.st[3] = r.x3; out.st[4] = r.x4;
@@ -306,61 +353,111 @@ __device__ void run_rollout(const double* ps, double pbx, double pby, double pvb
 }
 
 
+// feasibleGoalBias rrtplanner.cpp:292-
+__device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const double* st, double bx,
+                                                   double by) {
+  bool outL = sqrt((st[0] - p.gbLx) * (st[0] - p.gbLx) + (st[1] - p.gbLy) * (st[1] - p.gbLy)) > p.gbR2;
+  bool outR = sqrt((st[0] - p.gbRx) * (st[0] - p.gbRx) + (st[1] - p.gbRy) * (st[1] - p.gbRy)) > p.gbR2;
+  double aRef = atan2(p.g1 - by, p.g0 - bx);
+  double h1 = fabs(wrap_pi(p.g2 - aRef));
+  double h2 = fabs(wrap_pi(p.g2 + M_PI - aRef));
+  double m = mn(h1, h2);
+  double cv = glibc::cos(p.g2 + M_PI_2 - aRef);
+  double sg = (double)((0.0 < cv) - (cv < 0.0));
+  double ang = sg * m;
+  bool within = fabs(ang) < (M_PI_4 / 2);
+  return outL && outR && within;
+}
+
+// Rollout jobs (Simulation::propagate, rrt/src/simulation.cpp:26-...).
+//   SRC_SPEC: job j = (sample j / K, candidate j % K), parent = tree node cand[j]; after a successful
+//             regular rollout whose end passes the goal-bias gate the same lane runs the goal-biased
+//             rollout from the node it would append (expandTree rrtplanner.cpp:163-173), so goal
+//             bias overlaps other samples' candidates instead of forming a serial tail.  Rows go to
+//             job slots, interleaved across jobs: element k of row i of job j, pass p (0 regular,
+//             1 goal-biased) at slots[((p * slot_rows + i) * 10 + k) * slot_jobs + j].
+//   SRC_LIST: explicit jobs (parity entry): parent = tree node, rows to arena[row_off] when >= 0.
 template <int SRC, bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
   extern __shared__ float4 lds[];
   float4* cv = lds;
   float* rad = (float*)(lds + a.p.n_obs);
+  uint32_t* gstart = (uint32_t*)(rad + a.p.n_obs);
+  const int ncell = a.grid.gw * a.grid.gh;
+  uint16_t* gitems = (uint16_t*)(gstart + (a.grid.gw > 0 ? ncell + 1 : 0));
+  uint16_t* gmov = gitems + a.grid.nitems;
   if (a.p.coll_mode == CLRRT_COLLISION_OBB && !NEED_GAP) {
     for (int j = threadIdx.x; j < a.p.n_obs; j += blockDim.x) {
       const BakedObs& o = a.obs[j];
       cv[j] = make_float4((float)o.cx, (float)o.cy, (float)o.vlx, (float)o.vly);
-      float rr = o.brad + VEH_RAD + CULL_MARGIN;
-      rad[j] = rr;
+      rad[j] = o.brad + VEH_RAD + CULL_MARGIN;
+    }
+    if (a.grid.gw > 0) {
+      for (int j = threadIdx.x; j <= ncell; j += blockDim.x) gstart[j] = a.grid.start[j];
+      for (int j = threadIdx.x; j < a.grid.nitems; j += blockDim.x) gitems[j] = a.grid.items[j];
+      for (int j = threadIdx.x; j < a.grid.nmov; j += blockDim.x) gmov[j] = a.grid.mov[j];
     }
     __syncthreads();
   }
-  ObsView ov{a.obs, cv, rad, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0};
+  ObsView ov{a.obs, cv, rad, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
+             a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   WorkCtr w{0, 0, 0};
   bool act = j < a.njobs;
-  const double* ps = nullptr;
+  St10 ps;
   double pbx = 0, pby = 0, pvb = 0, sx = 0, sy = 0;
   int gb = 0;
   double* rows = nullptr;
+  int64_t es = 1;
+  const int64_t pass_stride = (int64_t)a.slot_rows * 10 * a.slot_jobs;
   if (act) {
+    const clrrt_node* n = nullptr;
     if (SRC == SRC_SPEC) {
-      int s = j / CAND_K;
-      int id = a.cand[j];
+      const int id = a.cand[j];
       if (id < 0) {
         a.res[j].outcome = -1;
+        a.res_gb[j].outcome = -1;
         act = false;
       } else {
-        const clrrt_node& n = a.tree[id];
-        ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
-        sx = a.samples[s].x; sy = a.samples[s].y;
-      }
-    } else if (SRC == SRC_GB) {
-      if (!a.gbflag[j]) {
-        a.res[j].outcome = -1;
-        act = false;
-      } else {
-        const clrrt_node& n = a.regnodes[j];
-        ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
-        gb = 1;
+        n = &a.tree[id];
+        sx = a.samples[j / CAND_K].x;
+        sy = a.samples[j / CAND_K].y;
+        if (a.slots) { rows = a.slots + j; es = a.slot_jobs; }
       }
     } else {
       const Job& jb = a.jobs[j];
-      const clrrt_node& n = jb.from_reg ? a.regnodes[jb.parent] : a.tree[jb.parent];
-      ps = n.state; pbx = n.ref_back[0]; pby = n.ref_back[1]; pvb = n.ref_vback;
+      n = &a.tree[jb.parent];
       gb = jb.gb; sx = jb.sx; sy = jb.sy;
       if (jb.row_off >= 0) rows = a.arena + (size_t)jb.row_off * 10;
     }
+    if (n) {
+#pragma unroll
+      for (int k = 0; k < 10; k++) ps.v[k] = n->state[k];
+      pbx = n->ref_back[0]; pby = n->ref_back[1]; pvb = n->ref_vback;
+    }
   }
   if (act) {
-    RollRes out;
-    run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, out, w);
-    a.res[j] = out;
+    for (int pass = 0; pass < 2; pass++) {
+      RollRes out;
+      run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, es, out, w);
+      if (pass == 1) {
+        a.res_gb[j] = out;
+        break;
+      }
+      a.res[j] = out;
+      if (SRC != SRC_SPEC) break;
+      const bool ok = (out.outcome == CLRRT_ROLL_END || out.outcome == CLRRT_ROLL_GOAL) &&
+                      feasible_goal_bias(a.p, out.st, out.bx, out.by);
+      if (!ok) {
+        a.res_gb[j].outcome = -1;
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < 10; k++) ps.v[k] = out.st[k];
+      pbx = out.bx; pby = out.by; pvb = out.vback;
+      gb = 1;
+      if (a.slots) rows = a.slots + pass_stride + j;
+    }
   }
   if (a.ctr) {  // algorithmic work counters (roofline): block reduction, one atomic per block
     __shared__ __attribute__((aligned(16))) unsigned long long s_ctr[4];
@@ -379,21 +476,6 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
 // --------------------------------------------------------------------------------------------
 // selection, goal bias, conflicts
 // --------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const double* st, double bx,
-                                                   double by) {
-  bool outL = sqrt((st[0] - p.gbLx) * (st[0] - p.gbLx) + (st[1] - p.gbLy) * (st[1] - p.gbLy)) > p.gbR2;
-  bool outR = sqrt((st[0] - p.gbRx) * (st[0] - p.gbRx) + (st[1] - p.gbRy) * (st[1] - p.gbRy)) > p.gbR2;
-  double aRef = atan2(p.g1 - by, p.g0 - bx);
-  double h1 = fabs(wrap_pi(p.g2 - aRef));
-  double h2 = fabs(wrap_pi(p.g2 + M_PI - aRef));
-  double m = mn(h1, h2);
-  double cv = glibc::cos(p.g2 + M_PI_2 - aRef);
-  double sg = (double)((0.0 < cv) - (cv < 0.0));
-  double ang = sg * m;
-  bool within = fabs(ang) < (M_PI_4 / 2);
-  return outL && outR && within;
-}
-
 __device__ __forceinline__ void fill_node(clrrt_node& n, const RollRes& r, int parent, float pcE,
                                           float pcS) {
   for (int k = 0; k < 10; k++) n.state[k] = r.st[k];
@@ -411,6 +493,7 @@ __device__ __forceinline__ void fill_node(clrrt_node& n, const RollRes& r, int p
 }
 
 
+// The first candidate whose rollout succeeded (expandTree :150-160) and its goal-biased follow-up.
 __global__ void k_select(SelArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.B) return;
@@ -428,7 +511,7 @@ __global__ void k_select(SelArgs a) {
   }
   // EXACT-mode conflict threshold: the key a new node must beat (<=) to be tried before the result.
   o.thr = o.k >= 0 ? a.ckey[s * CAND_K + o.k] : (nc == a.p.sort_limit ? a.ckey[s * CAND_K + nc - 1] : __builtin_inff());
-  int gbf = 0;
+  o.gb_ok = 0;
   if (o.k >= 0) {
     const int pid = a.cand[s * CAND_K + o.k];
     const clrrt_node& par = a.tree[pid];
@@ -436,34 +519,23 @@ __global__ void k_select(SelArgs a) {
     fill_node(n, a.res[s * CAND_K + o.k], pid, par.costE, par.costS);
     a.regnodes[s] = n;
     o.nrows_reg = n.nrows;
-    gbf = feasible_goal_bias(a.p, n.state, n.ref_back[0], n.ref_back[1]);
-  }
-  a.gbflag[s] = gbf;
-  a.so[s] = o;
-}
-
-__global__ void k_gb_select(int B, const clrrt_node* __restrict__ regnodes, const int* __restrict__ gbflag,
-                            const RollRes* __restrict__ gbres, clrrt_node* gbnodes, SampleOut* so) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= B) return;
-  SampleOut o = so[s];
-  o.gb_ok = 0;
-  if (gbflag[s]) {
-    const RollRes& r = gbres[s];
-    o.rollouts++;
-    o.steps += r.nrows - 1;
-    o.f_col += r.outcome == CLRRT_ROLL_COLLISION;
-    o.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
-    o.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
-    if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL) {
-      clrrt_node n;
-      fill_node(n, r, CLRRT_PARENT_PREV, regnodes[s].costE, regnodes[s].costS);
-      gbnodes[s] = n;
-      o.gb_ok = 1;
-      o.nrows_gb = n.nrows;
+    const RollRes& g = a.res_gb[s * CAND_K + o.k];
+    if (g.outcome >= 0) {  // the gate passed and the goal-biased rollout ran (:163-173)
+      o.rollouts++;
+      o.steps += g.nrows - 1;
+      o.f_col += g.outcome == CLRRT_ROLL_COLLISION;
+      o.f_acc += g.outcome == CLRRT_ROLL_ACCLIMIT;
+      o.f_it += g.outcome == CLRRT_ROLL_ITERLIMIT;
+      if (g.outcome == CLRRT_ROLL_END || g.outcome == CLRRT_ROLL_GOAL) {
+        clrrt_node gn;
+        fill_node(gn, g, CLRRT_PARENT_PREV, n.costE, n.costS);
+        a.gbnodes[s] = gn;
+        o.gb_ok = 1;
+        o.nrows_gb = gn.nrows;
+      }
     }
   }
-  so[s] = o;
+  a.so[s] = o;
 }
 
 // EXACT mode: sample j conflicts when a node produced by an earlier sample of the round would sort
@@ -542,9 +614,9 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
       n.owner = rank;
       n.row_offset = row_base + row_off;
       out[node_off] = n;
-      Job jb;
-      jb.parent = cand[s * CAND_K + o.k]; jb.from_reg = 0; jb.gb = 0;
-      jb.sx = S[s].x; jb.sy = S[s].y;
+      Job jb;  // row copy: slot of job (s, k*) pass 0 -> arena
+      jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 0; jb.pad = 0;
+      jb.sx = 0; jb.sy = 0;
       jb.row_off = row_base + row_off;
       jobs[node_off] = jb;
       node_off++;
@@ -555,8 +627,8 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
       n.owner = rank;
       n.row_offset = row_base + row_off;
       out[node_off] = n;
-      Job jb;
-      jb.parent = s; jb.from_reg = 1; jb.gb = 1;
+      Job jb;  // row copy: slot of job (s, k*) pass 1 (goal-biased rollout) -> arena
+      jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 1; jb.pad = 0;
       jb.sx = 0; jb.sy = 0;
       jb.row_off = row_base + row_off;
       jobs[node_off] = jb;
@@ -570,6 +642,43 @@ __global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __r
     totals[1] = s_rows[t];
   }
   if (t < 6) totals[2 + t] = s_cnt[t];
+}
+
+// Move committed trajectories (Node::tra) from their job slots into the arena: one block per node.
+__global__ void __launch_bounds__(256) k_copy_rows(const Job* __restrict__ jobs, const clrrt_node* __restrict__ recs,
+                                                   const double* __restrict__ slots, int slot_rows, int slot_jobs,
+                                                   double* __restrict__ arena) {
+  const int i = blockIdx.x;
+  const Job jb = jobs[i];
+  const int n = recs[i].nrows * 10;
+  const double* src = slots + (int64_t)jb.gb * slot_rows * 10 * slot_jobs + jb.parent;
+  double* dst = arena + jb.row_off * 10;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) dst[t] = src[(int64_t)t * slot_jobs];
+}
+
+__global__ void __launch_bounds__(256) k_bbox(const clrrt_node* __restrict__ recs, const int64_t* n_dev, int n_host,
+                                              double* __restrict__ out4) {
+  __shared__ double s[4][256];
+  const int n = n_dev ? (int)*n_dev : n_host;
+  double v[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double x = recs[i].state[0], y = recs[i].state[1];
+    if (isfinite(x) && isfinite(y)) {
+      v[0] = fmin(v[0], x); v[1] = fmin(v[1], y); v[2] = fmax(v[2], x); v[3] = fmax(v[3], y);
+    }
+  }
+  for (int k = 0; k < 4; k++) s[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + off]);
+      s[1][threadIdx.x] = fmin(s[1][threadIdx.x], s[1][threadIdx.x + off]);
+      s[2][threadIdx.x] = fmax(s[2][threadIdx.x], s[2][threadIdx.x + off]);
+      s[3][threadIdx.x] = fmax(s[3][threadIdx.x], s[3][threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) out4[threadIdx.x] = s[threadIdx.x][0];
 }
 
 // RRT.addNode for n records: resolve GB parents (CLRRT_PARENT_PREV -> the record before) and build
@@ -588,7 +697,7 @@ __global__ void k_append(const clrrt_node* __restrict__ in, int n, int64_t base,
   float ang = (float)(-d.state[2] - 0.0);
   r.c = cosf(ang); r.s = sinf(ang);
   r.costE = d.costE;
-  r.pad = 0.f;
+  r.id = (int32_t)(base + i);
   nn[base + i] = r;
 }
 
@@ -615,7 +724,7 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   NnRec r;
   r.x = n.state[0]; r.y = n.state[1]; r.bx = x; r.by = 0.0; r.ang_par = n.ang_par;
   float ang = (float)(-n.state[2] - 0.0);
-  r.c = cosf(ang); r.s = sinf(ang); r.costE = 0.f; r.pad = 0.f;
+  r.c = cosf(ang); r.s = sinf(ang); r.costE = 0.f; r.id = 0;
   nn[0] = r;
 }
 
@@ -660,21 +769,32 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     if (e__ != hipSuccess) return e__;                   \
   } while (0)
 
+static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                  const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
+                                  int* ctie, int max_chunks, const int* sidx, const int* scount);
+
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
-                     int max_chunks, KeyId* exact_scratch) {
-  int groups = (B + 255) / 256;
-  int nchunks = (N + 255) / 256;
-  int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
-  nchunks = max(1, min(nchunks, min(want, max_chunks)));
-  int chunk = (N + nchunks - 1) / nchunks;
-  nchunks = (N + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, pk, pi);
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
-                     cand, ckey, ncand, ctie);
-  LAUNCH_CHECK();
+                     int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
+                     int* fb_count, unsigned long long* stats) {
+  if (grid) {
+    // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
+    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    const int cap = max(2048, N / 64);
+    e = launch_nn_grid_search(st, S, B, *grid, p, cand, ckey, ncand, ctie, cap, fb_list, fb_count, *gbufs, stats);
+    if (e != hipSuccess) return e;
+    if (stats) {
+      e = hipMemcpyAsync(stats + 4, fb_count, sizeof(int), hipMemcpyDeviceToDevice, st);  // low word: fallbacks
+      if (e != hipSuccess) return e;
+    }
+    e = launch_nn_brute(st, S, B, nodes, N, p, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
+    if (e != hipSuccess) return e;
+  } else {
+    hipError_t e = launch_nn_brute(st, S, B, nodes, N, p, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr,
+                                   nullptr);
+    if (e != hipSuccess) return e;
+  }
   if (exact_scratch) {
     hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, exact_scratch,
                        cand, ckey, ncand);
@@ -683,10 +803,34 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
   return hipSuccess;
 }
 
+static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                  const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
+                                  int* ctie, int max_chunks, const int* sidx, const int* scount) {
+  int groups = (B + 255) / 256;
+  int nchunks = (N + 255) / 256;
+  int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
+  nchunks = max(1, min(nchunks, min(want, max_chunks)));
+  int chunk = (N + nchunks - 1) / nchunks;
+  nchunks = (N + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
+                     p, pk, pi, sidx, scount);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
+                     cand, ckey, ncand, ctie, sidx, scount);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 template <int SRC>
 static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   if (a.njobs <= 0) return hipSuccess;
-  size_t lds = (a.p.coll_mode == CLRRT_COLLISION_OBB) ? (size_t)a.p.n_obs * (sizeof(float4) + sizeof(float)) : 0;
+  size_t lds = 0;
+  if (a.p.coll_mode == CLRRT_COLLISION_OBB) {
+    lds = (size_t)a.p.n_obs * (sizeof(float4) + sizeof(float));
+    if (a.grid.gw > 0)
+      lds += sizeof(uint32_t) * ((size_t)a.grid.gw * a.grid.gh + 1) +
+             sizeof(uint16_t) * ((size_t)a.grid.nitems + a.grid.nmov);
+  }
   dim3 grid((a.njobs + 255) / 256), block(256);
   if (a.p.need_gap)
     hipLaunchKernelGGL((k_rollout<SRC, true>), grid, block, 0, st, a);
@@ -698,7 +842,6 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
 
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
   if (src == SRC_SPEC) return launch_roll_t<SRC_SPEC>(st, a);
-  if (src == SRC_GB) return launch_roll_t<SRC_GB>(st, a);
   return launch_roll_t<SRC_LIST>(st, a);
 }
 
@@ -708,9 +851,10 @@ hipError_t launch_select(hipStream_t st, const SelArgs& a) {
   return hipSuccess;
 }
 
-hipError_t launch_gb_select(hipStream_t st, int B, const clrrt_node* reg, const int* gbflag,
-                            const RollRes* gbres, clrrt_node* gbnodes, SampleOut* so) {
-  hipLaunchKernelGGL(k_gb_select, dim3((B + 255) / 256), dim3(256), 0, st, B, reg, gbflag, gbres, gbnodes, so);
+hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
+                            int slot_rows, int slot_jobs, double* arena) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_rows, dim3(n), dim3(256), 0, st, jobs, recs, slots, slot_rows, slot_jobs, arena);
   LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -728,6 +872,12 @@ hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const in
                           clrrt_node* out, Job* jobs, int64_t* totals) {
   hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, L, S, cand, reg, gbn, so, row_base, rank, out, jobs,
                      totals);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_bbox(hipStream_t st, const clrrt_node* recs, const int64_t* n_dev, int n_host, double* out4) {
+  hipLaunchKernelGGL(k_bbox, dim3(1), dim3(256), 0, st, recs, n_dev, n_host, out4);
   LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 1
+#define CLRRT_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -236,7 +236,10 @@ int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t
 /* ---- kernel-level parity entries ---- */
 int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n,
                         clrrt_rollout_result* out, double* rows_out, int32_t rows_cap);
-int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t* out_ids,
+/* Candidate lists (<= sortLimit node ids per sample, ascending key).  mode CLRRT_MODE_EXACT orders
+ * equal keys as the reference's std::sort does (replayed per tied sample, O(n * tree) scratch);
+ * CLRRT_MODE_BATCH orders them by node index. */
+int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t mode, int32_t* out_ids,
                    float* out_keys);
 
 /* Test hook: evaluates, on the device, the elementary functions exactly as the kernels call them,
@@ -249,7 +252,7 @@ int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const doubl
 int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);
 int clrrt_reset_counters(clrrt_ctx* ctx);
 /* Algorithmic work done by rollout kernels since the last reset (SURVEY §8(d) roofline basis):
- * out[0] = simulated steps (incl. speculative candidates and row replays), out[1] = reference
+ * out[0] = simulated steps (incl. speculative candidates), out[1] = reference
  * points scanned by findClosestPoint, out[2] = OBB box tests (first overlap ends a step's scan). */
 int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 
@@ -258,6 +261,16 @@ int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
  * 2 = commit; returns the summed ms and the launch count. */
 int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
 int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
+
+/* Nearest-node search strategy: trees of at least `min_nodes` nodes are searched through the
+ * per-round spatial grid index, smaller ones by brute force (both return the identical candidate
+ * lists).  Default: never (the brute-force search is faster on the benchmark trees); 0 = always
+ * the grid. */
+int clrrt_set_nn_grid_threshold(clrrt_ctx* ctx, int64_t min_nodes);
+/* Diagnostics of the grid nearest-node search since the last clrrt_reset_counters: out[0] waves,
+ * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget,
+ * out[4] samples handed to brute force by the LAST search. */
+int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[8]);
 
 #ifdef __cplusplus
 }

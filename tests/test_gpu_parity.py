@@ -83,9 +83,10 @@ def test_rollout_parity(kind):
     assert rate <= FLIP_RATE
 
 
-@pytest.mark.parametrize("kind", ["empty", "obb200"])
-def test_nearest_node_parity(kind):
+@pytest.mark.parametrize("kind,grid", [("empty", False), ("obb200", False), ("empty", True), ("obb200", True)])
+def test_nearest_node_parity(kind, grid):
     o, pl = _pair(kind, seed=4, iters=150)
+    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
     smp = list(clrrt.Rng(21).draw_samples(pl.params, 400))
     ids, keys = pl.sort_nodes_batch(smp)
     bad = 0
@@ -116,9 +117,11 @@ def _compare_trees(o, pl, label):
     return on, gn, first_bad
 
 
-@pytest.mark.parametrize("kind,seed,iters", [("empty", 1, 200), ("obb200", 3, 300), ("empty", 2, 300),
-                                             ("obb200", 5, 300), ("moving", 4, 250)])
-def test_exact_mode_tree_parity(kind, seed, iters):
+@pytest.mark.parametrize("kind,seed,iters,grid", [("empty", 1, 200, False), ("obb200", 3, 300, False),
+                                                  ("empty", 2, 300, False), ("obb200", 5, 300, False),
+                                                  ("moving", 4, 250, False), ("obb200", 3, 300, True),
+                                                  ("moving", 4, 250, True)])
+def test_exact_mode_tree_parity(kind, seed, iters, grid):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
     o = Oracle(abi.default_params(collision_mode=mode), obs)
@@ -127,6 +130,7 @@ def test_exact_mode_tree_parity(kind, seed, iters):
     o.expand(iters)
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 20,
                        max_batch=256)
+    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
     if obs is not None:
         pl.set_obstacles(obs)
     pl.tree_init()
@@ -150,8 +154,9 @@ def test_exact_mode_tree_parity(kind, seed, iters):
     assert bytes(ref.state) == bytes(rng.state)
 
 
-@pytest.mark.parametrize("kind,batch", [("empty", 64), ("obb200", 256), ("moving", 128)])
-def test_batch_mode_tree_parity(kind, batch):
+@pytest.mark.parametrize("kind,batch,grid", [("empty", 64, False), ("obb200", 256, False), ("moving", 128, False),
+                                              ("obb200", 256, True), ("moving", 128, True)])
+def test_batch_mode_tree_parity(kind, batch, grid):
     mode, obs = _scene(kind)
     iters = 4 * batch
     o = Oracle(abi.default_params(collision_mode=mode), obs)
@@ -160,6 +165,7 @@ def test_batch_mode_tree_parity(kind, batch):
     o.expand_batch(iters, batch, stable=True)
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 21,
                        max_batch=batch)
+    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
     if obs is not None:
         pl.set_obstacles(obs)
     pl.tree_init()
@@ -214,3 +220,61 @@ def _append_ref(o, ref_nodes, base):
         cur.append(nd)
     arr = (abi.Node * len(cur))(*cur)
     o.load_tree(arr)
+
+
+def _bitwise_report(gn, on, label):
+    """Count nodes whose FP64 state differs from the oracle's in any bit (expected: none)."""
+    diff = int(np.sum(np.any(gn["state"].view(np.uint64) != on["state"].view(np.uint64), axis=1)))
+    print(f"{label}: nodes with any state bit different: {diff}")
+    return diff
+
+
+@pytest.mark.parametrize("kind,seed,iters", [("obb200", 3, 300), ("moving", 4, 250)])
+def test_exact_mode_bitwise(kind, seed, iters):
+    """The EXACT-mode tree is bit-identical to the oracle's: node states, float costs, rows."""
+    mode, obs = _scene(kind)
+    o = Oracle(abi.default_params(collision_mode=mode), obs)
+    Oracle.srand(seed)
+    o.init_tree()
+    o.expand(iters)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 20,
+                       max_batch=256)
+    pl.set_obstacles(obs)
+    pl.tree_init()
+    pl.expand(clrrt.Rng(seed), n_iters=iters, mode=clrrt.CLRRT_MODE_EXACT, batch=256)
+    on, gn = o.nodes(), pl.nodes()
+    assert len(on["parent"]) == len(gn["parent"])
+    assert _bitwise_report(gn, on, f"{kind} seed {seed}") == 0
+    assert np.array_equal(gn["costE"].view(np.uint32), on["costE"].view(np.uint32))
+    assert np.array_equal(gn["costS"].view(np.uint32), on["costS"].view(np.uint32))
+    for i in range(1, len(on["parent"])):
+        rows = pl.rows(int(gn["row_offset"][i]), int(gn["nrows"][i]))
+        assert np.array_equal(rows.view(np.uint64), np.ascontiguousarray(o.rows(i)).view(np.uint64)), i
+
+
+def test_nn_grid_matches_brute_force_large_tree():
+    """Full-size property: on a BATCH-grown tree of ~100k nodes the grid search returns exactly the
+    brute-force candidate lists (ids and keys) for every sample of a 16384-sample batch."""
+    mode, obs = _scene("obb200")
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
+                       max_batch=16384)
+    pl.set_obstacles(obs)
+    pl.tree_init()
+    pl.expand(clrrt.Rng(9), n_iters=16384 * 8, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+    n_nodes = pl.size()[0]
+    assert n_nodes > 20000
+    smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
+    pl.set_nn_grid_threshold(1 << 40)
+    ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
+    pl.set_nn_grid_threshold(0)
+    ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
+    print(f"tree {n_nodes} nodes; lists equal: {np.array_equal(ids_b, ids_g)}")
+    assert np.array_equal(ids_b, ids_g)
+    assert np.array_equal(keys_b.view(np.uint32)[ids_b >= 0], keys_g.view(np.uint32)[ids_g >= 0])
+    # and against the oracle's std::sort on a subset
+    o = Oracle(abi.default_params(collision_mode=mode), obs)
+    o.load_tree(pl.nodes_raw())
+    for j in range(0, 16384, 1024):
+        s = smp[j]
+        cid, _ = o.sort_nodes(s.x, s.y, s.explore, stable=True)
+        assert [int(i) for i in ids_g[j] if i >= 0] == cid, j
