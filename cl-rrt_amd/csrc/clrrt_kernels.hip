@@ -46,12 +46,26 @@ __device__ __forceinline__ void topk_insert(float (&keys)[NN_K], int (&ids)[NN_K
   }
 }
 
+// Prune radius for a lane: a node at Euclidean distance |q| > R(kth - cost) cannot enter the list
+// (key >= |q| (1 - 1e-5) - 1e-4 with float rounding, see dubins_key; the radius used here is looser).
+__device__ __forceinline__ float prune_r2(float slack) {  // slack = kth (- cost)
+  const float r = (slack + 2e-4f) * (1.0f / 0.9999f);
+  return r < 0.f ? -1.f : r * r;  // -1: nothing can enter (d2 >= 0 > -1)
+}
+
+// Brute-force candidate lists: block = 256 samples x one chunk of nodes; the chunk is staged through
+// LDS 256 nodes at a time (coalesced loads, broadcast reads), each lane keeps its own top-11 and runs
+// the exact Dubins key / feasibleNode only for nodes that pass nn_prefilter.
 // sidx != nullptr: lanes t < *scount search sample sidx[t] (the grid search's over-budget samples).
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, float* __restrict__ pk,
                                                     int* __restrict__ pi, const int* __restrict__ sidx,
                                                     const int* __restrict__ scount) {
+  __shared__ double2 s_p[256];  // node x, y
+  __shared__ double2 s_b[256];  // ref.back() x, y
+  __shared__ float4 s_f[256];   // c, s, ca, sa
+  __shared__ float s_c[256];    // costE
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
   const int n0 = c * chunk;
@@ -66,17 +80,39 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   int ids[NN_K];
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
-  for (int n = n0; n < n1; n++) {
-    const NnRec rec = nodes[n];
-    float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
-    float lb = sqrtf(qx * qx + qy * qy) * 0.99999f - 1e-4f;
-    if (!ex) lb = rec.costE + lb;
-    if (act && lb <= keys[NN_K - 1]) {
-      float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
-      if (!ex) k = rec.costE + k;
-      if (lex_less(k, n, keys[NN_K - 1], ids[NN_K - 1]) &&
-          feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
-        topk_insert(keys, ids, k, n);
+  float r2 = __builtin_inff();  // explore: prune radius^2 for the current 11th key
+  const float feas2 = (float)(p.feas_len * (1 - 1e-6) * p.feas_len * (1 - 1e-6));
+  for (int b = n0; b < n1; b += 256) {
+    const int m = min(256, n1 - b);
+    __syncthreads();
+    if ((int)threadIdx.x < m) {
+      const NnRec& rec = nodes[b + threadIdx.x];
+      s_p[threadIdx.x] = make_double2(rec.x, rec.y);
+      s_b[threadIdx.x] = make_double2(rec.bx, rec.by);
+      s_f[threadIdx.x] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
+      s_c[threadIdx.x] = rec.costE;
+    }
+    __syncthreads();
+    if (!act) continue;
+    for (int k = 0; k < m; k++) {
+      const double2 np = s_p[k];
+      const float qx = (float)(sx - np.x), qy = (float)(sy - np.y);
+      const float d2 = qx * qx + qy * qy;
+      const float cost = s_c[k];
+      const float lim = ex ? r2 : prune_r2(keys[NN_K - 1] - cost);
+      if (!(d2 <= lim) && !(lim != lim)) continue;  // Euclidean prune (a NaN limit never prunes)
+      const float4 f = s_f[k];
+      const double2 bb = s_b[k];
+      if (!nn_prefilter(sx, sy, qx, qy, f.x, f.y, f.z, f.w, bb.x, bb.y, cost, ex, keys[NN_K - 1], feas2)) continue;
+      const int n = b + k;
+      const NnRec& rec = nodes[n];
+      float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+      if (!ex) key = rec.costE + key;
+      if (lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) &&
+          feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
+        topk_insert(keys, ids, key, n);
+        r2 = prune_r2(keys[NN_K - 1]);
+      }
     }
   }
   if (act) {
@@ -698,6 +734,7 @@ __global__ void k_append(const clrrt_node* __restrict__ in, int n, int64_t base,
   r.c = cosf(ang); r.s = sinf(ang);
   r.costE = d.costE;
   r.id = (int32_t)(base + i);
+  r.ca = cosf((float)d.ang_par); r.sa = sinf((float)d.ang_par);
   nn[base + i] = r;
 }
 
@@ -725,6 +762,7 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   r.x = n.state[0]; r.y = n.state[1]; r.bx = x; r.by = 0.0; r.ang_par = n.ang_par;
   float ang = (float)(-n.state[2] - 0.0);
   r.c = cosf(ang); r.s = sinf(ang); r.costE = 0.f; r.id = 0;
+  r.ca = cosf((float)n.ang_par); r.sa = sinf((float)n.ang_par);
   nn[0] = r;
 }
 

@@ -226,13 +226,16 @@ struct Lane {
 // Nodes recs[a .. b) (wave-uniform range) offered to the lanes with `take` set.
 __device__ __forceinline__ void scan_nodes(Lane& L, const NnRec* __restrict__ recs, uint32_t a, uint32_t b,
                                            bool take, double feas_len) {
+  const float feas2 = (float)(feas_len * (1 - 1e-6) * feas_len * (1 - 1e-6));
   for (uint32_t k = a; k < b; k++) {
     const NnRec rec = recs[k];
     if (!take) continue;
     float qx = (float)(L.sx - rec.x), qy = (float)(L.sy - rec.y);
     float lb = sqrtf(qx * qx + qy * qy) * 0.99999f - 1e-4f;
     if (!L.ex) lb = rec.costE + lb;
-    if (lb <= L.keys[NN_K - 1]) {
+    if (lb <= L.keys[NN_K - 1] &&
+        nn_prefilter(L.sx, L.sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, L.ex,
+                     L.keys[NN_K - 1], feas2)) {
       float key = dubins_key(L.sx, L.sy, rec.x, rec.y, rec.c, rec.s);
       if (!L.ex) key = rec.costE + key;
       if (lex_less2(key, rec.id, L.keys[NN_K - 1], L.ids[NN_K - 1]) &&
