@@ -57,8 +57,9 @@ _SIGS = {
     "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_kernel_time": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_int64)]),
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
-    "clrrt_set_nn_grid_threshold": (C.c_int, [C.c_void_p, C.c_int64]),
+    "clrrt_set_nn_grid": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
 }
 
 
@@ -305,15 +306,23 @@ class Planner:
     def enable_timing(self, on=True):
         self._chk(self.L.clrrt_enable_timing(self.h, 1 if on else 0), "enable_timing")
 
+    def set_option(self, key, value):
+        self._chk(self.L.clrrt_set_option(self.h, key.encode(), int(value)), f"set_option({key})")
+
     def nn_stats(self):
         out = (C.c_int64 * 8)()
         self._chk(self.L.clrrt_nn_stats(self.h, out), "nn_stats")
         return {"waves": out[0], "nodes_read": out[1], "rings": out[2], "truncated_waves": out[3],
                 "last_fallback_samples": out[4]}
 
+    def set_nn_grid(self, min_nodes, modes=1, wave_budget=0):
+        """Trees of >= min_nodes nodes search the samples of `modes` (1 explore, 2 optimize) through
+        the spatial grid (0: always; a huge value: never)."""
+        self._chk(self.L.clrrt_set_nn_grid(self.h, int(min_nodes), int(modes), int(wave_budget)), "set_nn_grid")
+
     def set_nn_grid_threshold(self, min_nodes):
-        """Trees of >= min_nodes nodes use the spatial-grid nearest-node search (0: always)."""
-        self._chk(self.L.clrrt_set_nn_grid_threshold(self.h, int(min_nodes)), "set_nn_grid_threshold")
+        """Grid search for both modes from min_nodes nodes (test helper)."""
+        self.set_nn_grid(min_nodes, 3, 0)
 
     def kernel_time(self, which):
         ms, n = C.c_double(), C.c_int64()

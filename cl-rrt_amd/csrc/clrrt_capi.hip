@@ -89,7 +89,16 @@ struct clrrt_ctx {
   double bbox[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   double* d_bbox = nullptr;  // [4] device result of launch_bbox
   double* h_bbox = nullptr;  // [4] pinned
-  int64_t nng_min_nodes = INT64_MAX;  // grid search off by default (see clrrt_set_nn_grid_threshold)
+  int64_t nng_min_nodes = INT64_MAX;  // clrrt_set_nn_grid: off by default (brute force is faster on bench trees)
+  int nng_modes = 1;
+  int nng_budget = 0;
+  // persistent rollouts (k_roll_prep + k_roll_run)
+  int roll_persistent = 1;
+  int roll_blocks = 0;       // persistent blocks (0: 2 per CU)
+  int n_cu = 256;
+  void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
+  int* roll_q = nullptr;      // [1] queue head
+  int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   double reg_x0 = 0, reg_y0 = 0, reg_x1 = 0, reg_y1 = 0;  // sampling region + margin
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
@@ -330,7 +339,7 @@ static void free_all(clrrt_ctx* c) {
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
                   c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
-                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->nng.scount, c->nng.sfill, c->nng.sstart,
+                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
                   c->nng.order};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -408,6 +417,14 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->nng.fmin, 4 * kNngMaxSuper));
   chk(dalloc(&c->nng.fmax, 4 * kNngMaxSuper));
   chk(dalloc(&c->fb_list, B));
+  chk(hipMalloc(&c->roll_prep, rollout_prep_bytes() * (size_t)B * CAND_K));
+  chk(dalloc(&c->roll_q, 1));
+  chk(dalloc(&c->roll_best, B));
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      c->n_cu = ncu;
+  }
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
   chk(dalloc(&c->fb_count, 1));
@@ -706,9 +723,20 @@ int clrrt_nn_stats(clrrt_ctx* c, int64_t out[8]) {
   return CLRRT_OK;
 }
 
-int clrrt_set_nn_grid_threshold(clrrt_ctx* c, int64_t min_nodes) {
-  if (!c || min_nodes < 0) return CLRRT_EINVAL;
+int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
+  if (!c || !key) return CLRRT_EINVAL;
+  const std::string k(key);
+  if (k == "roll_persistent") c->roll_persistent = value != 0;
+  else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
+  else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
+  return CLRRT_OK;
+}
+
+int clrrt_set_nn_grid(clrrt_ctx* c, int64_t min_nodes, int32_t modes, int32_t wave_budget) {
+  if (!c || min_nodes < 0 || modes < 0 || modes > 3 || wave_budget < 0) return CLRRT_EINVAL;
   c->nng_min_nodes = min_nodes;
+  c->nng_modes = modes;
+  c->nng_budget = wave_budget;
   return CLRRT_OK;
 }
 
@@ -772,7 +800,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     x1 = std::max(x1, c->bbox[2] + 1.0); y1 = std::max(y1, c->bbox[3] + 1.0);
   }
   const double W = x1 - x0, H = y1 - y0;
-  const bool use_grid = c->n_nodes >= c->nng_min_nodes && std::isfinite(W * H) && W * H > 0;
+  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && std::isfinite(W * H) && W * H > 0;
   if (use_grid) {
     double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
     auto supers = [&](double c) { return std::ceil(std::ceil(W / c) / 8) * std::ceil(std::ceil(H / c) / 8); };
@@ -782,6 +810,8 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     g.sw = ((int)std::ceil(W / cs) + 7) / 8; g.sh = ((int)std::ceil(H / cs) + 7) / 8;
     g.gw = 8 * g.sw; g.gh = 8 * g.sh;
     g.ncell = 64 * g.sw * g.sh;
+    g.modes = c->nng_modes;
+    g.budget = c->nng_budget;
     HIPC(c, launch_nn_grid_build(st, c->nn, (int)c->n_nodes, g, c->nng));
   }
   HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
@@ -812,7 +842,11 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
     a.slots = c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
-    HIPC(c, launch_rollout(st, SRC_SPEC, a));
+    if (c->roll_persistent && c->dp.n_steps_max > 0)
+      HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best,
+                                        c->roll_blocks > 0 ? c->roll_blocks : 2 * c->n_cu));
+    else
+      HIPC(c, launch_rollout(st, SRC_SPEC, a));
   }
   SelArgs s;
   s.p = c->dp; s.tree = c->tree; s.cand = c->cand; s.ckey = c->ckey; s.ncand = c->ncand; s.res = c->res_spec;

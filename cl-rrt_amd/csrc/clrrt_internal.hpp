@@ -107,6 +107,8 @@ struct SelArgs {
 struct NnGrid {
   double x0, y0, cs, inv, slack;
   int gw, gh, sw, sh, ncell;
+  int modes;   // sample modes searched through the grid: 1 explore, 2 optimize
+  int budget;  // node records a wave may read (0: automatic)
   const uint32_t* start;  // [ncell + 2]: cell c holds recs[start[c] .. start[c+1])
   const NnRec* recs;      // node records ordered by cell
   const uint32_t* cmin;   // per cell: min costE (order-preserving encoding)
@@ -135,6 +137,11 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
                      int* fb_count, unsigned long long* stats);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
+// Round rollouts as k_roll_prep + persistent k_roll_run (see clrrt_kernels.hip); prep holds
+// njobs * rollout_prep_bytes(), best B ints, qnext one int.
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
+                                     int blocks);
+size_t rollout_prep_bytes();
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);

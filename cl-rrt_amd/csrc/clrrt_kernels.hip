@@ -351,6 +351,21 @@ __device__ __forceinline__ void store_row(double* __restrict__ row, int64_t es, 
   row[5 * es] = r.x5; row[6 * es] = r.x6; row[7 * es] = c7; row[8 * es] = c8; row[9 * es] = c9;
 }
 
+// What Simulation exposes after propagate (stateArray.back(), costs, reference ends).
+__device__ __forceinline__ void finish_rollout(const Roll& r, double c7, double c8, double c9, int outcome,
+                                               int steps, RollRes& out) {
+  out.st[0] = r.x0; out.st[1] = r.x1; out.st[2] = r.x2; out.st[3] = r.x3; out.st[4] = r.x4;
+  out.st[5] = r.x5; out.st[6] = r.x6; out.st[7] = c7; out.st[8] = c8; out.st[9] = c9;
+  out.costE = r.costE;
+  out.costS = r.costS;
+  out.bx = r.R.bx; out.by = r.R.by;
+  out.fx = r.R.a1x; out.fy = r.R.a1y;
+  out.vback = r.vback;
+  out.outcome = outcome;
+  out.nrows = steps + 1;
+  out.refN = r.R.N;
+}
+
 // One whole rollout.  `ps` = parent state (10 doubles), (pbx, pby) = parent ref.back(),
 // pvb = parent ref.v.back().  rows (nullable) receives stateArray: element k of row i at
 // rows[(i * 10 + k) * es].
@@ -375,16 +390,7 @@ __device__ __forceinline__ void run_rollout(const St10& ps, double pbx, double p
     if (rows) store_row(rows + (int64_t)steps * 10 * es, es, r, c7, c8, c9);
     if (o >= 0) { outcome = o; break; }
   }
-  out.st[0] = r.x0; out.st[1] = r.x1; out.st[2] = r.x2; out.st[3] = r.x3; out.st[4] = r.x4;
-  out.st[5] = r.x5; out.st[6] = r.x6; out.st[7] = c7; out.st[8] = c8; out.st[9] = c9;
-  out.costE = r.costE;
-  out.costS = r.costS;
-  out.bx = r.R.bx; out.by = r.R.by;
-  out.fx = r.R.a1x; out.fy = r.R.a1y;
-  out.vback = r.vback;
-  out.outcome = outcome;
-  out.nrows = steps + 1;
-  out.refN = r.R.N;
+  finish_rollout(r, c7, c8, c9, outcome, steps, out);
   w.steps += (uint32_t)steps;
 }
 
@@ -413,9 +419,9 @@ __device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const dou
 //             job slots, interleaved across jobs: element k of row i of job j, pass p (0 regular,
 //             1 goal-biased) at slots[((p * slot_rows + i) * 10 + k) * slot_jobs + j].
 //   SRC_LIST: explicit jobs (parity entry): parent = tree node, rows to arena[row_off] when >= 0.
-template <int SRC, bool NEED_GAP>
-__global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
-  extern __shared__ float4 lds[];
+// Stage the obstacle cull table (and static-obstacle grid) of the query in LDS.
+template <bool NEED_GAP>
+__device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* lds) {
   float4* cv = lds;
   float* rad = (float*)(lds + a.p.n_obs);
   uint32_t* gstart = (uint32_t*)(rad + a.p.n_obs);
@@ -435,8 +441,14 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
     }
     __syncthreads();
   }
-  ObsView ov{a.obs, cv, rad, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
-             a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
+  return ObsView{a.obs, cv, rad, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
+                 a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
+}
+
+template <int SRC, bool NEED_GAP>
+__global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
+  extern __shared__ float4 lds[];
+  const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   WorkCtr w{0, 0, 0};
   bool act = j < a.njobs;
@@ -496,6 +508,160 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
     }
   }
   if (a.ctr) {  // algorithmic work counters (roofline): block reduction, one atomic per block
+    __shared__ __attribute__((aligned(16))) unsigned long long s_ctr[4];
+    if (threadIdx.x < 3) s_ctr[threadIdx.x] = 0;
+    __syncthreads();
+    if (w.steps) {
+      atomicAdd(&s_ctr[0], (unsigned long long)w.steps);
+      atomicAdd(&s_ctr[1], (unsigned long long)w.scan);
+      atomicAdd(&s_ctr[2], (unsigned long long)w.box);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// persistent speculative rollouts
+// --------------------------------------------------------------------------------------------
+// The candidate rollouts of a round differ wildly in length (a collision can end one after a few
+// steps, an end-of-reference one runs hundreds), so one lane per job leaves most lanes of a wave idle
+// behind its longest rollout.  Instead:
+//   k_roll_prep : one lane per job j = (sample s, candidate k) builds the Simulation state
+//                 (getReference + Simulation ctor: make_ref, roll_init) and writes row 0;
+//   k_roll_run  : persistent waves; idle lanes take the next jobs from a queue in candidate-major
+//                 order (all first candidates, then all second ones, ...), so when candidate k of
+//                 sample s is taken the earlier ones have usually finished: a job whose sample
+//                 already has a successful earlier candidate is skipped (or abandoned while
+//                 running) -- expandTree never looks past the first success (:150-160), so the
+//                 round's result is unchanged.  A successful regular rollout that passes the
+//                 goal-bias gate continues in the same lane with the goal-biased rollout.
+struct RollInit {
+  Roll r;
+  double c7, c8, c9;
+  int32_t valid, pad;
+};
+
+template <bool NEED_GAP>
+__global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.njobs) return;
+  const int id = a.cand[j];
+  if (id < 0) {
+    prep[j].valid = 0;
+    return;
+  }
+  const clrrt_node& n = a.tree[id];
+  St10 ps;
+#pragma unroll
+  for (int k = 0; k < 10; k++) ps.v[k] = n.state[k];
+  const RefD R = make_ref(n.ref_back[0], n.ref_back[1], a.samples[j / CAND_K].x, a.samples[j / CAND_K].y, a.p);
+  RollInit ini;
+  roll_init(ini.r, ps.v, R, n.ref_vback, false, a.p);
+  ini.c7 = (double)ini.r.wp;
+  ini.c8 = ps.v[8];
+  ini.c9 = ps.v[9];
+  ini.valid = 1;
+  ini.pad = 0;
+  prep[j] = ini;
+  const int64_t es = a.slot_jobs;
+  double* rows = a.slots + j;
+#pragma unroll
+  for (int k = 0; k < 10; k++) rows[k * es] = ps.v[k];
+  rows[7 * es] = ini.c7;
+}
+
+#define REFILL_MIN 8
+
+template <bool NEED_GAP>
+__global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
+                                                  int* __restrict__ qnext, int* __restrict__ best, int B) {
+  extern __shared__ float4 lds[];
+  const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
+  const int lane = threadIdx.x & 63;
+  const int64_t es = a.slot_jobs;
+  const int64_t pass_stride = (int64_t)a.slot_rows * 10 * es;
+  WorkCtr w{0, 0, 0};
+  Roll r;
+  double c7 = 0, c8 = 0, c9 = 0;
+  int j = -1, k = 0, s = 0, pass = 0, steps = 0;
+  bool exhausted = false;
+  for (;;) {
+    const bool idle = j < 0 && !exhausted;
+    const uint64_t m = __ballot(idle);
+    const uint64_t busy = __ballot(j >= 0);
+    if (m && (__popcll(m) >= REFILL_MIN || busy == 0)) {
+      // wave-aggregated fetch: the idle lanes take consecutive queue positions
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(qnext, __popcll(m));
+      base = __shfl(base, leader, 64);
+      if (idle) {
+        const int q = base + __popcll(m & ((1ull << lane) - 1));
+        if (q >= a.njobs) {
+          exhausted = true;
+        } else {
+          k = q / B;
+          s = q - k * B;
+          j = s * CAND_K + k;
+          if (!prep[j].valid || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+            a.res[j].outcome = -1;
+            a.res_gb[j].outcome = -1;
+            j = -1;
+          } else {
+            r = prep[j].r;
+            c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
+            pass = 0;
+            steps = 0;
+          }
+        }
+      }
+      continue;
+    }
+    if (busy == 0) {
+      if (__ballot(!exhausted) == 0) break;
+      continue;
+    }
+    if (j < 0) continue;
+    steps++;
+    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w);
+    w.steps++;
+    store_row(a.slots + pass * pass_stride + j + (int64_t)steps * 10 * es, es, r, c7, c8, c9);
+    if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
+    if (o >= 0) {
+      RollRes out;
+      finish_rollout(r, c7, c8, c9, o, steps, out);
+      if (pass == 1) {
+        a.res_gb[j] = out;
+        j = -1;
+        continue;
+      }
+      a.res[j] = out;
+      const bool ok = o == CLRRT_ROLL_END || o == CLRRT_ROLL_GOAL;
+      if (ok) atomicMin(&best[s], k);
+      if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
+        // goal-biased rollout from the node this rollout would append (expandTree :163-173)
+        const RefD R = make_goal_ref(out.bx, out.by, a.p);
+        roll_init(r, out.st, R, out.vback, true, a.p);
+        c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
+        pass = 1;
+        steps = 0;
+        double* rows = a.slots + pass_stride + j;
+#pragma unroll
+        for (int q = 0; q < 10; q++) rows[q * es] = out.st[q];
+        rows[7 * es] = c7;
+      } else {
+        a.res_gb[j].outcome = -1;
+        j = -1;
+      }
+    } else if ((steps & 7) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+      // an earlier candidate of this sample succeeded: this result will not be looked at
+      if (pass == 0) a.res[j].outcome = -1;
+      a.res_gb[j].outcome = -1;
+      j = -1;
+    }
+  }
+  if (a.ctr) {
     __shared__ __attribute__((aligned(16))) unsigned long long s_ctr[4];
     if (threadIdx.x < 3) s_ctr[threadIdx.x] = 0;
     __syncthreads();
@@ -819,7 +985,7 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
     // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
-    const int cap = max(2048, N / 64);
+    const int cap = grid->budget > 0 ? grid->budget : max(8192, N / 16);
     e = launch_nn_grid_search(st, S, B, *grid, p, cand, ckey, ncand, ctie, cap, fb_list, fb_count, *gbufs, stats);
     if (e != hipSuccess) return e;
     if (stats) {
@@ -859,9 +1025,7 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
   return hipSuccess;
 }
 
-template <int SRC>
-static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
-  if (a.njobs <= 0) return hipSuccess;
+static size_t roll_lds_bytes(const RollArgs& a) {
   size_t lds = 0;
   if (a.p.coll_mode == CLRRT_COLLISION_OBB) {
     lds = (size_t)a.p.n_obs * (sizeof(float4) + sizeof(float));
@@ -869,6 +1033,13 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
       lds += sizeof(uint32_t) * ((size_t)a.grid.gw * a.grid.gh + 1) +
              sizeof(uint16_t) * ((size_t)a.grid.nitems + a.grid.nmov);
   }
+  return lds;
+}
+
+template <int SRC>
+static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
+  if (a.njobs <= 0) return hipSuccess;
+  const size_t lds = roll_lds_bytes(a);
   dim3 grid((a.njobs + 255) / 256), block(256);
   if (a.p.need_gap)
     hipLaunchKernelGGL((k_rollout<SRC, true>), grid, block, 0, st, a);
@@ -877,6 +1048,30 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   LAUNCH_CHECK();
   return hipSuccess;
 }
+
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
+                                     int blocks) {
+  if (a.njobs <= 0) return hipSuccess;
+  hipError_t e;
+  if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
+  RollInit* pr = (RollInit*)prep;
+  const size_t lds = roll_lds_bytes(a);
+  const int nb = blocks < (a.njobs + 255) / 256 ? blocks : (a.njobs + 255) / 256;
+  if (a.p.need_gap) {
+    hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL((k_roll_run<true>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
+  } else {
+    hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL((k_roll_run<false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+  }
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+size_t rollout_prep_bytes() { return sizeof(RollInit); }
 
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
   if (src == SRC_SPEC) return launch_roll_t<SRC_SPEC>(st, a);

@@ -306,7 +306,8 @@ __global__ void __launch_bounds__(256) k_nn_tile(const clrrt_sample* __restrict_
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { L.keys[j] = __builtin_inff(); L.ids[j] = 0x7fffffff; }
   const double fx = (L.sx - g.x0) * g.inv / SUPER, fy = (L.sy - g.y0) * g.inv / SUPER;
-  bool fallback = L.act && !(isfinite(fx) && isfinite(fy));
+  // non-finite samples and samples of modes not searched through the grid go to brute force
+  bool fallback = L.act && (!(isfinite(fx) && isfinite(fy)) || !(g.modes & (L.ex ? 1 : 2)));
   if (fallback) L.act = false;
   int budget = cap;
   // nodes outside the grid (or with non-finite bounds) are offered to every lane

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 2
+#define CLRRT_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -262,11 +262,17 @@ int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
 int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
 
-/* Nearest-node search strategy: trees of at least `min_nodes` nodes are searched through the
- * per-round spatial grid index, smaller ones by brute force (both return the identical candidate
- * lists).  Default: never (the brute-force search is faster on the benchmark trees); 0 = always
- * the grid. */
-int clrrt_set_nn_grid_threshold(clrrt_ctx* ctx, int64_t min_nodes);
+/* Nearest-node search strategy (every strategy returns the identical candidate lists): trees of at
+ * least `min_nodes` nodes search the samples whose mode bit is set in `modes` (1 = explore,
+ * 2 = optimize) through the per-round spatial grid index, the rest by brute force.  A wave of the
+ * grid search that has read `wave_budget` node records (0: automatic) hands its unfinished samples
+ * to brute force.  Default: off (min_nodes = INT64_MAX; the brute-force search with its prefilter
+ * is faster on the benchmark trees), modes 1 (explore), automatic budget. */
+int clrrt_set_nn_grid(clrrt_ctx* ctx, int64_t min_nodes, int32_t modes, int32_t wave_budget);
+/* Execution knobs (results never depend on them): "roll_persistent" (1: candidate rollouts run on
+ * persistent waves with a job queue, default; 0: one lane per candidate), "roll_blocks" (persistent
+ * blocks of 256 lanes; 0: two per compute unit). */
+int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
 /* Diagnostics of the grid nearest-node search since the last clrrt_reset_counters: out[0] waves,
  * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget,
  * out[4] samples handed to brute force by the LAST search. */

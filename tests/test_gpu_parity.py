@@ -154,9 +154,10 @@ def test_exact_mode_tree_parity(kind, seed, iters, grid):
     assert bytes(ref.state) == bytes(rng.state)
 
 
-@pytest.mark.parametrize("kind,batch,grid", [("empty", 64, False), ("obb200", 256, False), ("moving", 128, False),
-                                              ("obb200", 256, True), ("moving", 128, True)])
-def test_batch_mode_tree_parity(kind, batch, grid):
+@pytest.mark.parametrize("kind,batch,grid,persistent", [("empty", 64, False, 1), ("obb200", 256, False, 1),
+                                                         ("moving", 128, False, 1), ("obb200", 256, True, 1),
+                                                         ("moving", 128, True, 1), ("obb200", 256, False, 0)])
+def test_batch_mode_tree_parity(kind, batch, grid, persistent):
     mode, obs = _scene(kind)
     iters = 4 * batch
     o = Oracle(abi.default_params(collision_mode=mode), obs)
@@ -166,6 +167,7 @@ def test_batch_mode_tree_parity(kind, batch, grid):
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 21,
                        max_batch=batch)
     pl.set_nn_grid_threshold(0 if grid else 1 << 40)
+    pl.set_option("roll_persistent", persistent)
     if obs is not None:
         pl.set_obstacles(obs)
     pl.tree_init()
