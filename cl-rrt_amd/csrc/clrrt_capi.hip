@@ -510,9 +510,11 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
   std::vector<uint16_t> items;
   int gw = 0, gh = 0;
   float fx0 = 0, fy0 = 0, finv = 0;
-  const size_t lds_budget = 60 * 1024 - (size_t)b.size() * 20;
+  // dynamic LDS of the rollout kernels (36 B per obstacle + grid) stays within 52 KiB so that, with the
+  // 9.3 KiB of libm tables, a block fits the default 64 KiB
+  const size_t lds_budget = b.size() * 36 < 52 * 1024 ? 52 * 1024 - b.size() * 36 : 0;
   if (!stat.empty() && std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1) &&
-      (size_t)b.size() * 20 < 48 * 1024) {
+      lds_budget >= 4 * 1024) {
     double W = x1 - x0, H = y1 - y0;
     double cs = std::max(0.25, std::sqrt(W * H / 1024.0));
     for (int attempt = 0; attempt < 40; attempt++, cs *= 1.25) {
@@ -579,7 +581,7 @@ extern "C" {
 int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
   if (!c || m < 0 || (m > 0 && !o)) return CLRRT_EINVAL;
   if (m > c->cap.max_obstacles) return fail(c, CLRRT_ECAPACITY, "too many obstacles");
-  if (m > 6000) return fail(c, CLRRT_ECAPACITY, "at most 6000 obstacles (rollout LDS cull table)");
+  if (m > 1400) return fail(c, CLRRT_ECAPACITY, "at most 1400 obstacles (rollout LDS cull table)");
   std::vector<BakedObs> b(m);
   for (int i = 0; i < m; i++) {
     BakedObs& d = b[i];

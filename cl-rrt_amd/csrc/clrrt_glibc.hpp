@@ -36,20 +36,30 @@ namespace glibc {
 #if defined(__HIPCC__)
 static __device__ __constant__ double d_sincostab[SINCOSTAB_N] = CLRRT_GLIBC_SINCOSTAB;
 static __device__ __constant__ double d_xfg[XFG_ROWS * 4] = CLRRT_GLIBC_XFG;
+// Per-block LDS copies: the table index depends on the argument, so lanes gather from scattered
+// addresses; from LDS that costs ~100 cycles instead of a cache-missing global load.  Every kernel
+// that evaluates these functions calls stage_tables() first.
+static __shared__ double s_sincostab[SINCOSTAB_N];
+static __shared__ double s_xfg[XFG_ROWS * 4];
+__device__ inline void stage_tables() {
+  for (int i = threadIdx.x; i < SINCOSTAB_N; i += blockDim.x) s_sincostab[i] = d_sincostab[i];
+  for (int i = threadIdx.x; i < XFG_ROWS * 4; i += blockDim.x) s_xfg[i] = d_xfg[i];
+  __syncthreads();
+}
 #endif
 static const double h_sincostab[SINCOSTAB_N] = CLRRT_GLIBC_SINCOSTAB;
 static const double h_xfg[XFG_ROWS * 4] = CLRRT_GLIBC_XFG;
 
 CLRRT_HD inline const double* sincostab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return d_sincostab;
+  return s_sincostab;
 #else
   return h_sincostab;
 #endif
 }
 CLRRT_HD inline const double* xfg() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return d_xfg;
+  return s_xfg;
 #else
   return h_xfg;
 #endif

@@ -201,6 +201,7 @@ struct ObsView {
   const BakedObs* __restrict__ g;  // global baked records
   const float4* cv;                // LDS: (cx, cy, vx, vy) float
   const float* rad;                // LDS: bounding radius + vehicle radius + margin
+  const float4* ob;                // LDS: box axis (ux, uy) and half extents (+ rounding slack)
   const uint32_t* gstart;          // LDS: grid cell -> first item (gw*gh + 1)
   const uint16_t* gitems;          // LDS: static obstacle ids per cell, ascending
   const uint16_t* gmov;            // LDS: moving obstacle ids, ascending
@@ -222,6 +223,12 @@ __device__ __forceinline__ float obs_gap(const Box4& veh, const ObsView& ov, int
     float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
     float rr = ov.rad[j];
     if (dx * dx + dy * dy > rr * rr) { culled = true; return 1.0f; }
+    // vehicle bounding circle against the obstacle box: apart -> no overlap possible
+    const float4 b = ov.ob[j];
+    const float e1 = fmaxf(fabsf(dx * b.x + dy * b.y) - b.z, 0.f);
+    const float e2 = fmaxf(fabsf(dy * b.x - dx * b.y) - b.w, 0.f);
+    const float vr = VEH_RAD + CULL_MARGIN;
+    if (e1 * e1 + e2 * e2 > vr * vr) { culled = true; return 1.0f; }
   }
   const BakedObs& o = ov.g[j];
   if (!o.moving) return sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
@@ -423,7 +430,8 @@ __device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const dou
 template <bool NEED_GAP>
 __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* lds) {
   float4* cv = lds;
-  float* rad = (float*)(lds + a.p.n_obs);
+  float4* ob = lds + a.p.n_obs;
+  float* rad = (float*)(ob + a.p.n_obs);
   uint32_t* gstart = (uint32_t*)(rad + a.p.n_obs);
   const int ncell = a.grid.gw * a.grid.gh;
   uint16_t* gitems = (uint16_t*)(gstart + (a.grid.gw > 0 ? ncell + 1 : 0));
@@ -433,6 +441,10 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
       const BakedObs& o = a.obs[j];
       cv[j] = make_float4((float)o.cx, (float)o.cy, (float)o.vlx, (float)o.vly);
       rad[j] = o.brad + VEH_RAD + CULL_MARGIN;
+      // box axes from the baked products: P = cos*hh, R = sin*hh, Q = sin*ww, S = cos*ww
+      const float hh = sqrtf(o.P * o.P + o.R * o.R), ww = sqrtf(o.Q * o.Q + o.S * o.S);
+      const float ux = hh > 0.f ? o.P / hh : 1.f, uy = hh > 0.f ? o.R / hh : 0.f;
+      ob[j] = make_float4(ux, uy, hh * 1.00001f + 1e-4f, ww * 1.00001f + 1e-4f);
     }
     if (a.grid.gw > 0) {
       for (int j = threadIdx.x; j <= ncell; j += blockDim.x) gstart[j] = a.grid.start[j];
@@ -441,13 +453,14 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
     }
     __syncthreads();
   }
-  return ObsView{a.obs, cv, rad, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
+  return ObsView{a.obs, cv, rad, ob, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
                  a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
 }
 
 template <int SRC, bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
   extern __shared__ float4 lds[];
+  glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   WorkCtr w{0, 0, 0};
@@ -544,6 +557,7 @@ struct RollInit {
 
 template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
+  glibc::stage_tables();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= a.njobs) return;
   const int id = a.cand[j];
@@ -577,6 +591,7 @@ template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
                                                   int* __restrict__ qnext, int* __restrict__ best, int B) {
   extern __shared__ float4 lds[];
+  glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int lane = threadIdx.x & 63;
   const int64_t es = a.slot_jobs;
@@ -935,6 +950,7 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
 // Elementary functions as the kernels evaluate them (test hook: bit-compared with the host libm).
 __global__ void k_selftest_math(int fn, const double* __restrict__ a, const double* __restrict__ b, int n,
                                 double* __restrict__ out) {
+  glibc::stage_tables();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double x = a[i], y = b[i];
@@ -1028,7 +1044,7 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
 static size_t roll_lds_bytes(const RollArgs& a) {
   size_t lds = 0;
   if (a.p.coll_mode == CLRRT_COLLISION_OBB) {
-    lds = (size_t)a.p.n_obs * (sizeof(float4) + sizeof(float));
+    lds = (size_t)a.p.n_obs * (2 * sizeof(float4) + sizeof(float));
     if (a.grid.gw > 0)
       lds += sizeof(uint32_t) * ((size_t)a.grid.gw * a.grid.gh + 1) +
              sizeof(uint16_t) * ((size_t)a.grid.nitems + a.grid.nmov);
