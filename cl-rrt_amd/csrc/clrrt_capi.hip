@@ -801,6 +801,17 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     x0 = std::min(x0, c->bbox[0] - 1.0); y0 = std::min(y0, c->bbox[1] - 1.0);
     x1 = std::max(x1, c->bbox[2] + 1.0); y1 = std::max(y1, c->bbox[3] + 1.0);
   }
+  // float frame of the brute-force prune: |coordinate - origin| <= E for every sample and finite node
+  // (samples of this round lie in the sample region, nodes in the tree's box); each float rounding
+  // of a coordinate difference errs by <= 2^-24 E, a squared distance difference by a few of them
+  NnFrame fr;
+  fr.ox = 0.5 * (x0 + x1);
+  fr.oy = 0.5 * (y0 + y1);
+  {
+    const double E = std::max(x1 - x0, y1 - y0) + 1.0;
+    const double d = 16.0 * std::ldexp(E, -24) + 1e-5;
+    fr.delta = std::isfinite(d) ? (float)d : HUGE_VALF;
+  }
   const double W = x1 - x0, H = y1 - y0;
   const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && std::isfinite(W * H) && W * H > 0;
   if (use_grid) {
@@ -818,7 +829,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   }
   HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
                     c->ncand, c->ctie, max_chunks, scratch, use_grid ? &g : nullptr, &c->nng, c->fb_list,
-                    c->fb_count, c->work_ctr + 8));
+                    c->fb_count, c->work_ctr + 8, fr));
   return CLRRT_OK;
 }
 

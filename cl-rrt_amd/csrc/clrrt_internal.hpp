@@ -130,12 +130,19 @@ hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, c
                                  int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
                                  int* fb_count, NnGridBufs& b, unsigned long long* stats);
 
+// Frame of the brute-force search's float prune: positions relative to (ox, oy) in float are within
+// delta of the exact differences for every node and sample of the round.
+struct NnFrame {
+  double ox, oy;
+  float delta;
+};
+
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
 // selection involves equal keys are re-sorted with the replay of std::sort.
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats);
+                     int* fb_count, unsigned long long* stats, const NnFrame& fr);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 // Round rollouts as k_roll_prep + persistent k_roll_run (see clrrt_kernels.hip); prep holds
 // njobs * rollout_prep_bytes(), best B ints, qnext one int.

@@ -46,26 +46,36 @@ __device__ __forceinline__ void topk_insert(float (&keys)[NN_K], int (&ids)[NN_K
   }
 }
 
-// Prune radius for a lane: a node at Euclidean distance |q| > R(kth - cost) cannot enter the list
-// (key >= |q| (1 - 1e-5) - 1e-4 with float rounding, see dubins_key; the radius used here is looser).
-__device__ __forceinline__ float prune_r2(float slack) {  // slack = kth (- cost)
+// Prune radius for a lane: a node at Euclidean distance |q| > prune_r(kth - cost) cannot enter the
+// list (key >= |q| (1 - 1e-5) - 1e-4 under float rounding, see dubins_key; this radius is looser).
+// Negative: nothing can enter.  NaN slack gives NaN (never prunes).
+__device__ __forceinline__ float prune_r(float slack) {
   const float r = (slack + 2e-4f) * (1.0f / 0.9999f);
-  return r < 0.f ? -1.f : r * r;  // -1: nothing can enter (d2 >= 0 > -1)
+  return r < 0.f ? -1.f : r;
 }
 
 // Brute-force candidate lists: block = 256 samples x one chunk of nodes; the chunk is staged through
-// LDS 256 nodes at a time (coalesced loads, broadcast reads), each lane keeps its own top-11 and runs
-// the exact Dubins key / feasibleNode only for nodes that pass nn_prefilter.
+// LDS 256 nodes at a time (coalesced loads, broadcast reads), each lane keeps its own top-11.
+// Per tile, a branch-free float pass over every (lane, node) pair evaluates necessary conditions for
+// the node to enter the lane's list on coordinates relative to the frame origin (each coordinate
+// difference within fr.delta of the exact one), with margins that cover that error:
+//   * Euclidean prune: |q| <= prune_r(kth - cost) + delta;
+//   * feasibleNode: |sample - ref.back()| >= feas_len - 2 delta and the angle to ang_par
+//     <= pi/4 + 0.02 rad (float error < 5e-3 rad for |v| >= 0.4 m and delta <= 2e-3 m);
+//   * not deep inside a turning circle when (cost +) 14.9 > kth (inside -> Dubins key >= rho pi).
+// Survivors are queued per lane; a second pass runs nn_prefilter, the exact Dubins key and
+// feasibleNode on the queue, so lanes stay converged instead of diverging node by node.
 // sidx != nullptr: lanes t < *scount search sample sidx[t] (the grid search's over-budget samples).
+#define NN_QCAP 32
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
-                                                    int nchunks, DevParams p, float* __restrict__ pk,
+                                                    int nchunks, DevParams p, NnFrame fr, float* __restrict__ pk,
                                                     int* __restrict__ pi, const int* __restrict__ sidx,
                                                     const int* __restrict__ scount) {
-  __shared__ double2 s_p[256];  // node x, y
-  __shared__ double2 s_b[256];  // ref.back() x, y
+  __shared__ float4 s_r[256];   // node x, y and ref.back() x, y relative to the frame origin (float)
   __shared__ float4 s_f[256];   // c, s, ca, sa
   __shared__ float s_c[256];    // costE
+  __shared__ uint8_t s_q[NN_QCAP][256];  // per-lane queue of tile positions (column = lane)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
   const int n0 = c * chunk;
@@ -76,44 +86,79 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   double sx = 0, sy = 0;
   int ex = 1;
   if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
+  const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
   float keys[NN_K];
   int ids[NN_K];
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
-  float r2 = __builtin_inff();  // explore: prune radius^2 for the current 11th key
   const float feas2 = (float)(p.feas_len * (1 - 1e-6) * p.feas_len * (1 - 1e-6));
-  for (int b = n0; b < n1; b += 256) {
-    const int m = min(256, n1 - b);
-    __syncthreads();
-    if ((int)threadIdx.x < m) {
-      const NnRec& rec = nodes[b + threadIdx.x];
-      s_p[threadIdx.x] = make_double2(rec.x, rec.y);
-      s_b[threadIdx.x] = make_double2(rec.bx, rec.by);
-      s_f[threadIdx.x] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
-      s_c[threadIdx.x] = rec.costE;
-    }
-    __syncthreads();
-    if (!act) continue;
-    for (int k = 0; k < m; k++) {
-      const double2 np = s_p[k];
-      const float qx = (float)(sx - np.x), qy = (float)(sy - np.y);
-      const float d2 = qx * qx + qy * qy;
-      const float cost = s_c[k];
-      const float lim = ex ? r2 : prune_r2(keys[NN_K - 1] - cost);
-      if (!(d2 <= lim) && !(lim != lim)) continue;  // Euclidean prune (a NaN limit never prunes)
-      const float4 f = s_f[k];
-      const double2 bb = s_b[k];
-      if (!nn_prefilter(sx, sy, qx, qy, f.x, f.y, f.z, f.w, bb.x, bb.y, cost, ex, keys[NN_K - 1], feas2)) continue;
-      const int n = b + k;
+  const float flen = (float)p.feas_len - 2.f * fr.delta;
+  const float fl2 = flen > 0.f ? flen * flen : 0.f;
+  const float c45 = 0.69276f;                    // cos(pi/4 + 0.02), rounded down
+  const float rho = 4.77f, rin = rho - 0.01f - 4.f * fr.delta;  // "deep inside" radius
+  const float rin2 = rin > 0.f ? rin * rin : -1.f;
+  float rr = __builtin_inff();  // explore: (prune radius + delta)^2 for the current 11th key
+  const int me = threadIdx.x;
+  auto drain = [&](int b, int cnt) {
+    for (int i = 0; i < cnt; i++) {
+      const int n = b + s_q[i][me];
       const NnRec& rec = nodes[n];
+      const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
+      if (!nn_prefilter(sx, sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, ex,
+                        keys[NN_K - 1], feas2))
+        continue;
       float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
       if (!ex) key = rec.costE + key;
       if (lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) &&
           feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
         topk_insert(keys, ids, key, n);
-        r2 = prune_r2(keys[NN_K - 1]);
+        const float R = prune_r(keys[NN_K - 1]);
+        rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
       }
     }
+  };
+  for (int b = n0; b < n1; b += 256) {
+    const int m = min(256, n1 - b);
+    __syncthreads();
+    if ((int)threadIdx.x < m) {
+      const NnRec& rec = nodes[b + threadIdx.x];
+      s_r[threadIdx.x] = make_float4((float)(rec.x - fr.ox), (float)(rec.y - fr.oy), (float)(rec.bx - fr.ox),
+                                     (float)(rec.by - fr.oy));
+      s_f[threadIdx.x] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
+      s_c[threadIdx.x] = rec.costE;
+    }
+    __syncthreads();
+    if (!act) continue;
+    int cnt = 0;
+    const float kth = keys[NN_K - 1];
+    const bool in_ok = (ex ? 14.9f : -__builtin_inff()) <= kth;  // explore: inside circles can enter
+    for (int k = 0; k < m; k++) {
+      const float4 q = s_r[k];
+      const float4 f = s_f[k];
+      const float cost = s_c[k];
+      const float dx = rsx - q.x, dy = rsy - q.y;
+      const float d2 = dx * dx + dy * dy;
+      float lim = rr;
+      if (!ex) {
+        const float R = prune_r(kth - cost);
+        lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+      }
+      const bool near = (d2 <= lim) || (lim != lim);  // a NaN limit never prunes
+      const float vx = rsx - q.z, vy = rsy - q.w;
+      const float dot = vx * f.z + vy * f.w, vv = vx * vx + vy * vy;
+      const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
+      const float tx = f.x * dx - f.y * dy, ty = fabsf(f.y * dx + f.x * dy);
+      const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
+      const bool in_bad = deep && !(ex ? in_ok : (cost + 14.9f <= kth));
+      if (near && !ang_bad && !in_bad) {
+        s_q[cnt][me] = (uint8_t)k;
+        if (++cnt == NN_QCAP) {
+          drain(b, cnt);
+          cnt = 0;
+        }
+      }
+    }
+    drain(b, cnt);
   }
   if (act) {
     size_t base = ((size_t)t * nchunks + c) * NN_K;
@@ -990,13 +1035,14 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
   } while (0)
 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                                  const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
-                                  int* ctie, int max_chunks, const int* sidx, const int* scount);
+                                  const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
+                                  float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
+                                  const int* scount);
 
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats) {
+                     int* fb_count, unsigned long long* stats, const NnFrame& fr) {
   if (grid) {
     // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
@@ -1008,10 +1054,10 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
       e = hipMemcpyAsync(stats + 4, fb_count, sizeof(int), hipMemcpyDeviceToDevice, st);  // low word: fallbacks
       if (e != hipSuccess) return e;
     }
-    e = launch_nn_brute(st, S, B, nodes, N, p, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
+    e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
     if (e != hipSuccess) return e;
   } else {
-    hipError_t e = launch_nn_brute(st, S, B, nodes, N, p, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr,
+    hipError_t e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr,
                                    nullptr);
     if (e != hipSuccess) return e;
   }
@@ -1024,8 +1070,9 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
 }
 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                                  const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand,
-                                  int* ctie, int max_chunks, const int* sidx, const int* scount) {
+                                  const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
+                                  float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
+                                  const int* scount) {
   int groups = (B + 255) / 256;
   int nchunks = (N + 255) / 256;
   int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
@@ -1033,7 +1080,7 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
   int chunk = (N + nchunks - 1) / nchunks;
   nchunks = (N + chunk - 1) / chunk;
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, pk, pi, sidx, scount);
+                     p, fr, pk, pi, sidx, scount);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      cand, ckey, ncand, ctie, sidx, scount);
