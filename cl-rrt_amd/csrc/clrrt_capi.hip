@@ -90,6 +90,7 @@ struct clrrt_ctx {
   double* d_bbox = nullptr;  // [4] device result of launch_bbox
   double* h_bbox = nullptr;  // [4] pinned
   int64_t nng_min_nodes = INT64_MAX;  // clrrt_set_nn_grid: off by default (brute force is faster on bench trees)
+  int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int nng_modes = 1;
   int nng_budget = 0;
   // persistent rollouts (k_roll_prep + k_roll_run)
@@ -340,7 +341,7 @@ static void free_all(clrrt_ctx* c) {
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
                   c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
                   c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
-                  c->nng.order};
+                  c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -414,6 +415,11 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->nng.sfill, 2 * kNngMaxSuper + 4));
   chk(dalloc(&c->nng.sstart, 2 * kNngMaxSuper + 4));
   chk(dalloc(&c->nng.order, B));
+  chk(dalloc(&c->nng.nsamp, 1));
+  chk(dalloc(&c->nng.home, B));
+  chk(dalloc(&c->nng.seed, B));
+  chk(dalloc(&c->nng.tbox, c->cap.max_nodes / 256 + 2));
+  chk(dalloc(&c->nng.tcost, c->cap.max_nodes / 256 + 2));
   chk(dalloc(&c->nng.fmin, 4 * kNngMaxSuper));
   chk(dalloc(&c->nng.fmax, 4 * kNngMaxSuper));
   chk(dalloc(&c->fb_list, B));
@@ -729,6 +735,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return CLRRT_EINVAL;
   const std::string k(key);
   if (k == "roll_persistent") c->roll_persistent = value != 0;
+  else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
   return CLRRT_OK;
@@ -813,8 +820,10 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     fr.delta = std::isfinite(d) ? (float)d : HUGE_VALF;
   }
   const double W = x1 - x0, H = y1 - y0;
-  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && std::isfinite(W * H) && W * H > 0;
-  if (use_grid) {
+  const bool region_ok = std::isfinite(W * H) && W * H > 0;
+  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && region_ok;
+  const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && region_ok;
+  if (use_grid || ordered) {
     double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
     auto supers = [&](double c) { return std::ceil(std::ceil(W / c) / 8) * std::ceil(std::ceil(H / c) / 8); };
     while (supers(cs) * 64 > (double)kNngMaxCells) cs *= 1.1;
@@ -828,8 +837,8 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     HIPC(c, launch_nn_grid_build(st, c->nn, (int)c->n_nodes, g, c->nng));
   }
   HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                    c->ncand, c->ctie, max_chunks, scratch, use_grid ? &g : nullptr, &c->nng, c->fb_list,
-                    c->fb_count, c->work_ctr + 8, fr));
+                    c->ncand, c->ctie, max_chunks, scratch, (use_grid || ordered) ? &g : nullptr, &c->nng, c->fb_list,
+                    c->fb_count, c->work_ctr + 8, fr, ordered));
   return CLRRT_OK;
 }
 

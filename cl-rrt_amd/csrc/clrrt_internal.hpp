@@ -124,8 +124,15 @@ struct NnGridBufs {
   NnRec* sorted;
   uint32_t *scount, *sfill, *sstart;  // sample buckets [2 * super-cells + 2]
   int* order;                         // [max_batch] samples ordered by bucket
+  int* nsamp;                         // [1] = B (device copy for the ordered brute force)
+  int* home;                          // [max_batch] first record of the ordered sample's cell
+  float* seed;                        // [max_batch] upper bound on each sample's 11th key
+  float4* tbox;                       // [max_nodes / 256 + 1] tile boxes of the ordered records
+  float* tcost;                       // [max_nodes / 256 + 1] tile minimum costs
 };
 hipError_t launch_nn_grid_build(hipStream_t st, const NnRec* nodes, int N, NnGrid& g, NnGridBufs& b);
+// b.order[0 .. B) = the samples ordered by mode and super-cell
+hipError_t launch_sample_order(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, NnGridBufs& b);
 hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, const DevParams& p,
                                  int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
                                  int* fb_count, NnGridBufs& b, unsigned long long* stats);
@@ -142,7 +149,7 @@ struct NnFrame {
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats, const NnFrame& fr);
+                     int* fb_count, unsigned long long* stats, const NnFrame& fr, bool ordered);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 // Round rollouts as k_roll_prep + persistent k_roll_run (see clrrt_kernels.hip); prep holds
 // njobs * rollout_prep_bytes(), best B ints, qnext one int.

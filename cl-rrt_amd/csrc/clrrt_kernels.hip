@@ -65,16 +65,26 @@ __device__ __forceinline__ float prune_r(float slack) {
 //   * not deep inside a turning circle when (cost +) 14.9 > kth (inside -> Dubins key >= rho pi).
 // Survivors are queued per lane; a second pass runs nn_prefilter, the exact Dubins key and
 // feasibleNode on the queue, so lanes stay converged instead of diverging node by node.
-// sidx != nullptr: lanes t < *scount search sample sidx[t] (the grid search's over-budget samples).
+// sidx != nullptr: lanes t < *scount search sample sidx[t] (samples ordered by place, or the grid
+// search's over-budget samples).
+// tbox != nullptr: the nodes are ordered by place (cell order) with per-tile float bounding boxes in
+// the frame and minimum costs, and the samples by place too.  Chunk c then takes the tiles
+// c, c + nchunks, c + 2 nchunks, ... (every chunk spans the whole tree), visited outward from the
+// tile holding the block's home cell so the lists fill with near nodes first; a tile none of whose
+// nodes can pass any lane's Euclidean prune is skipped by the whole block.  List entries are the
+// records' node ids.
 #define NN_QCAP 32
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, NnFrame fr, float* __restrict__ pk,
                                                     int* __restrict__ pi, const int* __restrict__ sidx,
-                                                    const int* __restrict__ scount) {
+                                                    const int* __restrict__ scount, const float4* __restrict__ tbox,
+                                                    const float* __restrict__ tcost, const int* __restrict__ home,
+                                                    const float* __restrict__ seed) {
   __shared__ float4 s_r[256];   // node x, y and ref.back() x, y relative to the frame origin (float)
   __shared__ float4 s_f[256];   // c, s, ca, sa
   __shared__ float s_c[256];    // costE
+  __shared__ int s_id[256];     // node id
   __shared__ uint8_t s_q[NN_QCAP][256];  // per-lane queue of tile positions (column = lane)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
@@ -97,12 +107,20 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   const float c45 = 0.69276f;                    // cos(pi/4 + 0.02), rounded down
   const float rho = 4.77f, rin = rho - 0.01f - 4.f * fr.delta;  // "deep inside" radius
   const float rin2 = rin > 0.f ? rin * rin : -1.f;
+  // kcap: an upper bound on the sample's final 11th key over the whole tree (seed pass), so the
+  // chunk's pruning starts tight: a node with key > kcap cannot be in the merged list
+  const float kcap = (seed && act) ? seed[s] : __builtin_inff();
   float rr = __builtin_inff();  // explore: (prune radius + delta)^2 for the current 11th key
+  if (kcap < __builtin_inff()) {
+    const float R = prune_r(kcap);
+    rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+  }
   const int me = threadIdx.x;
   auto drain = [&](int b, int cnt) {
     for (int i = 0; i < cnt; i++) {
-      const int n = b + s_q[i][me];
-      const NnRec& rec = nodes[n];
+      const int k = s_q[i][me];
+      const int n = s_id[k];
+      const NnRec& rec = nodes[b + k];
       const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
       if (!nn_prefilter(sx, sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, ex,
                         keys[NN_K - 1], feas2))
@@ -112,13 +130,50 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       if (lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) &&
           feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
         topk_insert(keys, ids, key, n);
-        const float R = prune_r(keys[NN_K - 1]);
+        const float R = prune_r(fminf(keys[NN_K - 1], kcap));
         rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
       }
     }
   };
-  for (int b = n0; b < n1; b += 256) {
-    const int m = min(256, n1 - b);
+  const int ntile = (N + 255) >> 8;
+  int tcount, i0 = 0;
+  if (tbox) {
+    tcount = c < ntile ? (ntile - 1 - c) / nchunks + 1 : 0;
+    const int ht = home[blockIdx.x * blockDim.x] >> 8;  // the block's first sample's home tile
+    i0 = min(max(0, (ht - c + nchunks - 1) / nchunks), max(0, tcount - 1));
+  } else {
+    tcount = (n1 - n0 + 255) >> 8;
+  }
+  for (int it = 0; it < tcount; it++) {
+    int b;
+    if (tbox) {
+      // i0, i0 + 1, i0 - 1, i0 + 2, ... clipped to [0, tcount)
+      const int lo = i0, hi = tcount - 1 - i0;  // steps available below / above
+      const int sym = min(lo, hi);
+      int i;
+      if (it <= 2 * sym) i = (it & 1) ? i0 + (it + 1) / 2 : i0 - it / 2;
+      else if (hi > lo) i = i0 + (it - lo);
+      else i = i0 - (it - hi);
+      b = (c + i * nchunks) << 8;
+    } else {
+      b = n0 + (it << 8);
+    }
+    const int m = min(256, N - b);
+    bool need = act;
+    if (tbox) {
+      // the tile's Euclidean bound (the same float positions the node test uses)
+      const float4 bx = tbox[b >> 8];
+      const float ex0 = fmaxf(fmaxf(bx.x - rsx, rsx - bx.z), 0.f);
+      const float ey0 = fmaxf(fmaxf(bx.y - rsy, rsy - bx.w), 0.f);
+      const float bd2 = (ex0 * ex0 + ey0 * ey0) * (1.f - 1e-6f);
+      float lim = rr;
+      if (!ex) {
+        const float R = prune_r(fminf(keys[NN_K - 1], kcap) - tcost[b >> 8]);
+        lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+      }
+      need = act && !(bd2 > lim);  // NaN bounds never skip
+      if (!__syncthreads_or(need)) continue;
+    }
     __syncthreads();
     if ((int)threadIdx.x < m) {
       const NnRec& rec = nodes[b + threadIdx.x];
@@ -126,11 +181,12 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
                                      (float)(rec.by - fr.oy));
       s_f[threadIdx.x] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
       s_c[threadIdx.x] = rec.costE;
+      s_id[threadIdx.x] = tbox ? rec.id : b + (int)threadIdx.x;
     }
     __syncthreads();
-    if (!act) continue;
+    if (!need) continue;
     int cnt = 0;
-    const float kth = keys[NN_K - 1];
+    const float kth = fminf(keys[NN_K - 1], kcap);
     const bool in_ok = (ex ? 14.9f : -__builtin_inff()) <= kth;  // explore: inside circles can enter
     for (int k = 0; k < m; k++) {
       const float4 q = s_r[k];
@@ -1037,13 +1093,112 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
                                   float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
-                                  const int* scount);
+                                  const int* scount, const float4* tbox = nullptr, const float* tcost = nullptr,
+                                  const int* home = nullptr, const float* seed = nullptr);
+
+// Per 256-node tile of the place-ordered records: bounding box of the float frame positions the
+// brute-force prune uses, and the minimum cost (NaN if any cost is NaN).
+__global__ void __launch_bounds__(256) k_tile_bounds(const NnRec* __restrict__ recs, int N, NnFrame fr,
+                                                     float4* __restrict__ tbox, float* __restrict__ tcost) {
+  __shared__ float s[5][256];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  float x0 = __builtin_inff(), y0 = __builtin_inff(), x1 = -__builtin_inff(), y1 = -__builtin_inff();
+  float cm = __builtin_inff();
+  if (i < N) {
+    const NnRec& r = recs[i];
+    const float x = (float)(r.x - fr.ox), y = (float)(r.y - fr.oy);
+    // NaN positions make the box NaN (never skipped)
+    x0 = x; x1 = x; y0 = y; y1 = y;
+    cm = r.costE;
+  }
+  s[0][threadIdx.x] = x0; s[1][threadIdx.x] = y0; s[2][threadIdx.x] = x1; s[3][threadIdx.x] = y1;
+  s[4][threadIdx.x] = cm;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      const int o = threadIdx.x + off;
+      const float a0 = s[0][threadIdx.x], b0 = s[0][o], a1 = s[1][threadIdx.x], b1 = s[1][o];
+      const float a2 = s[2][threadIdx.x], b2 = s[2][o], a3 = s[3][threadIdx.x], b3 = s[3][o];
+      const float a4 = s[4][threadIdx.x], b4 = s[4][o];
+      // NaN-propagating min / max
+      s[0][threadIdx.x] = (a0 != a0 || b0 != b0) ? __builtin_nanf("") : fminf(a0, b0);
+      s[1][threadIdx.x] = (a1 != a1 || b1 != b1) ? __builtin_nanf("") : fminf(a1, b1);
+      s[2][threadIdx.x] = (a2 != a2 || b2 != b2) ? __builtin_nanf("") : fmaxf(a2, b2);
+      s[3][threadIdx.x] = (a3 != a3 || b3 != b3) ? __builtin_nanf("") : fmaxf(a3, b3);
+      s[4][threadIdx.x] = (a4 != a4 || b4 != b4) ? __builtin_nanf("") : fminf(a4, b4);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    tbox[blockIdx.x] = make_float4(s[0][0], s[1][0], s[2][0], s[3][0]);
+    tcost[blockIdx.x] = s[4][0];
+  }
+}
+
+// Seed of the place-ordered search: the 11th smallest key (of feasible nodes) among the place-ordered
+// records around the sample's home cell (5 tiles), an upper bound on its 11th key over the tree
+// (+inf when fewer than 11 are found).  seed[s] for sample s.
+__global__ void __launch_bounds__(256) k_nn_seed(const clrrt_sample* __restrict__ S, int B,
+                                                 const NnRec* __restrict__ recs, int N, DevParams p,
+                                                 const int* __restrict__ order, const int* __restrict__ home,
+                                                 float* __restrict__ seed) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B) return;
+  const int s = order[t];
+  const double sx = S[s].x, sy = S[s].y;
+  const int ex = S[s].explore;
+  float keys[NN_K];
+  int ids[NN_K];
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  const int ht = home[t] >> 8;
+  const int a = max(0, (ht - 2) << 8), b = min(N, (ht + 3) << 8);
+  const float feas2 = (float)(p.feas_len * (1 - 1e-6) * p.feas_len * (1 - 1e-6));
+  for (int k = a; k < b; k++) {
+    const NnRec& rec = recs[k];
+    const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
+    if (!nn_prefilter(sx, sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, ex, keys[NN_K - 1],
+                      feas2))
+      continue;
+    float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+    if (!ex) key = rec.costE + key;
+    if (lex_less(key, rec.id, keys[NN_K - 1], ids[NN_K - 1]) &&
+        feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
+      topk_insert(keys, ids, key, rec.id);
+  }
+  seed[s] = keys[NN_K - 1];
+}
+
+hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
+                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
+                            int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
+                            float4* tbox, float* tcost, const int* home, float* seed) {
+  hipLaunchKernelGGL(k_tile_bounds, dim3((N + 255) / 256), dim3(256), 0, st, sorted, N, fr, tbox, tcost);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_seed, dim3((B + 255) / 256), dim3(256), 0, st, S, B, sorted, N, p, order, home, seed);
+  LAUNCH_CHECK();
+  return launch_nn_brute(st, S, B, sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, order, nsamp,
+                         tbox, tcost, home, seed);
+}
+
+hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
+                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
+                            int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
+                            float4* tbox, float* tcost, const int* home, float* seed);
 
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats, const NnFrame& fr) {
-  if (grid) {
+                     int* fb_count, unsigned long long* stats, const NnFrame& fr, bool ordered) {
+  if (ordered) {
+    // place-ordered records (built by launch_nn_grid_build) and place-ordered samples
+    hipError_t e = launch_sample_order(st, S, B, *grid, *gbufs);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)gbufs->nsamp, B, 1, st)) != hipSuccess) return e;
+    e = launch_nn_sorted(st, S, B, gbufs->sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks,
+                         gbufs->order, gbufs->nsamp, gbufs->tbox, gbufs->tcost, gbufs->home, gbufs->seed);
+    if (e != hipSuccess) return e;
+  } else if (grid) {
     // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
     hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
@@ -1072,15 +1227,17 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
                                   float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
-                                  const int* scount) {
+                                  const int* scount, const float4* tbox, const float* tcost, const int* home,
+                                  const float* seed) {
   int groups = (B + 255) / 256;
   int nchunks = (N + 255) / 256;
   int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
   nchunks = max(1, min(nchunks, min(want, max_chunks)));
   int chunk = (N + nchunks - 1) / nchunks;
+  chunk = (chunk + 255) & ~255;  // tiles of 256 nodes never straddle chunks
   nchunks = (N + chunk - 1) / chunk;
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, fr, pk, pi, sidx, scount);
+                     p, fr, pk, pi, sidx, scount, tbox, tcost, home, seed);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      cand, ckey, ncand, ctie, sidx, scount);

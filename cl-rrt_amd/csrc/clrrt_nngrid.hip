@@ -142,13 +142,24 @@ __global__ void __launch_bounds__(256) k_smp_count(const clrrt_sample* __restric
   if (t < B) atomicAdd(&count[sample_bucket(g, S[t])], 1u);
 }
 
+// order[pos] = sample; home[pos] = first place-ordered node record of the sample's grid cell (or of
+// the nearest cell inside the grid), where its nearest-node search starts.
 __global__ void __launch_bounds__(256) k_smp_scatter(const clrrt_sample* __restrict__ S, int B, NnGrid g,
                                                      const uint32_t* __restrict__ start, uint32_t* __restrict__ fill,
-                                                     int* __restrict__ order) {
+                                                     int* __restrict__ order, int* __restrict__ home) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B) return;
   const int b = sample_bucket(g, S[t]);
-  order[start[b] + atomicAdd(&fill[b], 1u)] = t;
+  const uint32_t pos = start[b] + atomicAdd(&fill[b], 1u);
+  order[pos] = t;
+  const double fx = (S[t].x - g.x0) * g.inv, fy = (S[t].y - g.y0) * g.inv;
+  int h = 0;
+  if (isfinite(fx) && isfinite(fy)) {
+    const int gx = (int)fmin((double)(g.gw - 1), fmax(0.0, floor(fx)));
+    const int gy = (int)fmin((double)(g.gh - 1), fmax(0.0, floor(fy)));
+    h = (int)g.start[cell_of(g, gx, gy)];
+  }
+  home[pos] = h;
 }
 
 // ------------------------------------------------------------------------------------ search
@@ -429,9 +440,7 @@ hipError_t launch_nn_grid_build(hipStream_t st, const NnRec* nodes, int N, NnGri
   return hipSuccess;
 }
 
-hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, const DevParams& p,
-                                 int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
-                                 int* fb_count, NnGridBufs& b, unsigned long long* stats) {
+hipError_t launch_sample_order(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, NnGridBufs& b) {
   const int nb = 2 * g.sw * g.sh + 1;
   hipError_t e;
   if ((e = hipMemsetAsync(b.scount, 0, sizeof(uint32_t) * (nb + 1), st)) != hipSuccess) return e;
@@ -440,8 +449,17 @@ hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, c
   LAUNCH_CHECK2();
   hipLaunchKernelGGL(k_nng_scan, dim3(1), dim3(1024), 0, st, b.scount, nb, b.sstart);
   LAUNCH_CHECK2();
-  hipLaunchKernelGGL(k_smp_scatter, dim3((B + 255) / 256), dim3(256), 0, st, S, B, g, b.sstart, b.sfill, b.order);
+  hipLaunchKernelGGL(k_smp_scatter, dim3((B + 255) / 256), dim3(256), 0, st, S, B, g, b.sstart, b.sfill, b.order,
+                     b.home);
   LAUNCH_CHECK2();
+  return hipSuccess;
+}
+
+hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, const DevParams& p,
+                                 int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
+                                 int* fb_count, NnGridBufs& b, unsigned long long* stats) {
+  hipError_t e = launch_sample_order(st, S, B, g, b);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_nn_tile, dim3((B + 255) / 256), dim3(256), 0, st, S, B, b.order, g, p, cand, ckey, ncand, ctie,
                      cap, fb_list, fb_count, stats);
   LAUNCH_CHECK2();

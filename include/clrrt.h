@@ -271,7 +271,8 @@ int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
 int clrrt_set_nn_grid(clrrt_ctx* ctx, int64_t min_nodes, int32_t modes, int32_t wave_budget);
 /* Execution knobs (results never depend on them): "roll_persistent" (1: candidate rollouts run on
  * persistent waves with a job queue, default; 0: one lane per candidate), "roll_blocks" (persistent
- * blocks of 256 lanes; 0: two per compute unit). */
+ * blocks of 256 lanes; 0: two per compute unit), "nn_ordered_min" (trees of at least this many
+ * nodes use the place-ordered brute-force search that skips far node tiles; default: never). */
 int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
 /* Diagnostics of the grid nearest-node search since the last clrrt_reset_counters: out[0] waves,
  * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget,

@@ -36,6 +36,13 @@ def _scene(kind):
     raise KeyError(kind)
 
 
+def _nn_strategy(pl, name):
+    """Select the nearest-node search: 'brute' (node order), 'ordered' (place-ordered brute force with
+    tile skipping) or 'grid' (wave-uniform grid search + brute-force fallback)."""
+    pl.set_nn_grid(0 if name == "grid" else 1 << 40, 3, 0)
+    pl.set_option("nn_ordered_min", 0 if name == "ordered" else 1 << 40)
+
+
 def _pair(kind, seed=1, iters=40):
     """Oracle grown `iters` iterations + a GPU planner holding the same tree."""
     mode, obs = _scene(kind)
@@ -83,10 +90,11 @@ def test_rollout_parity(kind):
     assert rate <= FLIP_RATE
 
 
-@pytest.mark.parametrize("kind,grid", [("empty", False), ("obb200", False), ("empty", True), ("obb200", True)])
-def test_nearest_node_parity(kind, grid):
+@pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "grid"),
+                                           ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered")])
+def test_nearest_node_parity(kind, strategy):
     o, pl = _pair(kind, seed=4, iters=150)
-    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
+    _nn_strategy(pl, strategy)
     smp = list(clrrt.Rng(21).draw_samples(pl.params, 400))
     ids, keys = pl.sort_nodes_batch(smp)
     bad = 0
@@ -117,11 +125,12 @@ def _compare_trees(o, pl, label):
     return on, gn, first_bad
 
 
-@pytest.mark.parametrize("kind,seed,iters,grid", [("empty", 1, 200, False), ("obb200", 3, 300, False),
-                                                  ("empty", 2, 300, False), ("obb200", 5, 300, False),
-                                                  ("moving", 4, 250, False), ("obb200", 3, 300, True),
-                                                  ("moving", 4, 250, True)])
-def test_exact_mode_tree_parity(kind, seed, iters, grid):
+@pytest.mark.parametrize("kind,seed,iters,strategy", [("empty", 1, 200, "brute"), ("obb200", 3, 300, "brute"),
+                                                      ("empty", 2, 300, "brute"), ("obb200", 5, 300, "brute"),
+                                                      ("moving", 4, 250, "brute"), ("obb200", 3, 300, "grid"),
+                                                      ("moving", 4, 250, "grid"), ("obb200", 5, 300, "ordered"),
+                                                      ("moving", 4, 250, "ordered")])
+def test_exact_mode_tree_parity(kind, seed, iters, strategy):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
     o = Oracle(abi.default_params(collision_mode=mode), obs)
@@ -130,7 +139,7 @@ def test_exact_mode_tree_parity(kind, seed, iters, grid):
     o.expand(iters)
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 20,
                        max_batch=256)
-    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
+    _nn_strategy(pl, strategy)
     if obs is not None:
         pl.set_obstacles(obs)
     pl.tree_init()
@@ -154,10 +163,12 @@ def test_exact_mode_tree_parity(kind, seed, iters, grid):
     assert bytes(ref.state) == bytes(rng.state)
 
 
-@pytest.mark.parametrize("kind,batch,grid,persistent", [("empty", 64, False, 1), ("obb200", 256, False, 1),
-                                                         ("moving", 128, False, 1), ("obb200", 256, True, 1),
-                                                         ("moving", 128, True, 1), ("obb200", 256, False, 0)])
-def test_batch_mode_tree_parity(kind, batch, grid, persistent):
+@pytest.mark.parametrize("kind,batch,strategy,persistent", [("empty", 64, "brute", 1), ("obb200", 256, "brute", 1),
+                                                             ("moving", 128, "brute", 1), ("obb200", 256, "grid", 1),
+                                                             ("moving", 128, "grid", 1), ("obb200", 256, "brute", 0),
+                                                             ("obb200", 256, "ordered", 1),
+                                                             ("moving", 128, "ordered", 1)])
+def test_batch_mode_tree_parity(kind, batch, strategy, persistent):
     mode, obs = _scene(kind)
     iters = 4 * batch
     o = Oracle(abi.default_params(collision_mode=mode), obs)
@@ -166,7 +177,7 @@ def test_batch_mode_tree_parity(kind, batch, grid, persistent):
     o.expand_batch(iters, batch, stable=True)
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 21,
                        max_batch=batch)
-    pl.set_nn_grid_threshold(0 if grid else 1 << 40)
+    _nn_strategy(pl, strategy)
     pl.set_option("roll_persistent", persistent)
     if obs is not None:
         pl.set_obstacles(obs)
@@ -266,13 +277,14 @@ def test_nn_grid_matches_brute_force_large_tree():
     n_nodes = pl.size()[0]
     assert n_nodes > 20000
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
-    pl.set_nn_grid_threshold(1 << 40)
+    _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    pl.set_nn_grid_threshold(0)
-    ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
-    print(f"tree {n_nodes} nodes; lists equal: {np.array_equal(ids_b, ids_g)}")
-    assert np.array_equal(ids_b, ids_g)
-    assert np.array_equal(keys_b.view(np.uint32)[ids_b >= 0], keys_g.view(np.uint32)[ids_g >= 0])
+    for strategy in ("grid", "ordered"):
+        _nn_strategy(pl, strategy)
+        ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
+        print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
+        assert np.array_equal(ids_b, ids_g)
+        assert np.array_equal(keys_b.view(np.uint32)[ids_b >= 0], keys_g.view(np.uint32)[ids_g >= 0])
     # and against the oracle's std::sort on a subset
     o = Oracle(abi.default_params(collision_mode=mode), obs)
     o.load_tree(pl.nodes_raw())

@@ -9,7 +9,7 @@ import clrrt
 from clrrt import abi, scenes
 
 ms = float(sys.argv[1]) if len(sys.argv) > 1 else 1000.0
-budgets = [int(b) for b in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
+budgets = [int(b) for b in sys.argv[2].split(",")] if len(sys.argv) > 2 and sys.argv[2] else []
 obs = scenes.urban_scene(200)
 pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=4 << 20,
                    max_rows=1 << 28, max_batch=16384)
@@ -24,8 +24,9 @@ smp = list(clrrt.Rng(77).draw_samples(pl.params, 16384))
 ex = np.array([s.explore for s in smp])
 
 
-def timed(sub, modes, budget):
+def timed(sub, modes, budget, ordered=False):
     pl.set_nn_grid(0 if modes else 1 << 40, modes, budget)
+    pl.set_option("nn_ordered_min", 0 if ordered else 1 << 40)
     ref = pl.sort_nodes_batch(sub, exact=False)
     torch.cuda.synchronize()
     pl.reset_counters()
@@ -37,7 +38,9 @@ def timed(sub, modes, budget):
 for label, sel in (("explore", ex == 1), ("optimize", ex == 0), ("all", ex >= 0)):
     sub = [s for s, k in zip(smp, sel) if k]
     tb, ids_b, _ = timed(sub, 0, 0)
-    print(f"  {label:8s} {len(sub):5d} samples brute force: {tb:.1f} ms")
+    to, ids_o, _ = timed(sub, 0, 0, ordered=True)
+    print(f"  {label:8s} {len(sub):5d} samples brute force: {tb:.1f} ms, place-ordered: {to:.1f} ms "
+          f"equal={np.array_equal(ids_b, ids_o)}")
     for b in budgets:
         for modes in (1, 3):
             tg, ids_g, stt = timed(sub, modes, b)
