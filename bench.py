@@ -128,12 +128,9 @@ def main():
     stream = torch.cuda.current_stream()
     pl.set_stream(stream.cuda_stream)
 
-    rec_bytes = 160
     if world > 1:
-        out_buf = torch.empty((2 * B, rec_bytes), dtype=torch.uint8, device="cuda")
-        gathered = torch.empty((world, 2 * B, rec_bytes), dtype=torch.uint8, device="cuda")
-        meta = torch.zeros(2, dtype=torch.float64, device="cuda")
-        meta_all = torch.zeros((world, 2), dtype=torch.float64, device="cuda")
+        from clrrt import dist as cdist
+        out_buf = torch.empty((2 * B, cdist.REC_BYTES), dtype=torch.uint8, device="cuda")
 
     def query(seed):
         """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""
@@ -151,21 +148,15 @@ def main():
                 cap_stop = 1
                 break
             allsmp = rng.draw_samples(params, world * B)
-            mine = (abi.Sample * B).from_buffer(allsmp, rank * B * C_SAMPLE)
+            first, count = cdist.shard(world * B, world, rank)
+            mine = (abi.Sample * count).from_buffer(allsmp, first * C_SAMPLE)
             n_local = pl.round_eval(mine, out_buf.data_ptr())
-            meta[0] = float(n_local)
-            meta[1] = (time.perf_counter() - t0) * 1e3
-            dist.all_gather_into_tensor(meta_all.view(-1), meta)
-            dist.all_gather_into_tensor(gathered.view(-1), out_buf.view(-1))
-            counts = meta_all[:, 0].to(torch.int64).tolist()
-            parts = [gathered[r, :counts[r]] for r in range(world)]
-            cat = torch.cat(parts, 0).contiguous()
-            total = cat.shape[0]
-            first = sum(counts[:rank])
-            pl.round_commit(cat.data_ptr(), total, first, counts[rank])
-            nodes += total
-            goals += int(cat[:, 140:144].contiguous().view(torch.int32).sum().item()) if total else 0
-            if float(meta_all[:, 1].max().item()) >= horizon:
+            cat, counts, my_first, t_max = cdist.exchange_round(out_buf, n_local,
+                                                                (time.perf_counter() - t0) * 1e3)
+            pl.round_commit(cat.data_ptr() if cat.shape[0] else 0, cat.shape[0], my_first, counts[rank])
+            nodes += cat.shape[0]
+            goals += cdist.goal_count(cat)
+            if t_max >= horizon:
                 break
         return nodes, goals, cap_stop
 

@@ -7,6 +7,7 @@ import ctypes as C
 
 CLRRT_ABI_VERSION = 3  # include/clrrt.h
 CLRRT_MODE_EXACT = 0
+CLRRT_PARENT_PREV = -2  # goal-biased record: parent = the record before it (include/clrrt.h)
 CLRRT_MODE_BATCH = 1
 CLRRT_COLLISION_STUB = 0
 CLRRT_COLLISION_OBB = 1
