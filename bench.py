@@ -60,6 +60,28 @@ def parse():
     return ap.parse_args()
 
 
+def measured_traffic():
+    """HBM bytes per rollout launch from the committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE
+    collected in separate runs, MI355X_MICROARCH.md HBM section); bench.py cannot collect counters
+    itself.  Returns (bytes or None, note)."""
+    import glob
+    prof = os.path.join(ROOT, "profiles")
+    fetch = sorted(glob.glob(os.path.join(prof, "r*_cfg3_pmc_fetch.json")))
+    write = sorted(glob.glob(os.path.join(prof, "r*_cfg3_pmc_write.json")))
+    if not fetch or not write:
+        return None, "no PMC profile committed"
+    try:
+        f = json.load(open(fetch[-1]))
+        w = json.load(open(write[-1]))
+        kb = 0.0
+        for name in ("void clrrt::k_roll_prep<false>", "void clrrt::k_roll_run<false>"):
+            kb += 2.0 * f[name]["per_dispatch"]["FETCH_SIZE"] + w[name]["per_dispatch"]["WRITE_SIZE"]
+        return kb * 1024.0, (f"{os.path.basename(fetch[-1])} + {os.path.basename(write[-1])}: "
+                             "(2 x FETCH_SIZE [gfx950 half-count correction] + WRITE_SIZE) KiB per launch")
+    except (KeyError, OSError, ValueError) as e:
+        return None, f"PMC profile unreadable: {e}"
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -197,6 +219,7 @@ def main():
             dist.destroy_process_group()
         return
 
+    traffic, traffic_note = measured_traffic()
     fp64 = FLOP_STEP * work["steps"] + FLOP_SCAN * work["scan_points"]
     fp32 = FLOP_BOX * work["box_tests"]
     achieved_tf = (fp64 + fp32) / (roll_ms * 1e-3) / 1e12 if roll_ms > 0 else 0.0
@@ -228,12 +251,13 @@ def main():
         },
         "roofline": {
             "bound": "valu",
-            "kernel": "k_rollout (speculative candidates + goal-bias + row replay)",
+            "kernel": "k_roll_prep + k_roll_run (candidate and goal-biased rollouts)",
             "achieved": achieved_tf,
             "peak": peak_tf,
             "unit": "TFLOP/s",
             "frac": achieved_tf / peak_tf if peak_tf else 0.0,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_note": traffic_note,
             "launches": roll_n,
             "avg_launch_ms": roll_ms / roll_n if roll_n else 0.0,
             "flop_per_launch": (fp64 + fp32) / roll_n if roll_n else 0.0,

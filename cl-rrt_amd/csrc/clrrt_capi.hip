@@ -72,7 +72,7 @@ struct clrrt_ctx {
   RollRes* res_spec = nullptr;
   clrrt_node* regnodes = nullptr;
   RollRes* res_gb = nullptr;
-  double* slots = nullptr;  // rollout rows of one round, [2][slot_rows][10][max_batch * CAND_K]
+  double* slots = nullptr;  // rollout rows of one round, [2][max_batch * CAND_K][slot_rows][10]
   int slot_rows = 0;
   clrrt_node* gbnodes = nullptr;
   SampleOut* so = nullptr;

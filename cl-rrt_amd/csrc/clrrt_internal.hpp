@@ -78,7 +78,7 @@ struct RollArgs {
   const Job* __restrict__ jobs;
   const BakedObs* __restrict__ obs;
   double* __restrict__ arena;              // rows destination (LIST with row_off >= 0)
-  double* __restrict__ slots;              // SPEC rows, see k_rollout
+  double* __restrict__ slots;              // SPEC rows, see k_rollout (job-major, rows contiguous)
   int slot_rows, slot_jobs;
   RollRes* __restrict__ res;               // regular rollout of each job
   RollRes* __restrict__ res_gb;            // SPEC: goal-biased rollout (outcome -1 = not run)

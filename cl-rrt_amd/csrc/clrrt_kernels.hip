@@ -525,7 +525,8 @@ __device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const dou
 //             rollout from the node it would append (expandTree rrtplanner.cpp:163-173), so goal
 //             bias overlaps other samples' candidates instead of forming a serial tail.  Rows go to
 //             job slots, interleaved across jobs: element k of row i of job j, pass p (0 regular,
-//             1 goal-biased) at slots[((p * slot_rows + i) * 10 + k) * slot_jobs + j].
+//             1 goal-biased) at slots[((p * slot_jobs + j) * slot_rows + i) * 10 + k] (a job's rows are
+//             contiguous, so a lane's consecutive row stores fill whole cache lines).
 //   SRC_LIST: explicit jobs (parity entry): parent = tree node, rows to arena[row_off] when >= 0.
 // Stage the obstacle cull table (and static-obstacle grid) of the query in LDS.
 template <bool NEED_GAP>
@@ -571,7 +572,8 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
   int gb = 0;
   double* rows = nullptr;
   int64_t es = 1;
-  const int64_t pass_stride = (int64_t)a.slot_rows * 10 * a.slot_jobs;
+  const int64_t slot = (int64_t)a.slot_rows * 10;
+  const int64_t pass_stride = slot * a.slot_jobs;
   if (act) {
     const clrrt_node* n = nullptr;
     if (SRC == SRC_SPEC) {
@@ -584,7 +586,7 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
         n = &a.tree[id];
         sx = a.samples[j / CAND_K].x;
         sy = a.samples[j / CAND_K].y;
-        if (a.slots) { rows = a.slots + j; es = a.slot_jobs; }
+        if (a.slots) rows = a.slots + j * slot;
       }
     } else {
       const Job& jb = a.jobs[j];
@@ -618,7 +620,7 @@ __global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
       for (int k = 0; k < 10; k++) ps.v[k] = out.st[k];
       pbx = out.bx; pby = out.by; pvb = out.vback;
       gb = 1;
-      if (a.slots) rows = a.slots + pass_stride + j;
+      if (a.slots) rows = a.slots + pass_stride + j * slot;
     }
   }
   if (a.ctr) {  // algorithmic work counters (roofline): block reduction, one atomic per block
@@ -679,11 +681,10 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
   ini.valid = 1;
   ini.pad = 0;
   prep[j] = ini;
-  const int64_t es = a.slot_jobs;
-  double* rows = a.slots + j;
+  double* rows = a.slots + (int64_t)j * a.slot_rows * 10;
 #pragma unroll
-  for (int k = 0; k < 10; k++) rows[k * es] = ps.v[k];
-  rows[7 * es] = ini.c7;
+  for (int k = 0; k < 10; k++) rows[k] = ps.v[k];
+  rows[7] = ini.c7;
 }
 
 #define REFILL_MIN 8
@@ -695,8 +696,8 @@ __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int lane = threadIdx.x & 63;
-  const int64_t es = a.slot_jobs;
-  const int64_t pass_stride = (int64_t)a.slot_rows * 10 * es;
+  const int64_t slot = (int64_t)a.slot_rows * 10;
+  const int64_t pass_stride = slot * a.slot_jobs;
   WorkCtr w{0, 0, 0};
   Roll r;
   double c7 = 0, c8 = 0, c9 = 0;
@@ -742,7 +743,7 @@ __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __
     steps++;
     int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w);
     w.steps++;
-    store_row(a.slots + pass * pass_stride + j + (int64_t)steps * 10 * es, es, r, c7, c8, c9);
+    store_row(a.slots + pass * pass_stride + j * slot + (int64_t)steps * 10, 1, r, c7, c8, c9);
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
       RollRes out;
@@ -762,10 +763,10 @@ __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __
         c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
         pass = 1;
         steps = 0;
-        double* rows = a.slots + pass_stride + j;
+        double* rows = a.slots + pass_stride + j * slot;
 #pragma unroll
-        for (int q = 0; q < 10; q++) rows[q * es] = out.st[q];
-        rows[7 * es] = c7;
+        for (int q = 0; q < 10; q++) rows[q] = out.st[q];
+        rows[7] = c7;
       } else {
         a.res_gb[j].outcome = -1;
         j = -1;
@@ -969,9 +970,9 @@ __global__ void __launch_bounds__(256) k_copy_rows(const Job* __restrict__ jobs,
   const int i = blockIdx.x;
   const Job jb = jobs[i];
   const int n = recs[i].nrows * 10;
-  const double* src = slots + (int64_t)jb.gb * slot_rows * 10 * slot_jobs + jb.parent;
+  const double* src = slots + ((int64_t)jb.gb * slot_jobs + jb.parent) * slot_rows * 10;
   double* dst = arena + jb.row_off * 10;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) dst[t] = src[(int64_t)t * slot_jobs];
+  for (int t = threadIdx.x; t < n; t += blockDim.x) dst[t] = src[t];
 }
 
 __global__ void __launch_bounds__(256) k_bbox(const clrrt_node* __restrict__ recs, const int64_t* n_dev, int n_host,
