@@ -95,6 +95,7 @@ struct clrrt_ctx {
   int nng_budget = 0;
   // persistent rollouts (k_roll_prep + k_roll_run)
   int roll_persistent = 1;
+  int nn_debug = 0;
   int roll_blocks = 0;       // persistent blocks (0: 2 per CU)
   int n_cu = 256;
   void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
@@ -434,8 +435,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
   chk(dalloc(&c->fb_count, 1));
-  chk(dalloc(&c->work_ctr, 16));
-  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 16 * sizeof(unsigned long long)));
+  chk(dalloc(&c->work_ctr, 24));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 24 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
@@ -705,7 +706,7 @@ int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 16 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 24 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return CLRRT_OK;
 }
@@ -720,13 +721,13 @@ int clrrt_work_counters(clrrt_ctx* c, int64_t out[3]) {
   return CLRRT_OK;
 }
 
-int clrrt_nn_stats(clrrt_ctx* c, int64_t out[8]) {
+int clrrt_nn_stats(clrrt_ctx* c, int64_t out[10]) {
   if (!c || !out) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipStreamSynchronize(c->stream));
-  unsigned long long h[8];
+  unsigned long long h[10];
   HIPC(c, hipMemcpy(h, c->work_ctr + 8, sizeof(h), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 8; i++) out[i] = (int64_t)h[i];
+  for (int i = 0; i < 10; i++) out[i] = (int64_t)h[i];
   out[4] &= 0xffffffff;
   return CLRRT_OK;
 }
@@ -736,6 +737,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   const std::string k(key);
   if (k == "roll_persistent") c->roll_persistent = value != 0;
   else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
+  else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
   return CLRRT_OK;
@@ -812,6 +814,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   // (samples of this round lie in the sample region, nodes in the tree's box); each float rounding
   // of a coordinate difference errs by <= 2^-24 E, a squared distance difference by a few of them
   NnFrame fr;
+  fr.debug = c->nn_debug;
   fr.ox = 0.5 * (x0 + x1);
   fr.oy = 0.5 * (y0 + y1);
   {
@@ -825,13 +828,18 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && region_ok;
   if (use_grid || ordered) {
     double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
-    auto supers = [&](double c) { return std::ceil(std::ceil(W / c) / 8) * std::ceil(std::ceil(H / c) / 8); };
-    while (supers(cs) * 64 > (double)kNngMaxCells) cs *= 1.1;
+    // square power-of-two grid (Morton cell numbering), at most kNngMaxCells cells
+    auto side = [&](double c) {
+      int n = 8;
+      while (n < std::ceil(std::max(W, H) / c)) n *= 2;
+      return n;
+    };
+    while ((double)side(cs) * side(cs) > (double)kNngMaxCells) cs *= 1.1;
     g.x0 = x0; g.y0 = y0; g.cs = cs; g.inv = 1.0 / cs;
     g.slack = 1e-9 * (1.0 + std::fabs(x0) + std::fabs(y0) + W + H);
-    g.sw = ((int)std::ceil(W / cs) + 7) / 8; g.sh = ((int)std::ceil(H / cs) + 7) / 8;
-    g.gw = 8 * g.sw; g.gh = 8 * g.sh;
-    g.ncell = 64 * g.sw * g.sh;
+    g.gw = g.gh = side(cs);
+    g.sw = g.sh = g.gw / 8;
+    g.ncell = g.gw * g.gh;
     g.modes = c->nng_modes;
     g.budget = c->nng_budget;
     HIPC(c, launch_nn_grid_build(st, c->nn, (int)c->n_nodes, g, c->nng));

@@ -142,6 +142,7 @@ hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, c
 struct NnFrame {
   double ox, oy;
   float delta;
+  int debug;  // diagnostics only (results change!): 1 = skip the exact pass
 };
 
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose

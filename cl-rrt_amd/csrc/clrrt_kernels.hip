@@ -46,6 +46,15 @@ __device__ __forceinline__ void topk_insert(float (&keys)[NN_K], int (&ids)[NN_K
   }
 }
 
+// Order-preserving float <-> uint32 (atomicMin over signed floats).
+__device__ __forceinline__ unsigned int ord_enc32(float f) {
+  unsigned int b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord_dec32(unsigned int u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
 // Prune radius for a lane: a node at Euclidean distance |q| > prune_r(kth - cost) cannot enter the
 // list (key >= |q| (1 - 1e-5) - 1e-4 under float rounding, see dubins_key; this radius is looser).
 // Negative: nothing can enter.  NaN slack gives NaN (never prunes).
@@ -80,8 +89,10 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
                                                     int* __restrict__ pi, const int* __restrict__ sidx,
                                                     const int* __restrict__ scount, const float4* __restrict__ tbox,
                                                     const float* __restrict__ tcost, const int* __restrict__ home,
-                                                    const float* __restrict__ seed) {
+                                                    const float* __restrict__ seed, unsigned long long* tstat) {
+  int tiles_seen = 0, tiles_done = 0, n_queued = 0, n_exact = 0;
   __shared__ float4 s_r[256];   // node x, y and ref.back() x, y relative to the frame origin (float)
+  __shared__ double2 s_p[256];  // node x, y
   __shared__ float4 s_f[256];   // c, s, ca, sa
   __shared__ float s_c[256];    // costE
   __shared__ int s_id[256];     // node id
@@ -107,9 +118,12 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   const float c45 = 0.69276f;                    // cos(pi/4 + 0.02), rounded down
   const float rho = 4.77f, rin = rho - 0.01f - 4.f * fr.delta;  // "deep inside" radius
   const float rin2 = rin > 0.f ? rin * rin : -1.f;
-  // kcap: an upper bound on the sample's final 11th key over the whole tree (seed pass), so the
-  // chunk's pruning starts tight: a node with key > kcap cannot be in the merged list
-  const float kcap = (seed && act) ? seed[s] : __builtin_inff();
+  // kcap: an upper bound on the sample's final 11th key over the whole tree, so the chunk's pruning
+  // starts tight: a node with key > kcap cannot be in the merged list.  It starts from the seed pass
+  // and is shared between the sample's chunks through gcap[s] (order-preserving uint encoding,
+  // atomicMin): every chunk's own 11th key bounds the tree's 11th key too.
+  unsigned int* gcap = (unsigned int*)seed;
+  float kcap = (seed && act) ? ord_dec32(__atomic_load_n(&gcap[s], __ATOMIC_RELAXED)) : __builtin_inff();
   float rr = __builtin_inff();  // explore: (prune radius + delta)^2 for the current 11th key
   if (kcap < __builtin_inff()) {
     const float R = prune_r(kcap);
@@ -117,19 +131,30 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   }
   const int me = threadIdx.x;
   auto drain = [&](int b, int cnt) {
+    if (fr.debug == 1) return;
     for (int i = 0; i < cnt; i++) {
       const int k = s_q[i][me];
       const int n = s_id[k];
+      // cheap lower bound on the key first (clrrt_dubins_lb.hpp), from the LDS copy of the tile
+      const double2 np = s_p[k];
+      const float4 f = s_f[k];
+      const float cost = s_c[k];
+      const float qx = (float)(sx - np.x), qy = (float)(sy - np.y);
+      const float tx = f.x * qx - f.y * qy, ty = fabsf(f.y * qx + f.x * qy);
+      float lb = dubins_lb(tx, ty);
+      if (!ex) lb = cost + lb;
+      if (lb > keys[NN_K - 1]) continue;
+      n_exact++;
+      float key = dubins_key(sx, sy, np.x, np.y, f.x, f.y);
+      if (!ex) key = cost + key;
+      if (!lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1])) continue;
       const NnRec& rec = nodes[b + k];
-      const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
-      if (!nn_prefilter(sx, sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, ex,
-                        keys[NN_K - 1], feas2))
-        continue;
-      float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
-      if (!ex) key = rec.costE + key;
-      if (lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) &&
-          feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
+      if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
         topk_insert(keys, ids, key, n);
+        if (seed && keys[NN_K - 1] < kcap) {
+          kcap = keys[NN_K - 1];
+          atomicMin(&gcap[s], ord_enc32(kcap));
+        }
         const float R = prune_r(fminf(keys[NN_K - 1], kcap));
         rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
       }
@@ -160,6 +185,14 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
     }
     const int m = min(256, N - b);
     bool need = act;
+    if (seed && act) {  // pick up tighter bounds published by the sample's other chunks
+      const float kc = ord_dec32(__atomic_load_n(&gcap[s], __ATOMIC_RELAXED));
+      if (kc < kcap) {
+        kcap = kc;
+        const float R = prune_r(fminf(keys[NN_K - 1], kcap));
+        rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+      }
+    }
     if (tbox) {
       // the tile's Euclidean bound (the same float positions the node test uses)
       const float4 bx = tbox[b >> 8];
@@ -172,16 +205,19 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
         lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
       }
       need = act && !(bd2 > lim);  // NaN bounds never skip
+      tiles_seen++;
       if (!__syncthreads_or(need)) continue;
+      tiles_done++;
     }
     __syncthreads();
-    if ((int)threadIdx.x < m) {
-      const NnRec& rec = nodes[b + threadIdx.x];
-      s_r[threadIdx.x] = make_float4((float)(rec.x - fr.ox), (float)(rec.y - fr.oy), (float)(rec.bx - fr.ox),
-                                     (float)(rec.by - fr.oy));
-      s_f[threadIdx.x] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
-      s_c[threadIdx.x] = rec.costE;
-      s_id[threadIdx.x] = tbox ? rec.id : b + (int)threadIdx.x;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+      const NnRec& rec = nodes[b + i];
+      s_r[i] = make_float4((float)(rec.x - fr.ox), (float)(rec.y - fr.oy), (float)(rec.bx - fr.ox),
+                           (float)(rec.by - fr.oy));
+      s_f[i] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
+      s_c[i] = rec.costE;
+      s_p[i] = make_double2(rec.x, rec.y);
+      s_id[i] = tbox ? rec.id : b + i;
     }
     __syncthreads();
     if (!need) continue;
@@ -207,6 +243,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
       const bool in_bad = deep && !(ex ? in_ok : (cost + 14.9f <= kth));
       if (near && !ang_bad && !in_bad) {
+        n_queued++;
         s_q[cnt][me] = (uint8_t)k;
         if (++cnt == NN_QCAP) {
           drain(b, cnt);
@@ -220,6 +257,14 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
     size_t base = ((size_t)t * nchunks + c) * NN_K;
 #pragma unroll
     for (int j = 0; j < NN_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
+  }
+  if (tstat) {  // diagnostics: tiles considered / searched per block, queued pairs, exact keys
+    if (threadIdx.x == 0) {
+      atomicAdd(&tstat[0], (unsigned long long)tiles_seen);
+      atomicAdd(&tstat[1], (unsigned long long)tiles_done);
+    }
+    atomicAdd(&tstat[2], (unsigned long long)n_queued);
+    atomicAdd(&tstat[3], (unsigned long long)n_exact);
   }
 }
 
@@ -1095,7 +1140,8 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
                                   float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
                                   const int* scount, const float4* tbox = nullptr, const float* tcost = nullptr,
-                                  const int* home = nullptr, const float* seed = nullptr);
+                                  const int* home = nullptr, const float* seed = nullptr,
+                                  unsigned long long* tstat = nullptr);
 
 // Per 256-node tile of the place-ordered records: bounding box of the float frame positions the
 // brute-force prune uses, and the minimum cost (NaN if any cost is NaN).
@@ -1167,25 +1213,27 @@ __global__ void __launch_bounds__(256) k_nn_seed(const clrrt_sample* __restrict_
         feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
       topk_insert(keys, ids, key, rec.id);
   }
-  seed[s] = keys[NN_K - 1];
+  ((unsigned int*)seed)[s] = ord_enc32(keys[NN_K - 1]);
 }
 
 hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
                             const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
                             int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
-                            float4* tbox, float* tcost, const int* home, float* seed) {
+                            float4* tbox, float* tcost, const int* home, float* seed,
+                            unsigned long long* tstat) {
   hipLaunchKernelGGL(k_tile_bounds, dim3((N + 255) / 256), dim3(256), 0, st, sorted, N, fr, tbox, tcost);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_seed, dim3((B + 255) / 256), dim3(256), 0, st, S, B, sorted, N, p, order, home, seed);
   LAUNCH_CHECK();
   return launch_nn_brute(st, S, B, sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, order, nsamp,
-                         tbox, tcost, home, seed);
+                         tbox, tcost, home, seed, tstat);
 }
 
 hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
                             const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
                             int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
-                            float4* tbox, float* tcost, const int* home, float* seed);
+                            float4* tbox, float* tcost, const int* home, float* seed,
+                            unsigned long long* tstat);
 
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
@@ -1197,7 +1245,8 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
     if (e != hipSuccess) return e;
     if ((e = hipMemsetD32Async((hipDeviceptr_t)gbufs->nsamp, B, 1, st)) != hipSuccess) return e;
     e = launch_nn_sorted(st, S, B, gbufs->sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks,
-                         gbufs->order, gbufs->nsamp, gbufs->tbox, gbufs->tcost, gbufs->home, gbufs->seed);
+                         gbufs->order, gbufs->nsamp, gbufs->tbox, gbufs->tcost, gbufs->home, gbufs->seed,
+                         stats ? stats + 5 : nullptr);
     if (e != hipSuccess) return e;
   } else if (grid) {
     // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
@@ -1213,8 +1262,11 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
     e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
     if (e != hipSuccess) return e;
   } else {
-    hipError_t e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr,
-                                   nullptr);
+    // shared per-sample key caps start at +inf (order-preserving encoding of +inf = 0xff800000)
+    hipError_t e = gbufs ? hipMemsetD32Async((hipDeviceptr_t)gbufs->seed, 0xff800000u, B, st) : hipSuccess;
+    if (e != hipSuccess) return e;
+    e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr, nullptr,
+                        nullptr, nullptr, nullptr, gbufs ? gbufs->seed : nullptr, stats ? stats + 5 : nullptr);
     if (e != hipSuccess) return e;
   }
   if (exact_scratch) {
@@ -1229,16 +1281,18 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
                                   float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
                                   const int* scount, const float4* tbox, const float* tcost, const int* home,
-                                  const float* seed) {
+                                  const float* seed, unsigned long long* tstat) {
+  int threads = 256;
   int groups = (B + 255) / 256;
   int nchunks = (N + 255) / 256;
   int want = max(1, 2048 / max(1, groups));  // aim for >= 2048 blocks of 4 waves
   nchunks = max(1, min(nchunks, min(want, max_chunks)));
+
   int chunk = (N + nchunks - 1) / nchunks;
   chunk = (chunk + 255) & ~255;  // tiles of 256 nodes never straddle chunks
   nchunks = (N + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, fr, pk, pi, sidx, scount, tbox, tcost, home, seed);
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(threads), 0, st, S, B, nodes, N, chunk, nchunks,
+                     p, fr, pk, pi, sidx, scount, tbox, tcost, home, seed, tstat);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      cand, ckey, ncand, ctie, sidx, scount);

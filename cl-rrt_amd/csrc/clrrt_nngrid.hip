@@ -44,10 +44,21 @@ __device__ __forceinline__ float ord_dec(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-// cell number of grid cell (gx, gy): super-cell-major
-__device__ __forceinline__ int cell_of(const NnGrid& g, int gx, int gy) {
-  return ((gy >> 3) * g.sw + (gx >> 3)) * 64 + (gy & 7) * 8 + (gx & 7);
+// Cells are numbered in Morton (Z) order on a square power-of-two grid, so any aligned 2^k x 2^k
+// block -- in particular an 8x8 super-cell -- is a contiguous range, and consecutive records of the
+// place-ordered array are close in the plane.
+__device__ __forceinline__ uint32_t spread2(uint32_t v) {  // bits of v to the even positions
+  v &= 0xffff;
+  v = (v | (v << 8)) & 0x00ff00ff;
+  v = (v | (v << 4)) & 0x0f0f0f0f;
+  v = (v | (v << 2)) & 0x33333333;
+  v = (v | (v << 1)) & 0x55555555;
+  return v;
 }
+__device__ __forceinline__ int morton(int x, int y) { return (int)(spread2((uint32_t)x) | (spread2((uint32_t)y) << 1)); }
+__device__ __forceinline__ int cell_of(const NnGrid& g, int gx, int gy) { return morton(gx, gy); }
+// super-cell (X, Y) holds cells [64 morton(X, Y), 64 morton(X, Y) + 64)
+__device__ __forceinline__ int super_of(int X, int Y) { return morton(X, Y); }
 
 __device__ __forceinline__ int node_cell(const NnGrid& g, double x, double y) {
   double fx = (x - g.x0) * g.inv, fy = (y - g.y0) * g.inv;
@@ -133,7 +144,7 @@ __device__ __forceinline__ int sample_bucket(const NnGrid& g, const clrrt_sample
   if (!(isfinite(fx) && isfinite(fy))) return 2 * SG;
   const int X = (int)fmin((double)(g.sw - 1), fmax(0.0, floor(fx)));
   const int Y = (int)fmin((double)(g.sh - 1), fmax(0.0, floor(fy)));
-  return (s.explore ? 0 : SG) + Y * g.sw + X;
+  return (s.explore ? 0 : SG) + super_of(X, Y);
 }
 
 __global__ void __launch_bounds__(256) k_smp_count(const clrrt_sample* __restrict__ S, int B, NnGrid g,
@@ -274,7 +285,7 @@ __device__ __forceinline__ void visit_super(Lane& L, const NnGrid& g, int SX, in
     truncated = true;
     return;
   }
-  const int sc = SY * g.sw + SX;
+  const int sc = super_of(SX, SY);
   const uint32_t sm = g.smin[sc];
   if (sm == 0xffffffffu) return;  // empty
   bool need = false;
@@ -290,7 +301,8 @@ __device__ __forceinline__ void visit_super(Lane& L, const NnGrid& g, int SX, in
     if (a == b) continue;
     bool take = false;
     if (need) {
-      const int gx = SX * SUPER + (c & 7), gy = SY * SUPER + (c >> 3);
+      const int gx = SX * SUPER + (c & 1) + ((c >> 1) & 2) + ((c >> 2) & 4);
+      const int gy = SY * SUPER + ((c >> 1) & 1) + ((c >> 2) & 2) + ((c >> 3) & 4);
       float lb = key_lb(rect_dist(g, L.sx, L.sy, gx, gy, gx + 1, gy + 1));
       if (!L.ex) lb = ord_dec(g.cmin[base + c]) + lb;
       take = !(lb > L.keys[NN_K - 1]);

@@ -274,10 +274,12 @@ int clrrt_set_nn_grid(clrrt_ctx* ctx, int64_t min_nodes, int32_t modes, int32_t 
  * blocks of 256 lanes; 0: two per compute unit), "nn_ordered_min" (trees of at least this many
  * nodes use the place-ordered brute-force search that skips far node tiles; default: never). */
 int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
-/* Diagnostics of the grid nearest-node search since the last clrrt_reset_counters: out[0] waves,
- * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget,
- * out[4] samples handed to brute force by the LAST search. */
-int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[8]);
+/* Nearest-node search diagnostics since the last clrrt_reset_counters.  Grid search: out[0] waves,
+ * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget, out[4]
+ * samples handed to brute force by the LAST search.  Brute force: out[5] / out[6] node tiles
+ * considered / searched (place-ordered strategy), out[7] (sample, node) pairs passing the float
+ * prefilter, out[8] exact Dubins keys evaluated. */
+int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[10]);
 
 #ifdef __cplusplus
 }

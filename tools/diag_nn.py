@@ -37,10 +37,17 @@ def timed(sub, modes, budget, ordered=False):
 
 for label, sel in (("explore", ex == 1), ("optimize", ex == 0), ("all", ex >= 0)):
     sub = [s for s, k in zip(smp, sel) if k]
-    tb, ids_b, _ = timed(sub, 0, 0)
-    to, ids_o, _ = timed(sub, 0, 0, ordered=True)
+    tb, ids_b, sb = timed(sub, 0, 0)
+    to, ids_o, so = timed(sub, 0, 0, ordered=True)
     print(f"  {label:8s} {len(sub):5d} samples brute force: {tb:.1f} ms, place-ordered: {to:.1f} ms "
-          f"equal={np.array_equal(ids_b, ids_o)}")
+          f"equal={np.array_equal(ids_b, ids_o)} tiles {so['tiles_searched']}/{so['tiles_seen']}")
+    print(f"      brute: queued {sb['pairs_queued']} exact {sb['exact_keys']}; ordered: queued {so['pairs_queued']} "
+          f"exact {so['exact_keys']}")
+    pl.set_option("nn_debug", 1)
+    tn, _, _ = timed(sub, 0, 0)
+    tno, _, _ = timed(sub, 0, 0, ordered=True)
+    pl.set_option("nn_debug", 0)
+    print(f"      without the exact pass: brute {tn:.1f} ms, ordered {tno:.1f} ms")
     for b in budgets:
         for modes in (1, 3):
             tg, ids_g, stt = timed(sub, modes, b)
