@@ -224,25 +224,41 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
     int cnt = 0;
     const float kth = fminf(keys[NN_K - 1], kcap);
     const bool in_ok = (ex ? 14.9f : -__builtin_inff()) <= kth;  // explore: inside circles can enter
-    for (int k = 0; k < m; k++) {
-      const float4 q = s_r[k];
-      const float4 f = s_f[k];
-      const float cost = s_c[k];
-      const float dx = rsx - q.x, dy = rsy - q.y;
-      const float d2 = dx * dx + dy * dy;
-      float lim = rr;
-      if (!ex) {
-        const float R = prune_r(kth - cost);
-        lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+    for (int k0 = 0; k0 < m; k0 += 4) {
+      // four nodes per pass: their LDS reads are issued together
+      float4 q[4];
+      float cst[4];
+      bool nr[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int k = min(k0 + u, m - 1);
+        q[u] = s_r[k];
+        cst[u] = s_c[k];
       }
-      const bool near = (d2 <= lim) || (lim != lim);  // a NaN limit never prunes
-      const float vx = rsx - q.z, vy = rsy - q.w;
-      const float dot = vx * f.z + vy * f.w, vv = vx * vx + vy * vy;
-      const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
-      const float tx = f.x * dx - f.y * dy, ty = fabsf(f.y * dx + f.x * dy);
-      const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
-      const bool in_bad = deep && !(ex ? in_ok : (cost + 14.9f <= kth));
-      if (near && !ang_bad && !in_bad) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float dx = rsx - q[u].x, dy = rsy - q[u].y;
+        const float d2 = dx * dx + dy * dy;
+        float lim = rr;
+        if (!ex) {
+          const float R = prune_r(kth - cst[u]);
+          lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
+        }
+        nr[u] = (k0 + u < m) && ((d2 <= lim) || (lim != lim));  // a NaN limit never prunes
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (!nr[u]) continue;
+        const int k = k0 + u;
+        const float4 f = s_f[k];
+        const float dx = rsx - q[u].x, dy = rsy - q[u].y;
+        const float vx = rsx - q[u].z, vy = rsy - q[u].w;
+        const float dot = vx * f.z + vy * f.w, vv = vx * vx + vy * vy;
+        const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
+        const float tx = f.x * dx - f.y * dy, ty = fabsf(f.y * dx + f.x * dy);
+        const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
+        const bool in_bad = deep && !(ex ? in_ok : (cst[u] + 14.9f <= kth));
+        if (ang_bad || in_bad) continue;
         n_queued++;
         s_q[cnt][me] = (uint8_t)k;
         if (++cnt == NN_QCAP) {
