@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-queries", type=int, default=5, help="oracle queries timed for cpu_baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path (e.g. several ranks sharing one GPU)")
     return ap.parse_args()
 
 
@@ -132,9 +134,13 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(1, ndev))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     import clrrt
     from clrrt import abi, scenes
@@ -143,7 +149,7 @@ def main():
     params = clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
     max_nodes = args.max_nodes
     max_rows = max_nodes * args.rows_per_node
-    pl = clrrt.Planner(params, device=local, max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
+    pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
                        max_obstacles=max(1, len(obs)))
     pl.set_obstacles(obs)
     pl.set_rank(rank)
@@ -203,9 +209,21 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    trees_identical = None
+    if world > 1:
+        # every rank appended the same records in the same order: compare the trees of the last query
+        import numpy as np
+        raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
+        hdr = np.ascontiguousarray(raw[:, :148])  # headers without the owner / row-offset fields
+        sig = torch.tensor([float(hdr.shape[0]), float(hdr.view(np.int32).astype(np.int64).sum() % (1 << 40))],
+                           dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        sigs = [torch.empty_like(sig) for _ in range(world)]
+        dist.all_gather(sigs, sig)
+        trees_identical = all(bool(torch.equal(x, sigs[0])) for x in sigs)
 
     roll_ms, roll_n = pl.kernel_time(1)
     nn_ms, nn_n = pl.kernel_time(0)
@@ -248,6 +266,7 @@ def main():
             "mode": "BATCH",
             "parallelism": f"dp{world}",
             "capacity_stops": cap_stops,
+            "trees_identical_across_ranks": trees_identical,
         },
         "roofline": {
             "bound": "valu",

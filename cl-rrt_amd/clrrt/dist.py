@@ -25,15 +25,21 @@ def exchange_round(out_buf, n_local, elapsed_ms, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = out_buf.device
-    meta = torch.tensor([float(n_local), float(elapsed_ms)], dtype=torch.float64, device=dev)
+    # gloo moves host tensors only: stage device buffers through the host (CPU rehearsal of the path)
+    host = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+    cdev = torch.device("cpu") if host else dev
+    meta = torch.tensor([float(n_local), float(elapsed_ms)], dtype=torch.float64, device=cdev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
     counts = [int(m[0].item()) for m in metas]
     t_max = max(float(m[1].item()) for m in metas)
-    bufs = [torch.empty_like(out_buf) for _ in range(world)]
-    dist.all_gather(bufs, out_buf.contiguous(), group=group)
+    src = out_buf.to(cdev) if host else out_buf.contiguous()
+    bufs = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(bufs, src, group=group)
     parts = [bufs[r][:counts[r]] for r in range(world)]
-    cat = torch.cat(parts, 0).contiguous() if sum(counts) else out_buf[:0]
+    cat = torch.cat(parts, 0).contiguous() if sum(counts) else src[:0]
+    if host:
+        cat = cat.to(dev)
     return cat, counts, sum(counts[:rank]), t_max
 
 

@@ -543,7 +543,23 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
             double cx = (double)(float)b[i].cx, cy = (double)(float)b[i].cy;
             double dx = std::max(0.0, std::max(rx0 - cx, cx - rx1));
             double dy = std::max(0.0, std::max(ry0 - cy, cy - ry1));
-            if (dx * dx + dy * dy <= (rr[i] + tol) * (rr[i] + tol)) items.push_back((uint16_t)i);
+            if (dx * dx + dy * dy > (rr[i] + tol) * (rr[i] + tol)) continue;
+            // the kernel's second cull: the vehicle circle (VEH_RAD + margin) against the obstacle box.
+            // A separating-axis gap between the cell and the (slackened) box bounds their distance from
+            // below, so a gap beyond the circle radius proves no centre in the cell survives that cull.
+            const double P = b[i].P, Q = b[i].Q, R = b[i].R, S = b[i].S;
+            const double hh = std::sqrt(P * P + R * R), ww = std::sqrt(Q * Q + S * S);
+            const double ux = hh > 0 ? P / hh : 1.0, uy = hh > 0 ? R / hh : 0.0;
+            const double eh = hh * 1.0001 + 1e-3, ew = ww * 1.0001 + 1e-3;
+            const double rcx = 0.5 * (rx0 + rx1), rcy = 0.5 * (ry0 + ry1);
+            const double hx = 0.5 * (rx1 - rx0), hy = 0.5 * (ry1 - ry0);
+            const double ex = std::fabs(ux) * eh + std::fabs(uy) * ew, ey = std::fabs(uy) * eh + std::fabs(ux) * ew;
+            double gap = std::max(std::fabs(cx - rcx) - hx - ex, std::fabs(cy - rcy) - hy - ey);
+            const double du = (cx - rcx) * ux + (cy - rcy) * uy, dv = -(cx - rcx) * uy + (cy - rcy) * ux;
+            gap = std::max(gap, std::fabs(du) - eh - (hx * std::fabs(ux) + hy * std::fabs(uy)));
+            gap = std::max(gap, std::fabs(dv) - ew - (hx * std::fabs(uy) + hy * std::fabs(ux)));
+            if (gap > (double)(kVehRad + kCullMargin) + tol) continue;
+            items.push_back((uint16_t)i);
           }
         }
       start[(size_t)gw * gh] = (uint32_t)items.size();

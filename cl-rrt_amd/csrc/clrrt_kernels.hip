@@ -377,6 +377,26 @@ struct ObsView {
 
 // One obstacle against the vehicle box: bounding-circle cull (no overlap possible when the
 // circles are apart), then the SAT gap.
+__device__ __forceinline__ bool obs_culled(const ObsView& ov, int j, float ft, float fvx, float fvy) {
+  float4 q = ov.cv[j];
+  float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
+  float rr = ov.rad[j];
+  if (dx * dx + dy * dy > rr * rr) return true;
+  const float4 b = ov.ob[j];
+  const float e1 = fmaxf(fabsf(dx * b.x + dy * b.y) - b.z, 0.f);
+  const float e2 = fmaxf(fabsf(dy * b.x - dx * b.y) - b.w, 0.f);
+  const float vr = VEH_RAD + CULL_MARGIN;
+  return e1 * e1 + e2 * e2 > vr * vr;
+}
+
+__device__ __forceinline__ float obs_sat(const Box4& veh, const ObsView& ov, int j, double t) {
+  const BakedObs& o = ov.g[j];
+  if (!o.moving) return sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
+  float bvx[4], bvy[4], bnx[4], bny[4];
+  box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
+  return sat_gap(veh, bvx, bvy, bnx, bny);
+}
+
 __device__ __forceinline__ float obs_gap(const Box4& veh, const ObsView& ov, int j, double t, float ft,
                                          float fvx, float fvy, bool cull, bool& culled) {
   culled = false;
@@ -411,13 +431,11 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
   if (p.coll_mode == CLRRT_COLLISION_STUB) return 100.0;
   const double t = p.obs_use_pred ? r.x6 : 0.0;
   const double vpx = r.x0 + 1.424 * r.c2, vpy = r.x1 + 1.424 * r.s2;
-  const float of = (float)r.x2;
-  const float cf = cosf(of), sf = sinf(of);
   const float hh = 4.848f / 2, ww = 2.0f / 2;
-  Box4 veh;
-  box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
   const float fvx = (float)vpx, fvy = (float)vpy, ft = (float)t;
+  Box4 veh;
   if (!NEED_GAP && ov.gw > 0 && isfinite(fvx) && isfinite(fvy) && isfinite(ft)) {
+    bool have_veh = false;  // the vehicle box (setVertices) is built only when an obstacle survives the cull
     int a = 0, ae = 0;
     const int gx = (int)floorf((fvx - ov.gx0) * ov.ginv), gy = (int)floorf((fvy - ov.gy0) * ov.ginv);
     if (gx >= 0 && gx < ov.gw && gy >= 0 && gy < ov.gh) {
@@ -431,12 +449,22 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       const int jb = b < ov.nmov ? (int)ov.gmov[b] : 0x7fffffff;
       int j;
       if (ja < jb) { j = ja; a++; } else { j = jb; b++; }
-      bool culled;
-      float D = obs_gap(veh, ov, j, t, ft, fvx, fvy, true, culled);
-      if (!culled && D == 0) { tests += j + 1; return 0.0; }
+      if (obs_culled(ov, j, ft, fvx, fvy)) continue;
+      if (!have_veh) {
+        const float of = (float)r.x2;
+        const float cf = cosf(of), sf = sinf(of);
+        box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
+        have_veh = true;
+      }
+      if (obs_sat(veh, ov, j, t) == 0) { tests += j + 1; return 0.0; }
     }
     tests += ov.n;  // the reference tests every obstacle until the first overlap
     return 10000;
+  }
+  {
+    const float of = (float)r.x2;
+    const float cf = cosf(of), sf = sinf(of);
+    box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
   }
   double best = 10000;
   for (int j = 0; j < ov.n; j++) {
