@@ -517,13 +517,15 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
   std::vector<uint16_t> items;
   int gw = 0, gh = 0;
   float fx0 = 0, fy0 = 0, finv = 0;
-  // dynamic LDS of the rollout kernels (36 B per obstacle + grid) stays within 52 KiB so that, with the
-  // 9.3 KiB of libm tables, a block fits the default 64 KiB
-  const size_t lds_budget = b.size() * 36 < 52 * 1024 ? 52 * 1024 - b.size() * 36 : 0;
+  // dynamic LDS of the rollout kernels (36 B per obstacle + grid): the rollout kernels run one
+  // 256-lane block per CU (256 VGPRs), so up to ~140 KiB of the CU's 160 KiB serve the grid
+  // (launches raise hipFuncAttributeMaxDynamicSharedMemorySize accordingly)
+  const size_t lds_cap = 120 * 1024;
+  const size_t lds_budget = b.size() * 36 < lds_cap ? lds_cap - b.size() * 36 : 0;
   if (!stat.empty() && std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1) &&
       lds_budget >= 4 * 1024) {
     double W = x1 - x0, H = y1 - y0;
-    double cs = std::max(0.25, std::sqrt(W * H / 1024.0));
+    double cs = std::max(0.25, std::sqrt(W * H / 8192.0));
     for (int attempt = 0; attempt < 40; attempt++, cs *= 1.25) {
       finv = (float)(1.0 / cs);
       fx0 = (float)x0; fy0 = (float)y0;

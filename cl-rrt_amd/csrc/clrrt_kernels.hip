@@ -443,6 +443,21 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       a = ov.gstart[cell];
       ae = ov.gstart[cell + 1];
     }
+    if (ov.nmov == 0) {  // static obstacles only: plain walk of the cell list
+      for (; a < ae; a++) {
+        const int j = ov.gitems[a];
+        if (obs_culled(ov, j, ft, fvx, fvy)) continue;
+        if (!have_veh) {
+          const float of = (float)r.x2;
+          const float cf = cosf(of), sf = sinf(of);
+          box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
+          have_veh = true;
+        }
+        if (obs_sat(veh, ov, j, t) == 0) { tests += j + 1; return 0.0; }
+      }
+      tests += ov.n;
+      return 10000;
+    }
     int b = 0;
     while (a < ae || b < ov.nmov) {
       const int ja = a < ae ? (int)ov.gitems[a] : 0x7fffffff;
@@ -1363,7 +1378,14 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   if (a.p.need_gap)
     hipLaunchKernelGGL((k_rollout<SRC, true>), grid, block, 0, st, a);
   else
+  {
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)&k_rollout<SRC, false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL((k_rollout<SRC, false>), grid, block, lds, st, a);
+  }
   LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -1384,6 +1406,11 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, v
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
+    if (lds > 64 * 1024) {
+      hipError_t e2 = hipFuncSetAttribute((const void*)&k_roll_run<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds);
+      if (e2 != hipSuccess) return e2;
+    }
     hipLaunchKernelGGL((k_roll_run<false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   }
   LAUNCH_CHECK();
