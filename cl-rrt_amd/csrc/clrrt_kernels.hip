@@ -377,11 +377,12 @@ struct ObsView {
 
 // One obstacle against the vehicle box: bounding-circle cull (no overlap possible when the
 // circles are apart), then the SAT gap.
+// Vehicle bounding circle (VEH_RAD + margin around the box centre) against the obstacle box (with
+// slack): apart -> the two boxes cannot overlap.  (The grid lists already come from this test at the
+// cell level, so the bounding-circle pre-test of the brute-force path is not repeated.)
 __device__ __forceinline__ bool obs_culled(const ObsView& ov, int j, float ft, float fvx, float fvy) {
   float4 q = ov.cv[j];
   float dx = q.x + q.z * ft - fvx, dy = q.y + q.w * ft - fvy;
-  float rr = ov.rad[j];
-  if (dx * dx + dy * dy > rr * rr) return true;
   const float4 b = ov.ob[j];
   const float e1 = fmaxf(fabsf(dx * b.x + dy * b.y) - b.z, 0.f);
   const float e2 = fmaxf(fabsf(dy * b.x - dx * b.y) - b.w, 0.f);
