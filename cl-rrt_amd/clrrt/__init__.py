@@ -44,6 +44,8 @@ _SIGS = {
     "clrrt_tree_size": (C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64)]),
     "clrrt_tree_download": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(abi.Node)]),
     "clrrt_tree_rows": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(C.c_double)]),
+    "clrrt_extract_best_path": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int32), P(C.c_float),
+                                          P(C.c_int64)]),
     "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
@@ -219,6 +221,15 @@ class Planner:
         out = np.zeros((nrows, 10))
         self._chk(self.L.clrrt_tree_rows(self.h, row_offset, nrows, out.ctypes.data_as(P(C.c_double))), "tree_rows")
         return out
+
+    def extract_best_path(self, cap=4096):
+        """extractBestPath (rrtplanner.cpp:318-368): node ids root -> goal ([] when no node reached
+        the goal), the chosen node's costS and the number of goal nodes."""
+        ids = np.zeros(max(1, cap), dtype=np.int32)
+        n, cost, ng = C.c_int32(), C.c_float(), C.c_int64()
+        self._chk(self.L.clrrt_extract_best_path(self.h, ids.ctypes.data_as(P(C.c_int32)), cap, C.byref(n),
+                                                 C.byref(cost), C.byref(ng)), "extract_best_path")
+        return [int(v) for v in ids[:min(n.value, cap)]], float(cost.value), int(ng.value)
 
     def expand(self, rng, n_iters=0, budget_ms=0.0, mode=CLRRT_MODE_EXACT, batch=0):
         st = abi.Stats()

@@ -101,6 +101,9 @@ struct clrrt_ctx {
   void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
+  // extractBestPath scratch (allocated on first use, max_nodes entries each)
+  GoalRec* goal_recs = nullptr;
+  int* bp_path = nullptr;  // [max_nodes + 2]: chain, then count and length
   double reg_x0 = 0, reg_y0 = 0, reg_x1 = 0, reg_y1 = 0;  // sampling region + margin
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
@@ -342,7 +345,8 @@ static void free_all(clrrt_ctx* c) {
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
                   c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
                   c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
-                  c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed};
+                  c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
+                  c->goal_recs, c->bp_path};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -711,6 +715,55 @@ int clrrt_tree_rows(clrrt_ctx* c, int64_t row_offset, int64_t nrows, double* out
   HIPC(c, hipMemcpyAsync(out, c->arena + row_offset * 10, sizeof(double) * 10 * nrows, hipMemcpyDeviceToHost,
                          c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_extract_best_path(clrrt_ctx* c, int32_t* path, int32_t cap, int32_t* n_path, float* best_cost,
+                            int64_t* n_goal) {
+  if (!c || !n_path || cap < 0 || (cap > 0 && !path)) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  *n_path = 0;
+  if (best_cost) *best_cost = HUGE_VALF;
+  if (n_goal) *n_goal = 0;
+  const int64_t n = c->n_nodes;
+  if (n == 0) return CLRRT_OK;
+  if (!c->goal_recs) {
+    HIPC(c, hipMalloc(&c->goal_recs, sizeof(GoalRec) * c->cap.max_nodes));
+    HIPC(c, hipMalloc(&c->bp_path, sizeof(int) * (c->cap.max_nodes + 2)));
+  }
+  int* d_cnt = c->bp_path + c->cap.max_nodes;
+  HIPC(c, launch_goal_gather(c->stream, c->tree, n, c->goal_recs, d_cnt));
+  int cnt = 0;
+  HIPC(c, hipMemcpyAsync(&cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (n_goal) *n_goal = cnt;
+  if (cnt == 0) return CLRRT_OK;  // "No feasible path found" (rrtplanner.cpp:361-366)
+  std::vector<GoalRec> g(cnt);
+  HIPC(c, hipMemcpyAsync(g.data(), c->goal_recs, sizeof(GoalRec) * cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  // pair_vector in tree order (rrtplanner.cpp:330-335), then the reference's sort verbatim in
+  // semantics: std::sort on (id, double(costS)) pairs by .second -- equal costs keep whatever
+  // order introsort leaves them in, which depends on the input order, hence the id pass first.
+  std::sort(g.begin(), g.end(), [](const GoalRec& a, const GoalRec& b) { return a.id < b.id; });
+  std::vector<std::pair<int, double>> pv(cnt);
+  for (int i = 0; i < cnt; i++) pv[i] = std::make_pair((int)g[i].id, (double)g[i].cost);
+  std::sort(pv.begin(), pv.end(),
+            [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.second < b.second; });
+  const int best = pv.front().first;
+  if (best_cost) *best_cost = (float)pv.front().second;
+  HIPC(c, launch_backtrack(c->stream, c->tree, n, best, (int)c->cap.max_nodes, c->bp_path, d_cnt + 1));
+  int len = 0;
+  HIPC(c, hipMemcpyAsync(&len, d_cnt + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (len <= 0) return fail(c, CLRRT_EINVAL, "extract_best_path: parent chain does not reach the root");
+  const int m = std::min<int>(len, cap);
+  if (m > 0) {
+    std::vector<int> chain(len);  // goal -> root
+    HIPC(c, hipMemcpyAsync(chain.data(), c->bp_path, sizeof(int) * len, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < m; i++) path[i] = chain[len - 1 - i];
+  }
+  *n_path = len;
   return CLRRT_OK;
 }
 

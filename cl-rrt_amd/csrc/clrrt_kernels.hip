@@ -1154,6 +1154,41 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   nn[0] = r;
 }
 
+// Goal nodes of the tree (extractBestPath's pair_vector, rrtplanner.cpp:330-335) -- wave-aggregated
+// append; the host restores tree order by id before replaying the reference's sort.
+__global__ void __launch_bounds__(256) k_goal_gather(const clrrt_node* __restrict__ tree, int64_t n,
+                                                     GoalRec* __restrict__ out, int* __restrict__ cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - threadIdx.x < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool g = i < n && tree[i].goal != 0;
+    const unsigned long long m = __ballot(g);
+    if (m == 0) continue;
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(cnt, __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (g) {
+      const int off = __popcll(m & ((1ull << lane) - 1ull));
+      out[base + off] = GoalRec{(int32_t)i, tree[i].costS};
+    }
+  }
+}
+
+// Backtracking from the chosen goal node to the root (rrtplanner.cpp:339-346): parents precede
+// their children, so the chain ends at the root (parent -1) within n steps.
+__global__ void k_backtrack(const clrrt_node* __restrict__ tree, int64_t n, int start, int cap,
+                            int* __restrict__ path, int* __restrict__ len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int k = 0;
+  int64_t p = start;
+  while (p >= 0 && p < n && k <= n) {
+    if (k < cap) path[k] = (int)p;
+    k++;
+    p = tree[p].parent;
+  }
+  *len = (p == -1) ? k : -1;  // -1: a broken chain (parent outside the tree)
+}
+
 // Elementary functions as the kernels evaluate them (test hook: bit-compared with the host libm).
 __global__ void k_selftest_math(int fn, const double* __restrict__ a, const double* __restrict__ b, int n,
                                 double* __restrict__ out) {
@@ -1474,6 +1509,21 @@ hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const d
   hipLaunchKernelGGL(k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, st, fn, a, b, n, out);
   LAUNCH_CHECK();
   return hipSuccess;
+}
+
+hipError_t launch_goal_gather(hipStream_t st, const clrrt_node* tree, int64_t n, GoalRec* out, int* cnt) {
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int), st);
+  if (e != hipSuccess || n == 0) return e;
+  const int64_t want = (n + 255) / 256;
+  const int blocks = (int)std::min<int64_t>(want, 4096);
+  hipLaunchKernelGGL(k_goal_gather, dim3(blocks), dim3(256), 0, st, tree, n, out, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_backtrack(hipStream_t st, const clrrt_node* tree, int64_t n, int start, int cap, int* path,
+                            int* len) {
+  hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64), 0, st, tree, n, start, cap, path, len);
+  return hipGetLastError();
 }
 
 hipError_t launch_init_root(hipStream_t st, const double* state, clrrt_node* tree, NnRec* nn, double* arena) {

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 3
+#define CLRRT_ABI_VERSION 4
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -212,6 +212,15 @@ int clrrt_tree_load(clrrt_ctx* ctx, const clrrt_node* nodes, int64_t n);
 int clrrt_tree_size(clrrt_ctx* ctx, int64_t* n_nodes, int64_t* n_rows);
 int clrrt_tree_download(clrrt_ctx* ctx, int64_t first, int64_t count, clrrt_node* out);
 int clrrt_tree_rows(clrrt_ctx* ctx, int64_t row_offset, int64_t nrows, double* out);
+
+/* extractBestPath (rrtplanner.cpp:318-368; declared rrtplanner.h:92): among the nodes with
+ * goalReached set, in tree order, the front after the reference's std::sort by costS (ascending,
+ * same unstable introsort) and its ancestors.  Writes the node ids root -> goal into path[0 .. cap)
+ * and the full length into *n_path (0 when no node reached the goal -- the reference logs
+ * "No feasible path found" and returns an empty vector).  Optional outputs: *best_cost (costS of
+ * the chosen node, +inf when none) and *n_goal (goal nodes in the tree). */
+int clrrt_extract_best_path(clrrt_ctx* ctx, int32_t* path, int32_t cap, int32_t* n_path, float* best_cost,
+                            int64_t* n_goal);
 
 /* ---- expansion ---- */
 /* Runs expandTree iterations drawn from `rng` until `n_iters` iterations are consumed

@@ -49,6 +49,8 @@ __attribute__((noinline)) static void lm_sincosf(float x, float* s, float* c) { 
 __attribute__((noinline)) static float lm_sinf(float x) { return ::sinf(x); }
 
 using std::vector;
+using std::pair;
+using std::make_pair;
 typedef vector<double> Row;
 
 struct Pt { double x = 0, y = 0; };
@@ -830,3 +832,24 @@ int orc_eval_iteration(void* h, double sx, double sy, int explore, int stable, c
 }
 
 }  // extern "C"
+
+// extractBestPath rrtplanner.cpp:318-368: goal nodes as (id, costS) pairs in tree order, std::sort
+// ascending by cost (the reference's lambda; not stable), the front's ancestors by backtracking.
+// Writes the path root -> goal into ids (at most cap) and returns its length (0: no solution).
+extern "C" int orc_extract_best_path(void* h, int* ids, int cap) {
+  Oracle* o = (Oracle*)h;
+  vector<pair<int, double>> pv;
+  for (int nodeid = 0; nodeid != (int)o->tree.size(); nodeid++)
+    if (o->tree[nodeid].goalReached) pv.push_back(make_pair(nodeid, (double)o->tree[nodeid].costS));
+  if (pv.empty()) return 0;
+  sort(pv.begin(), pv.end(), [](const pair<int, double>& a, const pair<int, double>& b) { return a.second < b.second; });
+  vector<int> path{pv.front().first};
+  int parent = o->tree[pv.front().first].parentID;
+  while (parent != -1) {
+    path.insert(path.begin(), parent);
+    parent = o->tree[parent].parentID;
+  }
+  int n = (int)path.size();
+  for (int i = 0; i < n && i < cap; i++) ids[i] = path[i];
+  return n;
+}

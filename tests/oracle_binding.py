@@ -51,6 +51,7 @@ def lib():
             "orc_check_obs": (d, [vp, P(d)]),
             "orc_draw_samples": (None, [vp, i, P(d), P(i)]),
             "orc_eval_iteration": (i, [vp, d, d, i, i, P(abi.Node)]),
+            "orc_extract_best_path": (i, [vp, P(i), i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -188,6 +189,11 @@ class Oracle:
         ex = (C.c_int * n)()
         self.L.orc_draw_samples(self.h, n, _dp(xy), ex)
         return xy.reshape(n, 2), np.array(list(ex), dtype=np.int32)
+
+    def extract_best_path(self, cap=4096):
+        ids = (C.c_int * cap)()
+        n = self.L.orc_extract_best_path(self.h, ids, cap)
+        return list(ids[:min(n, cap)])
 
     def eval_iteration(self, sx, sy, explore, stable=False):
         out = (abi.Node * 2)()
