@@ -46,6 +46,12 @@ _SIGS = {
     "clrrt_tree_rows": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(C.c_double)]),
     "clrrt_extract_best_path": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int32), P(C.c_float),
                                           P(C.c_int64)]),
+    "clrrt_path_commit": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int32)]),
+    "clrrt_path_load": (C.c_int, [C.c_void_p, P(abi.Node), C.c_int32, P(C.c_double), C.c_int64]),
+    "clrrt_path_size": (C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int64)]),
+    "clrrt_path_download": (C.c_int, [C.c_void_p, P(abi.Node), P(C.c_double)]),
+    "clrrt_path_transform": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double)]),
+    "clrrt_tree_init_from_path": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
     "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
@@ -230,6 +236,45 @@ class Planner:
         self._chk(self.L.clrrt_extract_best_path(self.h, ids.ctypes.data_as(P(C.c_int32)), cap, C.byref(n),
                                                  C.byref(cost), C.byref(ng)), "extract_best_path")
         return [int(v) for v in ids[:min(n.value, cap)]], float(cost.value), int(ng.value)
+
+    # committed path (MotionPlanner::bestNodes) and initializeTree -- include/clrrt.h
+    def path_commit(self, ids):
+        arr = np.ascontiguousarray(ids, dtype=np.int32)
+        rem = C.c_int32()
+        self._chk(self.L.clrrt_path_commit(self.h, arr.ctypes.data_as(P(C.c_int32)), len(arr), C.byref(rem)),
+                  "path_commit")
+        return rem.value
+
+    def path_load(self, nodes_raw, rows):
+        rows = np.ascontiguousarray(rows, dtype=np.float64).reshape(-1, 10)
+        self._chk(self.L.clrrt_path_load(self.h, nodes_raw, len(nodes_raw), rows.ctypes.data_as(P(C.c_double)),
+                                         len(rows)), "path_load")
+
+    def path_size(self):
+        n, r = C.c_int32(), C.c_int64()
+        self._chk(self.L.clrrt_path_size(self.h, C.byref(n), C.byref(r)), "path_size")
+        return n.value, r.value
+
+    def path_download(self):
+        """(headers as abi.Node array, rows (R, 10)) of the committed path."""
+        n, r = self.path_size()
+        nodes = (abi.Node * max(1, n))()
+        rows = np.zeros((max(1, r), 10))
+        self._chk(self.L.clrrt_path_download(self.h, nodes, rows.ctypes.data_as(P(C.c_double))), "path_download")
+        return (nodes if n else (abi.Node * 0)()), rows[:r]
+
+    def path_transform(self, to_world, pose):
+        pose = np.ascontiguousarray(pose[:3], dtype=np.float64)
+        d = abi.CLRRT_CAR_TO_WORLD if to_world else abi.CLRRT_WORLD_TO_CAR
+        self._chk(self.L.clrrt_path_transform(self.h, d, pose.ctypes.data_as(P(C.c_double))), "path_transform")
+
+    def tree_init_from_path(self, car_state):
+        cs = np.zeros(6)
+        cs[:min(6, len(car_state))] = np.asarray(car_state, dtype=np.float64)[:6]
+        oc = C.c_int32()
+        self._chk(self.L.clrrt_tree_init_from_path(self.h, cs.ctypes.data_as(P(C.c_double)), C.byref(oc)),
+                  "tree_init_from_path")
+        return oc.value
 
     def expand(self, rng, n_iters=0, budget_ms=0.0, mode=CLRRT_MODE_EXACT, batch=0):
         st = abi.Stats()

@@ -5,7 +5,7 @@ header documents so a drift between the two fails at import time.
 """
 import ctypes as C
 
-CLRRT_ABI_VERSION = 4  # include/clrrt.h
+CLRRT_ABI_VERSION = 5  # include/clrrt.h
 CLRRT_MODE_EXACT = 0
 CLRRT_PARENT_PREV = -2  # goal-biased record: parent = the record before it (include/clrrt.h)
 CLRRT_MODE_BATCH = 1
@@ -15,6 +15,8 @@ CLRRT_COLLISION_OBB = 1
 ROLL_ITERLIMIT, ROLL_END, ROLL_GOAL, ROLL_COLLISION, ROLL_ACCLIMIT = range(5)
 ROLL_NAMES = {ROLL_ITERLIMIT: "iterlimit", ROLL_END: "end", ROLL_GOAL: "goal",
               ROLL_COLLISION: "collision", ROLL_ACCLIMIT: "acclimit"}
+REINIT_EMPTY, REINIT_ALL_ERASED, REINIT_COLLISION, REINIT_KEPT = range(4)  # CLRRT_REINIT_*
+CLRRT_WORLD_TO_CAR, CLRRT_CAR_TO_WORLD = 0, 1
 
 
 class Vehicle(C.Structure):

@@ -104,6 +104,17 @@ struct clrrt_ctx {
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
   GoalRec* goal_recs = nullptr;
   int* bp_path = nullptr;  // [max_nodes + 2]: chain, then count and length
+  // committed path (MotionPlanner::bestNodes) + initializeTree scratch
+  clrrt_node* path_nodes = nullptr;
+  double* path_rows = nullptr;
+  int path_cap = 0;
+  int64_t path_rows_cap = 0;
+  int path_n = 0;
+  int64_t path_nrows = 0;
+  int* ri_int = nullptr;       // [2 * path_cap + ...] ids, kept index, goal flags
+  int64_t* ri_off = nullptr;   // [path_cap] new row offsets, then [3] outcome / nodes / rows
+  float* ri_cost = nullptr;    // [path_cap]
+  double* ri_terms = nullptr;  // [2 * path_rows_cap]
   double reg_x0 = 0, reg_y0 = 0, reg_x1 = 0, reg_y1 = 0;  // sampling region + margin
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
@@ -346,7 +357,8 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
                   c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
-                  c->goal_recs, c->bp_path};
+                  c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
+                  c->ri_terms};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -764,6 +776,168 @@ int clrrt_extract_best_path(clrrt_ctx* c, int32_t* path, int32_t cap, int32_t* n
     for (int i = 0; i < m; i++) path[i] = chain[len - 1 - i];
   }
   *n_path = len;
+  return CLRRT_OK;
+}
+
+// ------------------------------------------------------------------ committed path / re-init
+// Grow the path buffers to hold n nodes and nrows rows (contents not preserved).
+static int path_reserve(clrrt_ctx* c, int n, int64_t nrows) {
+  if (n > c->path_cap) {
+    const int cap = std::max(n, 2 * c->path_cap);
+    for (void* p : {(void*)c->path_nodes, (void*)c->ri_int, (void*)c->ri_off, (void*)c->ri_cost})
+      if (p) hipFree(p);
+    c->path_nodes = nullptr; c->ri_int = nullptr; c->ri_off = nullptr; c->ri_cost = nullptr;
+    c->path_cap = 0;
+    HIPC(c, hipMalloc((void**)&c->path_nodes, sizeof(clrrt_node) * cap));
+    HIPC(c, hipMalloc((void**)&c->ri_int, sizeof(int) * (3 * (size_t)cap)));
+    HIPC(c, hipMalloc((void**)&c->ri_off, sizeof(int64_t) * ((size_t)cap + 3)));
+    HIPC(c, hipMalloc((void**)&c->ri_cost, sizeof(float) * cap));
+    c->path_cap = cap;
+  }
+  if (nrows > c->path_rows_cap) {
+    const int64_t cap = std::max<int64_t>(nrows, 2 * c->path_rows_cap);
+    if (c->path_rows) hipFree(c->path_rows);
+    if (c->ri_terms) hipFree(c->ri_terms);
+    c->path_rows = nullptr; c->ri_terms = nullptr;
+    c->path_rows_cap = 0;
+    HIPC(c, hipMalloc((void**)&c->path_rows, sizeof(double) * 10 * cap));
+    HIPC(c, hipMalloc((void**)&c->ri_terms, sizeof(double) * 2 * cap));
+    c->path_rows_cap = cap;
+  }
+  return CLRRT_OK;
+}
+
+int clrrt_path_commit(clrrt_ctx* c, const int32_t* ids, int32_t n, int32_t* n_remote) {
+  if (!c || n < 0 || (n > 0 && !ids)) return CLRRT_EINVAL;
+  for (int i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= c->n_nodes) return fail(c, CLRRT_EINVAL, "path_commit: node id outside the tree");
+  HIPC(c, hipSetDevice(c->device));
+  if (n_remote) *n_remote = 0;
+  c->path_n = 0;
+  c->path_nrows = 0;
+  if (n == 0) return CLRRT_OK;
+  int rc = path_reserve(c, n, 1);
+  if (rc != CLRRT_OK) return rc;
+  // headers of the path nodes, then path-local row offsets on the host
+  HIPC(c, hipMemcpyAsync(c->ri_int, ids, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_gather_nodes(c->stream, c->tree, c->ri_int, n, c->path_nodes));
+  std::vector<clrrt_node> h(n);
+  HIPC(c, hipMemcpyAsync(h.data(), c->path_nodes, sizeof(clrrt_node) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  std::vector<int64_t> src(n);
+  int64_t rows = 0;
+  int remote = 0;
+  for (int i = 0; i < n; i++) {
+    if (h[i].nrows < 1) return fail(c, CLRRT_EINVAL, "path_commit: node without trajectory rows");
+    src[i] = h[i].row_offset;
+    h[i].row_offset = rows;
+    rows += h[i].nrows;
+    if (h[i].owner != c->rank) remote++;
+  }
+  rc = path_reserve(c, n, rows);
+  if (rc != CLRRT_OK) return rc;
+  HIPC(c, hipMemcpyAsync(c->path_nodes, h.data(), sizeof(clrrt_node) * n, hipMemcpyHostToDevice, c->stream));
+  for (int i = 0; i < n; i++) {
+    double* dst = c->path_rows + h[i].row_offset * 10;
+    const size_t bytes = sizeof(double) * 10 * h[i].nrows;
+    if (h[i].owner == c->rank) {
+      HIPC(c, hipMemcpyAsync(dst, c->arena + src[i] * 10, bytes, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      HIPC(c, hipMemsetAsync(dst, 0, bytes, c->stream));
+    }
+  }
+  HIPC(c, hipStreamSynchronize(c->stream));
+  c->path_n = n;
+  c->path_nrows = rows;
+  if (n_remote) *n_remote = remote;
+  return CLRRT_OK;
+}
+
+int clrrt_path_load(clrrt_ctx* c, const clrrt_node* nodes, int32_t n, const double* rows, int64_t n_rows) {
+  if (!c || n < 0 || n_rows < 0 || (n > 0 && (!nodes || !rows))) return CLRRT_EINVAL;
+  for (int i = 0; i < n; i++)
+    if (nodes[i].nrows < 1 || nodes[i].row_offset < 0 || nodes[i].row_offset + nodes[i].nrows > n_rows)
+      return fail(c, CLRRT_EINVAL, "path_load: node rows outside the row buffer");
+  HIPC(c, hipSetDevice(c->device));
+  int rc = path_reserve(c, n, n_rows);
+  if (rc != CLRRT_OK) return rc;
+  if (n > 0) {
+    HIPC(c, hipMemcpyAsync(c->path_nodes, nodes, sizeof(clrrt_node) * n, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->path_rows, rows, sizeof(double) * 10 * n_rows, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+  }
+  c->path_n = n;
+  c->path_nrows = n > 0 ? n_rows : 0;
+  return CLRRT_OK;
+}
+
+int clrrt_path_size(clrrt_ctx* c, int32_t* n, int64_t* n_rows) {
+  if (!c) return CLRRT_EINVAL;
+  if (n) *n = c->path_n;
+  if (n_rows) *n_rows = c->path_nrows;
+  return CLRRT_OK;
+}
+
+int clrrt_path_download(clrrt_ctx* c, clrrt_node* nodes, double* rows) {
+  if (!c) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (c->path_n > 0 && nodes)
+    HIPC(c, hipMemcpyAsync(nodes, c->path_nodes, sizeof(clrrt_node) * c->path_n, hipMemcpyDeviceToHost, c->stream));
+  if (c->path_nrows > 0 && rows)
+    HIPC(c, hipMemcpyAsync(rows, c->path_rows, sizeof(double) * 10 * c->path_nrows, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_path_transform(clrrt_ctx* c, int32_t dir, const double pose[3]) {
+  if (!c || !pose || (dir != CLRRT_WORLD_TO_CAR && dir != CLRRT_CAR_TO_WORLD)) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (c->path_n == 0) return CLRRT_OK;
+  HIPC(c, launch_path_transform(c->stream, c->path_nodes, c->path_n, c->path_rows, c->path_nrows,
+                                dir == CLRRT_CAR_TO_WORLD, pose));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_tree_init_from_path(clrrt_ctx* c, const double car_state[6], int32_t* outcome) {
+  if (!c || !car_state) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  int rc = path_reserve(c, std::max(1, c->path_n), std::max<int64_t>(1, c->path_nrows));
+  if (rc != CLRRT_OK) return rc;
+  if (c->path_n > c->cap.max_nodes || c->path_nrows > c->cap.max_rows)
+    return fail(c, CLRRT_ECAPACITY, "tree_init_from_path: committed path exceeds the tree capacity");
+  ReinitArgs a;
+  a.p = c->dp;
+  a.obs = c->obs;
+  a.pn = c->path_nodes;
+  a.n = c->path_n;
+  a.prow = c->path_rows;
+  for (int k = 0; k < 10; k++) a.car[k] = k < 6 ? car_state[k] : 0.0;
+  a.tree = c->tree;
+  a.nn = c->nn;
+  a.arena = c->arena;
+  a.kidx = c->ri_int;
+  a.koff = c->ri_off;
+  a.terms = c->ri_terms;
+  a.costs = c->ri_cost;
+  a.out = c->ri_off + c->path_cap;
+  a.rank = c->rank;
+  a.max_nodes = c->cap.max_nodes;
+  a.max_rows = c->cap.max_rows;
+  HIPC(c, launch_tree_reinit(c->stream, a));
+  int64_t out[3];
+  HIPC(c, hipMemcpyAsync(out, a.out, sizeof(out), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (out[0] < 0) return fail(c, CLRRT_ECAPACITY, "tree_init_from_path: tree capacity");
+  c->n_nodes = out[1];
+  c->n_rows = out[2];
+  bbox_reset(c);
+  HIPC(c, launch_bbox(c->stream, c->tree, nullptr, (int)c->n_nodes, c->d_bbox));
+  HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+  if (outcome) *outcome = (int32_t)out[0];
   return CLRRT_OK;
 }
 

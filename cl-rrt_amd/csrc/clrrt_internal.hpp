@@ -176,6 +176,29 @@ struct GoalRec { int32_t id; float cost; };
 hipError_t launch_goal_gather(hipStream_t st, const clrrt_node* tree, int64_t n, GoalRec* out, int* cnt);
 hipError_t launch_backtrack(hipStream_t st, const clrrt_node* tree, int64_t n, int start, int cap, int* path,
                             int* len);
+// initializeTree (rrtplanner.cpp:39-95) from the committed path pn[0 .. n) / prow (path-local rows).
+struct ReinitArgs {
+  DevParams p;
+  const BakedObs* obs;
+  const clrrt_node* pn;
+  int n;
+  const double* prow;
+  double car[10];      // carState with the four appended zeros
+  clrrt_node* tree;
+  NnRec* nn;
+  double* arena;
+  int* kidx;           // [n] kept path index per new node; then [n] goal flag
+  int64_t* koff;       // [n] new row offset per kept node
+  double* terms;       // [2 * path rows] per-row cost term and lane term
+  float* costs;        // [n]
+  int64_t* out;        // [3] outcome, nodes, rows
+  int rank;
+  int64_t max_nodes, max_rows;
+};
+hipError_t launch_gather_nodes(hipStream_t st, const clrrt_node* tree, const int* ids, int n, clrrt_node* out);
+hipError_t launch_path_transform(hipStream_t st, clrrt_node* nodes, int n, double* rows, int64_t nrows, int to_world,
+                                 const double pose[3]);
+hipError_t launch_tree_reinit(hipStream_t st, const ReinitArgs& a);
 hipError_t launch_init_root(hipStream_t st, const double* state, clrrt_node* tree, NnRec* nn, double* arena);
 
 }  // namespace clrrt

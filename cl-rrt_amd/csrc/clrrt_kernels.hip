@@ -1126,9 +1126,22 @@ __global__ void k_append(const clrrt_node* __restrict__ in, int n, int64_t base,
   nn[base + i] = r;
 }
 
+// Nearest-node mirror record of tree node `id`.
+__device__ __forceinline__ NnRec nn_record(const clrrt_node& d, int64_t id) {
+  NnRec r;
+  r.x = d.state[0]; r.y = d.state[1];
+  r.bx = d.ref_back[0]; r.by = d.ref_back[1];
+  r.ang_par = d.ang_par;
+  float ang = (float)(-d.state[2] - 0.0);
+  r.c = cosf(ang); r.s = sinf(ang);
+  r.costE = d.costE;
+  r.id = (int32_t)id;
+  r.ca = cosf((float)d.ang_par); r.sa = sinf((float)d.ang_par);
+  return r;
+}
+
 // addInitialNode rrtplanner.cpp:21-37: reference = linspace(0, 1, floor(1/0.1)) at v = state[4].
-__global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnRec* nn, double* arena) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void init_root(const double* st, clrrt_node* tree, NnRec* nn, double* arena, int owner) {
   const int N = (int)floor(sqrt(1.0 * 1.0 + 0.0 * 0.0) / 0.1);
   double h = (1.0 - 0.0) / (double)(uint64_t)(N - 1);
   double x = 0.0;
@@ -1143,15 +1156,15 @@ __global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnR
   n.costE = 0.f; n.costS = 0.f;
   n.goal = 0;
   n.nrows = 1;
-  n.owner = 0;
+  n.owner = owner;
   n.row_offset = 0;
   tree[0] = n;
-  NnRec r;
-  r.x = n.state[0]; r.y = n.state[1]; r.bx = x; r.by = 0.0; r.ang_par = n.ang_par;
-  float ang = (float)(-n.state[2] - 0.0);
-  r.c = cosf(ang); r.s = sinf(ang); r.costE = 0.f; r.id = 0;
-  r.ca = cosf((float)n.ang_par); r.sa = sinf((float)n.ang_par);
-  nn[0] = r;
+  nn[0] = nn_record(n, 0);
+}
+
+__global__ void k_init_root(const double* __restrict__ st, clrrt_node* tree, NnRec* nn, double* arena) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  init_root(st, tree, nn, arena, 0);
 }
 
 // Goal nodes of the tree (extractBestPath's pair_vector, rrtplanner.cpp:330-335) -- wave-aggregated
@@ -1187,6 +1200,174 @@ __global__ void k_backtrack(const clrrt_node* __restrict__ tree, int64_t n, int 
     p = tree[p].parent;
   }
   *len = (p == -1) ? k : -1;  // -1: a broken chain (parent outside the tree)
+}
+
+// ----------------------------------------------------------------- committed path / re-init
+__global__ void k_gather_nodes(const clrrt_node* __restrict__ tree, const int* __restrict__ ids, int n,
+                               clrrt_node* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = tree[ids[i]];
+}
+
+// transformPointWorldToCar / CarToWorld (transformations.cpp:6-17); sin and cos of one argument
+// in one function: the generic sincos, as the oracle's restatement.
+__device__ __forceinline__ void point_world_to_car(double& Xw, double& Yw, double P0, double P1, double s,
+                                                   double c) {
+  double Xc = Xw * c - P0 * c - P1 * s + Yw * s;
+  double Yc = Yw * c - P1 * c + P0 * s - Xw * s;
+  Xw = Xc; Yw = Yc;
+}
+__device__ __forceinline__ void point_car_to_world(double& Xc, double& Yc, double P0, double P1, double s,
+                                                   double c) {
+  double Xw = c * Xc - s * Yc + P0;
+  double Yw = s * Xc + c * Yc + P1;
+  Xc = Xw; Yc = Yw;
+}
+
+// transformNodesWorldToCar / CarToworld (transformations.cpp:289-315): node state (x, y, heading),
+// the reference end points (the only reference points the engine keeps; the reference transforms
+// each point independently, so front/back come out the same), and (x, y) of every row.
+__global__ void __launch_bounds__(256) k_path_transform(clrrt_node* __restrict__ nodes, int n,
+                                                        double* __restrict__ rows, int64_t nrows, int to_world,
+                                                        double P0, double P1, double P2) {
+  glibc::stage_tables();
+  double s, c;
+  glibc::sincos(P2, s, c);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    clrrt_node& d = nodes[i];
+    if (to_world) {
+      point_car_to_world(d.state[0], d.state[1], P0, P1, s, c);
+      d.state[2] += P2;
+      point_car_to_world(d.ref_front[0], d.ref_front[1], P0, P1, s, c);
+      point_car_to_world(d.ref_back[0], d.ref_back[1], P0, P1, s, c);
+    } else {
+      point_world_to_car(d.state[0], d.state[1], P0, P1, s, c);
+      d.state[2] -= P2;
+      point_world_to_car(d.ref_front[0], d.ref_front[1], P0, P1, s, c);
+      point_world_to_car(d.ref_back[0], d.ref_back[1], P0, P1, s, c);
+    }
+    d.ang_par = atan2(d.ref_back[1] - d.ref_front[1], d.ref_back[0] - d.ref_front[0]);
+  } else if (i - n < nrows) {
+    double* r = rows + (i - n) * 10;
+    if (to_world) point_car_to_world(r[0], r[1], P0, P1, s, c);
+    else point_world_to_car(r[0], r[1], P0, P1, s, c);
+  }
+}
+
+// initializeTree rrtplanner.cpp:39-95 + getNodeCost :104-119, one workgroup (a committed path is
+// a few nodes / a few thousand rows: latency, not throughput).  Row checks run across the block;
+// the cost recurrence (costS float, read back as the next node's double parent cost) on lane 0.
+__global__ void __launch_bounds__(256) k_tree_reinit(ReinitArgs a) {
+  glibc::stage_tables();
+  __shared__ int s_kept, s_coll;
+  __shared__ long long s_rows;
+  const int tid = threadIdx.x;
+  const DevParams& p = a.p;
+  const ObsView ov{a.obs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                   p.coll_mode == CLRRT_COLLISION_OBB ? p.n_obs : 0, 0, 0, 0, 0.f, 0.f, 0.f};
+  int* goal = a.kidx + a.n;
+  // :51-57 erase(it--) over the path = keep the nodes whose last row has x >= 0 (or NaN)
+  if (tid == 0) {
+    int k = 0;
+    long long r = 0;
+    for (int i = 0; i < a.n; i++) {
+      const clrrt_node& h = a.pn[i];
+      const double xb = a.prow[(h.row_offset + h.nrows - 1) * 10];
+      if (!(xb < 0)) {
+        a.kidx[k] = i;
+        a.koff[k] = r;
+        goal[k] = 0;
+        r += h.nrows;
+        k++;
+      }
+    }
+    s_kept = k;
+    s_rows = r;
+    s_coll = 0;
+  }
+  __syncthreads();
+  const int kept = s_kept;
+  const int64_t rows = s_rows;
+  if (a.n == 0 || kept == 0) {
+    if (tid == 0) {
+      init_root(a.car, a.tree, a.nn, a.arena, a.rank);
+      a.out[0] = a.n == 0 ? CLRRT_REINIT_EMPTY : CLRRT_REINIT_ALL_ERASED;
+      a.out[1] = 1; a.out[2] = 1;
+    }
+    return;
+  }
+  // :60-69 goal flags, :72-81 collisions, getNodeCost's per-row terms
+  for (int k = 0; k < kept; k++) {
+    const clrrt_node& h = a.pn[a.kidx[k]];
+    for (int i = tid; i < h.nrows; i += blockDim.x) {
+      const double* x = a.prow + (h.row_offset + i) * 10;
+      const double ex = x[0] - p.g0;
+      const double Dgoal = sqrt(ex * ex + x[1] * x[1]);
+      const double Hgoal = fabs(x[2] - p.g2);
+      const double dVgoal = fabs(x[4] - p.g3);
+      if ((Dgoal <= 1) && (Hgoal <= 0.05) && (dVgoal <= 0.1)) goal[k] = 1;
+      Roll r;
+      r.x0 = x[0]; r.x1 = x[1]; r.x2 = x[2]; r.x6 = x[6];
+      glibc::sincos(r.x2, r.s2, r.c2);
+      uint32_t tests = 0;
+      const double Dobs = obs_distance<true>(r, p, ov, tests);
+      if (Dobs == 0) s_coll = 1;
+      const double kappa = glibc::tan(x[3]) / p.L;
+      double term = p.W0 * x[4] * p.dt + p.W1 * fabs(kappa);
+      if (p.use_exp) term = term + p.W2 * exp(-p.W3 * Dobs);
+      double* t = a.terms + (a.koff[k] + i) * 2;
+      t[0] = term;
+      t[1] = p.bend ? p.W4 * dist_to_lane(x[0], x[1], p.lane_shift0, p.Cxy1, p.Cxy2) : 0.0;
+    }
+  }
+  __syncthreads();
+  if (s_coll) {
+    if (tid == 0) {
+      init_root(a.car, a.tree, a.nn, a.arena, a.rank);
+      a.out[0] = CLRRT_REINIT_COLLISION;
+      a.out[1] = 1; a.out[2] = 1;
+    }
+    return;
+  }
+  if (kept > a.max_nodes || rows > a.max_rows) {  // the host checks the path's totals; kept fits
+    if (tid == 0) { a.out[0] = -1; a.out[1] = kept; a.out[2] = rows; }
+    return;
+  }
+  // :84-87 cost recurrence
+  if (tid == 0) {
+    double parent = 0;
+    for (int k = 0; k < kept; k++) {
+      const clrrt_node& h = a.pn[a.kidx[k]];
+      double cost = parent;
+      const double* t = a.terms + a.koff[k] * 2;
+      for (int i = 0; i < h.nrows; i++) {
+        cost += t[2 * i];
+        if (p.bend) cost += t[2 * i + 1];
+      }
+      a.costs[k] = (float)cost;
+      parent = (double)a.costs[k];
+    }
+  }
+  __syncthreads();
+  // :90-93 the chain, rows into the arena
+  for (int k = tid; k < kept; k += blockDim.x) {
+    clrrt_node h = a.pn[a.kidx[k]];
+    h.parent = k - 1;
+    h.goal = goal[k];
+    h.costS = a.costs[k];
+    h.row_offset = a.koff[k];
+    h.owner = a.rank;
+    a.tree[k] = h;
+    a.nn[k] = nn_record(h, k);
+  }
+  for (int k = 0; k < kept; k++) {
+    const clrrt_node& h = a.pn[a.kidx[k]];
+    const double* src = a.prow + h.row_offset * 10;
+    double* dst = a.arena + a.koff[k] * 10;
+    for (int e = tid; e < h.nrows * 10; e += blockDim.x) dst[e] = src[e];
+  }
+  if (tid == 0) { a.out[0] = CLRRT_REINIT_KEPT; a.out[1] = kept; a.out[2] = rows; }
 }
 
 // Elementary functions as the kernels evaluate them (test hook: bit-compared with the host libm).
@@ -1523,6 +1704,26 @@ hipError_t launch_goal_gather(hipStream_t st, const clrrt_node* tree, int64_t n,
 hipError_t launch_backtrack(hipStream_t st, const clrrt_node* tree, int64_t n, int start, int cap, int* path,
                             int* len) {
   hipLaunchKernelGGL(k_backtrack, dim3(1), dim3(64), 0, st, tree, n, start, cap, path, len);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_nodes(hipStream_t st, const clrrt_node* tree, const int* ids, int n, clrrt_node* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_nodes, dim3((n + 255) / 256), dim3(256), 0, st, tree, ids, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_path_transform(hipStream_t st, clrrt_node* nodes, int n, double* rows, int64_t nrows, int to_world,
+                                 const double pose[3]) {
+  const int64_t total = (int64_t)n + nrows;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_path_transform, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, nodes, n, rows,
+                     nrows, to_world, pose[0], pose[1], pose[2]);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_reinit(hipStream_t st, const ReinitArgs& a) {
+  hipLaunchKernelGGL(k_tree_reinit, dim3(1), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 4
+#define CLRRT_ABI_VERSION 5
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -67,6 +67,17 @@ extern "C" {
 #define CLRRT_ROLL_GOAL 2      /* goalReached (simulation.cpp:125-132) */
 #define CLRRT_ROLL_COLLISION 3 /* fail_collision (simulation.cpp:84-86) */
 #define CLRRT_ROLL_ACCLIMIT 4  /* fail_acclimit (simulation.cpp:100-104) */
+
+/* ---- initializeTree outcomes (rrtplanner.cpp:39-95) ---- */
+#define CLRRT_REINIT_EMPTY 0      /* no committed nodes: addInitialNode(carState) (:43-48) */
+#define CLRRT_REINIT_ALL_ERASED 1 /* every node behind the car; the reference reads nodes.front() of an
+                                     empty vector (:90, undefined): taken as an empty tree */
+#define CLRRT_REINIT_COLLISION 2  /* a committed row collides: empty tree (goto makeEmptyTree, :72-81) */
+#define CLRRT_REINIT_KEPT 3       /* surviving nodes chained (parent i-1), goal flags and costS redone */
+
+/* transformNodes* directions (transformations.cpp:289-315) */
+#define CLRRT_WORLD_TO_CAR 0
+#define CLRRT_CAR_TO_WORLD 1
 
 /* Vehicle parameters (class Vehicle, rrt/include/rrt/vehicle.h:4-60).  Only the fields the
  * hot path reads are carried. */
@@ -221,6 +232,34 @@ int clrrt_tree_rows(clrrt_ctx* ctx, int64_t row_offset, int64_t nrows, double* o
  * the chosen node, +inf when none) and *n_goal (goal nodes in the tree). */
 int clrrt_extract_best_path(clrrt_ctx* ctx, int32_t* path, int32_t cap, int32_t* n_path, float* best_cost,
                             int64_t* n_goal);
+
+/* ---- committed path (MotionPlanner::bestNodes, motionplanner.h:23) and tree re-initialisation ----
+ * The path is held on the device: node headers (row_offset local to the path's own row buffer) and
+ * their trajectories.  A planMotion query with commit_path = 1 (motionplanner.cpp:22-32, 50-54) is
+ *   clrrt_path_transform(ctx, CLRRT_WORLD_TO_CAR, worldState)      transformNodesWorldToCar (:22)
+ *   clrrt_set_params / clrrt_set_obstacles for the query
+ *   clrrt_tree_init_from_path(ctx, carPose, &outcome)               initializeTree (:32)
+ *   clrrt_expand(...)                                                the Timer(200) loop (:39-43)
+ *   clrrt_extract_best_path + clrrt_path_commit                     bestNodes = extractBestPath (:51)
+ *   clrrt_path_transform(ctx, CLRRT_CAR_TO_WORLD, worldState)      transformNodesCarToworld (:54)  */
+/* bestNodes = the tree nodes ids[0 .. n) (headers and trajectories copied; rows of nodes owned by
+ * another rank are zero-filled and counted in *n_remote -- fetch them from the owner and
+ * clrrt_path_load the result). */
+int clrrt_path_commit(clrrt_ctx* ctx, const int32_t* ids, int32_t n, int32_t* n_remote);
+/* Replace the committed path with host data: n headers whose row_offset/nrows index `rows`
+ * (n_rows rows of 10 doubles); every node needs nrows >= 1. */
+int clrrt_path_load(clrrt_ctx* ctx, const clrrt_node* nodes, int32_t n, const double* rows, int64_t n_rows);
+int clrrt_path_size(clrrt_ctx* ctx, int32_t* n, int64_t* n_rows);
+int clrrt_path_download(clrrt_ctx* ctx, clrrt_node* nodes, double* rows);
+/* transformNodesWorldToCar (dir CLRRT_WORLD_TO_CAR) / transformNodesCarToworld (CLRRT_CAR_TO_WORLD)
+ * (transformations.cpp:289-315) of the committed path; pose = carState[0..2] (x, y, heading). */
+int clrrt_path_transform(clrrt_ctx* ctx, int32_t dir, const double pose[3]);
+/* initializeTree(RRT, veh, bestNodes, carState) (rrtplanner.cpp:39-95; getNodeCost :104-119) with
+ * carState = 6 doubles (x, y, heading, delta, v, a; four zeros are appended as in :41): replaces the
+ * tree with the re-initialised one and reports CLRRT_REINIT_* in *outcome.  Collision checks and
+ * the obstacle cost term evaluate each trajectory row (the commented-out call at :74/:108) under
+ * the context's collision mode and obstacles. */
+int clrrt_tree_init_from_path(clrrt_ctx* ctx, const double car_state[6], int32_t* outcome);
 
 /* ---- expansion ---- */
 /* Runs expandTree iterations drawn from `rng` until `n_iters` iterations are consumed

@@ -84,6 +84,7 @@ struct Oracle {
   int64_t sim_count = 0, fail_collision = 0, fail_acclimit = 0, fail_iterlimit = 0, rollouts = 0;
   vector<Obs> det;
   vector<Node> tree;
+  vector<Node> best;  // MotionPlanner::bestNodes (motionplanner.h:23): the committed path
 };
 
 // ---------------------------------------------------------------- helpers (functions.h)
@@ -595,6 +596,93 @@ static void add_initial_node(Oracle& o, const vector<double>& state) {
   o.tree.push_back(n);
 }
 
+// ---------------------------------------------------------------- tree re-initialisation
+// transformPointWorldToCar / CarToWorld transformations.cpp:6-17 (sin and cos of one argument in
+// one function: a single sincos call, as for transformToVehicle).
+static void point_world_to_car(double& Xw, double& Yw, const double* P) {
+  double s, c;
+  lm_sincos(P[2], &s, &c);
+  double Xc = Xw * c - P[0] * c - P[1] * s + Yw * s;
+  double Yc = Yw * c - P[1] * c + P[0] * s - Xw * s;
+  Xw = Xc; Yw = Yc;
+}
+static void point_car_to_world(double& Xc, double& Yc, const double* P) {
+  double s, c;
+  lm_sincos(P[2], &s, &c);
+  double Xw = c * Xc - s * Yc + P[0];
+  double Yw = s * Xc + c * Yc + P[1];
+  Xc = Xw; Yc = Yw;
+}
+
+// transformNodesWorldToCar / CarToworld transformations.cpp:289-315: node state (x, y, heading),
+// every reference point, and the (x, y) of every trajectory row (row headings are left alone).
+static void transform_nodes(vector<Node>& nodes, int to_world, const double* P) {
+  for (auto& n : nodes) {
+    if (to_world) { point_car_to_world(n.state[0], n.state[1], P); n.state[2] += P[2]; }
+    else { point_world_to_car(n.state[0], n.state[1], P); n.state[2] -= P[2]; }
+    for (size_t i = 0; i != n.ref.x.size(); i++)
+      to_world ? point_car_to_world(n.ref.x[i], n.ref.y[i], P) : point_world_to_car(n.ref.x[i], n.ref.y[i], P);
+    for (size_t j = 0; j != n.tra.size(); j++)
+      to_world ? point_car_to_world(n.tra[j][0], n.tra[j][1], P) : point_world_to_car(n.tra[j][0], n.tra[j][1], P);
+  }
+}
+
+// getNodeCost rrtplanner.cpp:104-119 (checkObsDistance of the row, the commented-out form at :108,
+// under the context's collision mode; d2L :97-101 is getDistToLane's formula).
+static double node_cost(Oracle& o, const double& parentCost, const Node& node) {
+  double cost = parentCost;
+  for (auto it = node.tra.begin(); it != node.tra.end(); it++) {
+    double Dobs = obs_distance(o, *it);
+    double kappa = lm_tan((*it)[3]) / o.p.veh.L;
+    cost += o.p.Wcost[0] * (*it)[4] * o.p.sim_dt + o.p.Wcost[1] * std::abs(kappa) +
+            o.p.Wcost[2] * exp(-o.p.Wcost[3] * Dobs);
+    if (o.p.bend) cost += o.p.Wcost[4] * dist_to_lane((*it)[0], (*it)[1], o.p.lane_shift0, o.p.Cxy);
+  }
+  return cost;
+}
+
+// initializeTree rrtplanner.cpp:39-95 into a fresh tree (MyRRT is constructed per query,
+// motionplanner.cpp:23).  Returns CLRRT_REINIT_*:
+//   EMPTY      no committed nodes -> addInitialNode(carState)                          (:43-48)
+//   ALL_ERASED every node erased (x of its last row < 0); the reference then reads
+//              nodes.front() of an empty vector (:90, undefined) -- taken as an empty tree
+//   COLLISION  a committed row collides -> empty tree (goto makeEmptyTree, :72-81)
+//   KEPT       the surviving nodes as a chain (parent i-1), goal flags and costS recomputed
+static int initialize_tree(Oracle& o, vector<Node>& nodes, vector<double> carState) {
+  carState.push_back(0); carState.push_back(0); carState.push_back(0); carState.push_back(0);
+  o.tree.clear();
+  if (nodes.size() == 0) { add_initial_node(o, carState); return CLRRT_REINIT_EMPTY; }
+  // :51-57 -- erase(it--) revisits the element moved into the erased slot, i.e. a filter
+  vector<Node> kept;
+  for (auto& n : nodes) {
+    n.goalReached = 0;
+    if (!((n.tra.back()[0]) < 0)) kept.push_back(n);
+  }
+  nodes.swap(kept);
+  if (nodes.size() == 0) { add_initial_node(o, carState); return CLRRT_REINIT_ALL_ERASED; }
+  // :60-69 (Dgoal uses the row's y, not y - goal y)
+  for (auto& n : nodes)
+    for (size_t i = 0; i != n.tra.size(); i++) {
+      double Dgoal = sqrt(pow(n.tra[i][0] - o.p.goal[0], 2) + pow(n.tra[i][1], 2));
+      double Hgoal = std::abs(n.tra[i][2] - o.p.goal[2]);
+      double dVgoal = std::abs(n.tra[i][4] - o.p.goal[3]);
+      if ((Dgoal <= 1) && (Hgoal <= 0.05) && (dVgoal <= 0.1)) n.goalReached = 1;
+    }
+  // :72-81
+  for (auto& n : nodes)
+    for (size_t i = 0; i != n.tra.size(); i++)
+      if (obs_distance(o, n.tra[i]) == 0) { add_initial_node(o, carState); return CLRRT_REINIT_COLLISION; }
+  // :84-87 (costS is a float; the parent's value is read back through a double)
+  nodes.front().costS = node_cost(o, 0, nodes.front());
+  for (size_t i = 1; i != nodes.size(); i++) nodes[i].costS = node_cost(o, nodes[i - 1].costS, nodes[i]);
+  // :90-93
+  for (size_t i = 0; i != nodes.size(); i++) {
+    nodes[i].parentID = (int)i - 1;
+    o.tree.push_back(nodes[i]);
+  }
+  return CLRRT_REINIT_KEPT;
+}
+
 }  // namespace orc
 
 // ============================================================================ C API (ctypes)
@@ -852,4 +940,31 @@ extern "C" int orc_extract_best_path(void* h, int* ids, int cap) {
   int n = (int)path.size();
   for (int i = 0; i < n && i < cap; i++) ids[i] = path[i];
   return n;
+}
+
+// bestNodes = tree nodes `ids` (what extractBestPath returns, motionplanner.cpp:51).
+extern "C" void orc_path_commit(void* h, const int* ids, int n) {
+  Oracle* o = (Oracle*)h;
+  o->best.clear();
+  for (int i = 0; i < n; i++) o->best.push_back(o->tree[ids[i]]);
+}
+extern "C" long orc_path_size(void* h) { return (long)((Oracle*)h)->best.size(); }
+// to_world 0: transformNodesWorldToCar (motionplanner.cpp:22); 1: transformNodesCarToworld (:54).
+extern "C" void orc_path_transform(void* h, int to_world, const double* pose3) {
+  orc::transform_nodes(((Oracle*)h)->best, to_world, pose3);
+}
+extern "C" void orc_path_get_nodes(void* h, clrrt_node* out) {
+  Oracle tmp;
+  tmp.tree = ((Oracle*)h)->best;
+  if (!tmp.tree.empty()) orc_get_nodes(&tmp, 0, (long)tmp.tree.size(), out);
+}
+extern "C" void orc_path_get_rows(void* h, long i, double* out) {
+  Oracle tmp;
+  tmp.tree.push_back(((Oracle*)h)->best[i]);
+  orc_get_rows(&tmp, 0, out);
+}
+// initializeTree(RRT, veh, bestNodes, carPose) with carPose = 6 doubles (x, y, theta, delta, v, a).
+extern "C" int orc_initialize_tree(void* h, const double* car6) {
+  Oracle* o = (Oracle*)h;
+  return orc::initialize_tree(*o, o->best, vector<double>(car6, car6 + 6));
 }

@@ -52,6 +52,12 @@ def lib():
             "orc_draw_samples": (None, [vp, i, P(d), P(i)]),
             "orc_eval_iteration": (i, [vp, d, d, i, i, P(abi.Node)]),
             "orc_extract_best_path": (i, [vp, P(i), i]),
+            "orc_path_commit": (None, [vp, P(i), i]),
+            "orc_path_size": (C.c_long, [vp]),
+            "orc_path_transform": (None, [vp, i, P(d)]),
+            "orc_path_get_nodes": (None, [vp, P(abi.Node)]),
+            "orc_path_get_rows": (None, [vp, C.c_long, P(d)]),
+            "orc_initialize_tree": (i, [vp, P(d)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -98,6 +104,10 @@ class Oracle:
             self.L.orc_destroy(self.h)
         except Exception:
             pass
+
+    def set_params(self, params):
+        self.params = params
+        self.L.orc_set_params(self.h, C.byref(params))
 
     def set_obstacles(self, obs):
         obs = np.ascontiguousarray(obs, dtype=np.float64).reshape(-1, 7)
@@ -194,6 +204,32 @@ class Oracle:
         ids = (C.c_int * cap)()
         n = self.L.orc_extract_best_path(self.h, ids, cap)
         return list(ids[:min(n, cap)])
+
+    def path_commit(self, ids):
+        assert all(0 <= i < self.size() for i in ids), "path_commit: node id outside the tree"
+        arr = (C.c_int * max(1, len(ids)))(*ids)
+        self.L.orc_path_commit(self.h, arr, len(ids))
+
+    def path_transform(self, to_world, pose):
+        self.L.orc_path_transform(self.h, 1 if to_world else 0, _dp(np.ascontiguousarray(pose[:3], dtype=np.float64)))
+
+    def path_nodes(self):
+        n = self.L.orc_path_size(self.h)
+        arr = (abi.Node * max(1, n))()
+        if n:
+            self.L.orc_path_get_nodes(self.h, arr)
+        return arr if n else (abi.Node * 0)()
+
+    def path_rows(self, i):
+        nr = self.path_nodes()[i].nrows
+        out = np.zeros((nr, 10))
+        self.L.orc_path_get_rows(self.h, i, _dp(out))
+        return out
+
+    def initialize_tree(self, car_state):
+        cs = np.zeros(6)
+        cs[:min(6, len(car_state))] = np.asarray(car_state, dtype=np.float64)[:6]
+        return self.L.orc_initialize_tree(self.h, _dp(cs))
 
     def eval_iteration(self, sx, sy, explore, stable=False):
         out = (abi.Node * 2)()
