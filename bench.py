@@ -31,8 +31,9 @@ CONFIGS = {
                  desc="cfg2: 50-obstacle static urban scene, 4096 samples/batch, 0.2 s horizon"),
     "cfg3": dict(obstacles=200, moving=0, batch=16384, horizon_ms=2000.0,
                  desc="cfg3: 200-obstacle static urban scene, 16384 samples/batch per GPU, 2 s horizon"),
-    "cfg5": dict(obstacles=200, moving=20, batch=16384, horizon_ms=200.0,
-                 desc="cfg5-scene: 200 static + 20 moving obstacles, 16384 samples/batch per GPU, 0.2 s (5 Hz) horizon"),
+    "cfg5": dict(obstacles=200, moving=20, batch=16384, horizon_ms=200.0, replan=True,
+                 desc="cfg5: 200 static + 20 moving obstacles, 5 Hz replanning (0.2 s per query) with the tree "
+                      "re-initialised from the previous best path, 16384 samples/batch per GPU"),
 }
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
@@ -96,15 +97,39 @@ def cpu_model():
 
 def cpu_baseline(cfg, horizon_ms, n_queries, seed):
     """The reference-faithful CPU restatement (oracle/, kind 'port'), 1 thread, same scene and
-    horizon: nodes appended per second of wall time, n_queries fresh queries."""
+    horizon: nodes appended per second of wall time, n_queries queries (fresh trees; config 5: the
+    replanning sequence with the tree re-initialised from the committed path)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from clrrt import abi, scenes
+    import numpy as np
+    from clrrt import abi, replan, scenes
     from oracle_binding import Oracle
 
     obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
     nodes = goals = 0
     t_total = 0.0
+    pose = np.zeros(6)
+    o = None
     for q in range(n_queries):
+        if cfg.get("replan"):
+            o = o or Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), None)
+            Oracle.srand(seed + q)
+            t0 = time.perf_counter()
+            o.set_params(abi.default_params(v0=pose[4], goal=replan.goal_in_car_frame((40.0, 0.0, 0.0, 0.0), pose),
+                                            collision_mode=abi.CLRRT_COLLISION_OBB))
+            o.set_obstacles(replan.obstacles_in_car_frame(obs, q * replan.QUERY_PERIOD, pose))
+            o.path_transform(False, pose)
+            n0 = 1 if o.initialize_tree([0.0, 0.0, 0.0, pose[3], pose[4], pose[5]]) != abi.REINIT_KEPT else o.size()
+            o.expand_budget(horizon_ms, wall=True)
+            ids = o.extract_best_path()
+            o.path_commit(ids)
+            o.path_transform(True, pose)
+            t_total += time.perf_counter() - t0
+            n = o.nodes()
+            nodes += len(n["goal"]) - n0
+            goals += int(n["goal"][n0:].sum())
+            rows = [o.path_rows(i) for i in range(len(ids))]
+            pose = replan.advance_pose(pose, np.concatenate(rows) if rows else None)
+            continue
         o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
         Oracle.srand(seed + q)
         o.init_tree()
@@ -147,6 +172,7 @@ def main():
 
     obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
     params = clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
+    GOAL_WORLD = (40.0, 0.0, 0.0, 0.0)
     max_nodes = args.max_nodes
     max_rows = max_nodes * args.rows_per_node
     pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
@@ -160,10 +186,14 @@ def main():
         from clrrt import dist as cdist
         out_buf = torch.empty((2 * B, cdist.REC_BYTES), dtype=torch.uint8, device="cuda")
 
-    def query(seed):
-        """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""
-        pl.tree_init()
-        rng = clrrt.Rng(seed)
+    replanning = bool(cfg.get("replan"))
+    if replanning:
+        from clrrt import replan
+        make_params = replan.default_make_params(abi.CLRRT_COLLISION_OBB)
+        backend = replan.PlannerBackend(pl, make_params)
+        rp = {"pose": [0.0, 0.0, 0.0, 0.0, 0.0, 0.0], "q": 0, "outcomes": [], "reinit_ms": 0.0, "path_len": []}
+
+    def expand_query(rng):
         if world == 1:
             st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
             return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
@@ -175,7 +205,7 @@ def main():
             if n_now + 2 * world * B > max_nodes:
                 cap_stop = 1
                 break
-            allsmp = rng.draw_samples(params, world * B)
+            allsmp = rng.draw_samples(pl.params, world * B)
             first, count = cdist.shard(world * B, world, rank)
             mine = (abi.Sample * count).from_buffer(allsmp, first * C_SAMPLE)
             n_local = pl.round_eval(mine, out_buf.data_ptr())
@@ -187,6 +217,34 @@ def main():
             if t_max >= horizon:
                 break
         return nodes, goals, cap_stop
+
+    def query(seed):
+        """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""
+        rng = clrrt.Rng(seed)
+        if not replanning:
+            pl.tree_init()
+            return expand_query(rng)
+        # config 5: MotionPlanner::planMotion with commit_path = 1 (replan.py)
+        import numpy as np
+        pose = np.asarray(rp["pose"])
+        t_w = rp["q"] * replan.QUERY_PERIOD
+        t0 = time.perf_counter()
+        oc = backend.begin_query(pose, replan.goal_in_car_frame(GOAL_WORLD, pose),
+                                 replan.obstacles_in_car_frame(obs, t_w, pose))
+        rp["reinit_ms"] += (time.perf_counter() - t0) * 1e3
+        rp["outcomes"].append(oc)
+        res = expand_query(rng)
+        ids, _, n_goal = pl.extract_best_path()
+        rp.setdefault("goal_nodes", []).append(n_goal)
+        pl.path_commit(ids)
+        if world > 1:
+            cdist.fetch_path_rows(pl, rank)
+        pl.path_transform(True, pose)
+        _, rows = pl.path_download()
+        rp["path_len"].append(len(ids))
+        rp["pose"] = replan.advance_pose(pose, rows)
+        rp["q"] += 1
+        return res
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -288,6 +346,13 @@ def main():
                       "launches": {"rollout": roll_n, "nn": nn_n, "other": other_n}},
         "work": {**work, **cnt},
     }
+    if replanning:
+        nq = max(1, len(rp["outcomes"]))
+        line["config"]["replanning"] = {
+            "queries": len(rp["outcomes"]), "reinit_outcomes": rp["outcomes"][-args.steps:],
+            "path_lengths": rp["path_len"][-args.steps:], "goal_nodes": rp["goal_nodes"][-args.steps:],
+            "tree_nodes_last": pl.size()[0], "reinit_ms_avg": rp["reinit_ms"] / nq,
+            "note": "outcome 0 empty, 1 all erased, 2 committed path collides, 3 re-initialised from the path"}
     if not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(cfg, horizon, args.cpu_queries, args.seed)
     print(json.dumps(line), flush=True)

@@ -54,3 +54,31 @@ def shard(n_total, world, rank):
     """Contiguous slice [first, first + count) of a round's samples handled by `rank`."""
     per = n_total // world
     return rank * per, per
+
+
+def fetch_path_rows(planner, rank, group=None):
+    """Complete the committed path's trajectories across ranks (config 5 with N > 1).
+
+    clrrt_path_commit copies the rows of nodes this rank owns and zero-fills the others; the path
+    (a few nodes, a few thousand rows) is all-gathered and every node takes its rows from its owner,
+    so every rank ends up with the same committed path.  Returns the number of rows moved."""
+    import numpy as np
+    nodes, rows = planner.path_download()
+    if len(nodes) == 0:
+        return 0
+    world = dist.get_world_size(group)
+    cdev = torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    t = torch.from_numpy(np.ascontiguousarray(rows)).to(cdev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    parts = [p.cpu().numpy() for p in parts]
+    fixed = rows.copy()
+    moved = 0
+    for nd in nodes:
+        if nd.owner != rank:
+            a, b = nd.row_offset, nd.row_offset + nd.nrows
+            fixed[a:b] = parts[nd.owner][a:b]
+            moved += nd.nrows
+    if moved:
+        planner.path_load(nodes, fixed)
+    return moved
