@@ -100,3 +100,47 @@ def test_shard_slices_cover_the_round():
             first, count = cdist.shard(16384 * world, world, r)
             seen += list(range(first, first + count))
         assert seen == list(range(16384 * world))
+
+
+class _PathHolder:
+    """Stands in for clrrt.Planner's committed-path entries (path_download / path_load)."""
+
+    def __init__(self, nodes, rows):
+        self.nodes, self.rows = nodes, rows
+
+    def path_download(self):
+        return self.nodes, self.rows.copy()
+
+    def path_load(self, nodes, rows):
+        self.nodes, self.rows = nodes, np.array(rows)
+
+
+def _path_worker(rank, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from clrrt import abi
+    from clrrt import dist as cdist
+    owners, nrows = [0, 1, 1, 0], [1, 3, 2, 4]
+    nodes = (abi.Node * 4)()
+    full = np.arange(sum(nrows) * 10, dtype=np.float64).reshape(-1, 10) - 7.0
+    rows = np.zeros_like(full)
+    off = 0
+    for i in range(4):
+        nodes[i].owner, nodes[i].nrows, nodes[i].row_offset = owners[i], nrows[i], off
+        if owners[i] == rank:  # what clrrt_path_commit leaves: own rows copied, the others zero
+            rows[off:off + nrows[i]] = full[off:off + nrows[i]]
+        off += nrows[i]
+    h = _PathHolder(nodes, rows)
+    moved = cdist.fetch_path_rows(h, rank)
+    np.savez(os.path.join(out_dir, f"path{rank}.npz"), rows=h.rows, full=full, moved=moved)
+    dist.destroy_process_group()
+
+
+def test_two_rank_committed_path_rows_fetch(tmp_path):
+    """Config 5 on N GPUs: every rank completes the committed path with the rows held by their owners."""
+    mp.spawn(_path_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        d = np.load(tmp_path / f"path{r}.npz")
+        assert np.array_equal(d["rows"], d["full"])
+    assert int(np.load(tmp_path / "path0.npz")["moved"]) == 5 and int(np.load(tmp_path / "path1.npz")["moved"]) == 5
