@@ -52,6 +52,7 @@ _SIGS = {
     "clrrt_path_download": (C.c_int, [C.c_void_p, P(abi.Node), P(C.c_double)]),
     "clrrt_path_transform": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double)]),
     "clrrt_tree_init_from_path": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
+    "clrrt_path_mpc_message": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), C.c_int32, P(C.c_int32)]),
     "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
@@ -275,6 +276,15 @@ class Planner:
         self._chk(self.L.clrrt_tree_init_from_path(self.h, cs.ctypes.data_as(P(C.c_double)), C.byref(oc)),
                   "tree_init_from_path")
         return oc.value
+
+    def path_mpc_message(self, filtered=True):
+        """(P, 8) array x, y, theta, delta, v, a, a_cmd, d_cmd of the committed path's MPC message."""
+        n = C.c_int32()
+        self._chk(self.L.clrrt_path_mpc_message(self.h, int(filtered), None, 0, C.byref(n)), "path_mpc_message")
+        out = np.zeros((max(1, n.value), 8))
+        self._chk(self.L.clrrt_path_mpc_message(self.h, int(filtered), out.ctypes.data_as(P(C.c_double)), n.value,
+                                                C.byref(n)), "path_mpc_message")
+        return out[:n.value]
 
     def expand(self, rng, n_iters=0, budget_ms=0.0, mode=CLRRT_MODE_EXACT, batch=0):
         st = abi.Stats()

@@ -5,7 +5,7 @@ header documents so a drift between the two fails at import time.
 """
 import ctypes as C
 
-CLRRT_ABI_VERSION = 5  # include/clrrt.h
+CLRRT_ABI_VERSION = 6  # include/clrrt.h
 CLRRT_MODE_EXACT = 0
 CLRRT_PARENT_PREV = -2  # goal-biased record: parent = the record before it (include/clrrt.h)
 CLRRT_MODE_BATCH = 1

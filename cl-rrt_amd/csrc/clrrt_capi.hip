@@ -15,6 +15,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -938,6 +939,43 @@ int clrrt_tree_init_from_path(clrrt_ctx* c, const double car_state[6], int32_t* 
   HIPC(c, hipStreamSynchronize(c->stream));
   bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   if (outcome) *outcome = (int32_t)out[0];
+  return CLRRT_OK;
+}
+
+int clrrt_path_mpc_message(clrrt_ctx* c, int32_t filtered, double* out, int32_t cap, int32_t* n_points) {
+  if (!c || !n_points || cap < 0 || (cap > 0 && !out)) return CLRRT_EINVAL;
+  *n_points = 0;
+  if (c->path_n == 0) return CLRRT_OK;
+  std::vector<clrrt_node> h(c->path_n);
+  std::vector<double> rows(10 * c->path_nrows);
+  int rc = clrrt_path_download(c, h.data(), rows.data());
+  if (rc != CLRRT_OK) return rc;
+  // generateMPCmessage: rows 1 .. nrows-1 of every segment
+  std::vector<std::array<double, 8>> msg;
+  for (const clrrt_node& nd : h)
+    for (int i = 1; i < nd.nrows; i++) {
+      const double* r = &rows[(nd.row_offset + i) * 10];
+      msg.push_back({r[0], r[1], r[2], r[3], r[4], r[5], r[8], r[9]});
+    }
+  if (filtered && !msg.empty()) {  // filterMPCmessage: keep index i when the distance since the last kept is 0
+    std::vector<std::array<double, 8>> f;
+    const double interval = 5;
+    double d = 0;
+    for (size_t i = 1; i != msg.size(); i++) {
+      if (d == 0) {
+        std::array<double, 8> p = msg[i];
+        p[3] = NAN;
+        f.push_back(p);
+      }
+      const double dx = msg[i][0] - msg[i - 1][0], dy = msg[i][1] - msg[i - 1][1];
+      d += sqrt(dx * dx + dy * dy);
+      if (d >= interval) d = 0;
+    }
+    msg.swap(f);
+  }
+  *n_points = (int32_t)msg.size();
+  for (int i = 0; i < (int)msg.size() && i < cap; i++)
+    for (int k = 0; k < 8; k++) out[8 * i + k] = msg[i][k];
   return CLRRT_OK;
 }
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 5
+#define CLRRT_ABI_VERSION 6
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -260,6 +260,13 @@ int clrrt_path_transform(clrrt_ctx* ctx, int32_t dir, const double pose[3]);
  * the obstacle cost term evaluate each trajectory row (the commented-out call at :74/:108) under
  * the context's collision mode and obstacles. */
 int clrrt_tree_init_from_path(clrrt_ctx* ctx, const double car_state[6], int32_t* outcome);
+/* The MPC trajectory message of the committed path (convertNodesToPath motionplanner.cpp:264-275 +
+ * generateMPCmessage :103-128; with `filtered`, filterMPCmessage :130-151, waypoints >= 5 m apart).
+ * One point = 8 doubles (x, y, theta, delta, v, a, a_cmd = row[8], d_cmd = row[9]); rows 1.. of
+ * every node.  The filtered message carries no delta (the reference does not copy it): NaN there.
+ * Writes min(*n_points, cap) points.  An empty message stays empty (the reference's loops over
+ * size()-1 / from index 1 are undefined for it). */
+int clrrt_path_mpc_message(clrrt_ctx* ctx, int32_t filtered, double* out, int32_t cap, int32_t* n_points);
 
 /* ---- expansion ---- */
 /* Runs expandTree iterations drawn from `rng` until `n_iters` iterations are consumed

@@ -968,3 +968,46 @@ extern "C" int orc_initialize_tree(void* h, const double* car6) {
   Oracle* o = (Oracle*)h;
   return orc::initialize_tree(*o, o->best, vector<double>(car6, car6 + 6));
 }
+
+// convertNodesToPath motionplanner.cpp:264-275 + generateMPCmessage :103-128 (+ filterMPCmessage
+// :130-151 when `filtered`) over bestNodes; the message's fields as in car_msgs::Trajectory.
+// Points are written as 8 doubles (x, y, theta, delta, v, a, a_cmd, d_cmd; delta NaN when filtered,
+// the reference leaves it out).  Returns the point count.  Empty messages stay empty (the
+// reference's size()-1 loop and i = 1 loop are undefined there).
+namespace orc {
+struct Traj { vector<double> x, y, theta, delta, v, a, a_cmd, d_cmd; };
+}
+extern "C" int orc_path_mpc_message(void* h, int filtered, double* out, int cap) {
+  using orc::Traj;
+  Oracle* o = (Oracle*)h;
+  Traj tra;
+  for (auto it = o->best.begin(); it != o->best.end(); ++it)
+    for (size_t i = 1; i < it->tra.size(); i++) {
+      tra.x.push_back(it->tra[i][0]); tra.y.push_back(it->tra[i][1]); tra.theta.push_back(it->tra[i][2]);
+      tra.delta.push_back(it->tra[i][3]); tra.v.push_back(it->tra[i][4]); tra.a.push_back(it->tra[i][5]);
+      tra.a_cmd.push_back(it->tra[i][8]); tra.d_cmd.push_back(it->tra[i][9]);
+    }
+  if (filtered && !tra.x.empty()) {
+    Traj f;
+    double interval = 5;
+    double d = 0;
+    for (size_t i = 1; i != tra.x.size(); i++) {
+      if (d == 0) {
+        f.x.push_back(tra.x[i]); f.y.push_back(tra.y[i]); f.theta.push_back(tra.theta[i]);
+        f.v.push_back(tra.v[i]); f.a.push_back(tra.a[i]); f.a_cmd.push_back(tra.a_cmd[i]);
+        f.d_cmd.push_back(tra.d_cmd[i]);
+      }
+      d += sqrt(pow(tra.x[i] - tra.x[i - 1], 2) + pow(tra.y[i] - tra.y[i - 1], 2));
+      if (d >= interval) d = 0;
+    }
+    tra = f;
+  }
+  int n = (int)tra.x.size();
+  for (int i = 0; i < n && i < cap; i++) {
+    double* p = out + 8 * i;
+    p[0] = tra.x[i]; p[1] = tra.y[i]; p[2] = tra.theta[i];
+    p[3] = filtered ? NAN : tra.delta[i];
+    p[4] = tra.v[i]; p[5] = tra.a[i]; p[6] = tra.a_cmd[i]; p[7] = tra.d_cmd[i];
+  }
+  return n;
+}

@@ -58,6 +58,7 @@ def lib():
             "orc_path_get_nodes": (None, [vp, P(abi.Node)]),
             "orc_path_get_rows": (None, [vp, C.c_long, P(d)]),
             "orc_initialize_tree": (i, [vp, P(d)]),
+            "orc_path_mpc_message": (i, [vp, i, P(d), i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -225,6 +226,12 @@ class Oracle:
         out = np.zeros((nr, 10))
         self.L.orc_path_get_rows(self.h, i, _dp(out))
         return out
+
+    def path_mpc_message(self, filtered=True):
+        n = self.L.orc_path_mpc_message(self.h, int(filtered), None, 0)
+        out = np.zeros((max(1, n), 8))
+        self.L.orc_path_mpc_message(self.h, int(filtered), _dp(out), n)
+        return out[:n]
 
     def initialize_tree(self, car_state):
         cs = np.zeros(6)

@@ -151,6 +151,35 @@ def test_oracle_replanning_loop_runs():
     assert any(e[1] == abi.REINIT_KEPT for e in log[1:]), [e[1] for e in log]
 
 
+def _mpc_ref(seg_rows, filtered):
+    """generateMPCmessage / filterMPCmessage (motionplanner.cpp:103-151) in plain Python."""
+    msg = [[r[0], r[1], r[2], r[3], r[4], r[5], r[8], r[9]] for rows in seg_rows for r in rows[1:]]
+    if not filtered or not msg:
+        return np.array(msg).reshape(-1, 8)
+    out, d = [], 0.0
+    for i in range(1, len(msg)):
+        if d == 0:
+            out.append(msg[i][:3] + [math.nan] + msg[i][4:])
+        d += math.sqrt((msg[i][0] - msg[i - 1][0]) ** 2 + (msg[i][1] - msg[i - 1][1]) ** 2)
+        if d >= 5:
+            d = 0.0
+    return np.array(out).reshape(-1, 8)
+
+
+def test_oracle_mpc_message():
+    o = _grown_oracle(iters=400)
+    ids = o.extract_best_path()
+    o.path_commit(ids)
+    o.path_transform(True, (10.0, 5.0, 0.3))
+    seg = [o.path_rows(i) for i in range(len(ids))]
+    for filtered in (False, True):
+        got, ref = o.path_mpc_message(filtered), _mpc_ref(seg, filtered)
+        assert got.shape == ref.shape and got.shape[0] > 3
+        assert np.array_equal(got, ref, equal_nan=True)
+    o.path_commit([])
+    assert o.path_mpc_message(True).shape == (0, 8)
+
+
 # ------------------------------------------------------------------------------------------- GPU
 def _planner(mode, max_batch=256):
     return clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 21,
@@ -226,6 +255,9 @@ def test_replanning_queries_parity(kind):
         ids_g, rows_g = gb.end_query(pose)
         assert ids_o == ids_g
         assert np.array_equal(rows_g.view(np.uint64), rows_o.view(np.uint64))
+        for filtered in (False, True):
+            mo, mg = o.path_mpc_message(filtered), pl.path_mpc_message(filtered)
+            assert mo.shape == mg.shape and np.array_equal(mg.view(np.uint64), mo.view(np.uint64)), (q, filtered)
         pose = replan.advance_pose(pose, rows_o)
     print(kind, "outcomes", outcomes)
     assert outcomes[0] == abi.REINIT_EMPTY
