@@ -376,11 +376,13 @@ class Planner:
         self._chk(self.L.clrrt_set_option(self.h, key.encode(), int(value)), f"set_option({key})")
 
     def nn_stats(self):
-        out = (C.c_int64 * 10)()
+        out = (C.c_int64 * 19)()
         self._chk(self.L.clrrt_nn_stats(self.h, out), "nn_stats")
         return {"waves": out[0], "nodes_read": out[1], "rings": out[2], "truncated_waves": out[3],
                 "last_fallback_samples": out[4], "tiles_seen": out[5], "tiles_searched": out[6],
-                "pairs_queued": out[7], "exact_keys": out[8]}
+                "pairs_queued": out[7], "exact_keys": out[8], "walk_supers": out[10], "walk_tiles": out[11],
+                "walk_queued": out[12], "walk_exact": out[13], "walk_clk_bounds": out[14], "walk_clk_super": out[15],
+                "walk_clk_visit": out[16], "walk_clk_drain": out[17], "walk_clk_total": out[18]}
 
     def set_nn_grid(self, min_nodes, modes=1, wave_budget=0):
         """Trees of >= min_nodes nodes search the samples of `modes` (1 explore, 2 optimize) through

@@ -92,6 +92,8 @@ struct clrrt_ctx {
   double* h_bbox = nullptr;  // [4] pinned
   int64_t nng_min_nodes = INT64_MAX;  // clrrt_set_nn_grid: off by default (brute force is faster on bench trees)
   int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
+  int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
+  WalkBufs nnw{};                      // allocated on first use
   int nng_modes = 1;
   int nng_budget = 0;
   // persistent rollouts (k_roll_prep + k_roll_run)
@@ -359,7 +361,8 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
-                  c->ri_terms};
+                  c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -452,8 +455,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
   chk(dalloc(&c->fb_count, 1));
-  chk(dalloc(&c->work_ctr, 24));
-  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 24 * sizeof(unsigned long long)));
+  chk(dalloc(&c->work_ctr, 32));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 32 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
@@ -989,7 +992,7 @@ int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 24 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 32 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return CLRRT_OK;
 }
@@ -1004,13 +1007,13 @@ int clrrt_work_counters(clrrt_ctx* c, int64_t out[3]) {
   return CLRRT_OK;
 }
 
-int clrrt_nn_stats(clrrt_ctx* c, int64_t out[10]) {
+int clrrt_nn_stats(clrrt_ctx* c, int64_t out[19]) {
   if (!c || !out) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipStreamSynchronize(c->stream));
-  unsigned long long h[10];
+  unsigned long long h[19];
   HIPC(c, hipMemcpy(h, c->work_ctr + 8, sizeof(h), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 10; i++) out[i] = (int64_t)h[i];
+  for (int i = 0; i < 19; i++) out[i] = (int64_t)h[i];
   out[4] &= 0xffffffff;
   return CLRRT_OK;
 }
@@ -1020,6 +1023,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   const std::string k(key);
   if (k == "roll_persistent") c->roll_persistent = value != 0;
   else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
+  else if (k == "nn_walk_min" && value >= 0) c->nnw_min_nodes = value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
@@ -1081,6 +1085,29 @@ static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
   return CLRRT_OK;
 }
 
+// Walk-search buffers, sized for the context's capacity (first use).
+static int ensure_walk(clrrt_ctx* c) {
+  if (c->nnw.P) return CLRRT_OK;
+  const int64_t M = std::max<int64_t>(c->cap.max_nodes, c->cap.max_batch);
+  const int64_t Mp = c->cap.max_nodes + 1024;
+  HIPC(c, dalloc(&c->nnw.sorder, c->cap.max_batch));
+  HIPC(c, dalloc(&c->nnw.keys, 2 * M));
+  HIPC(c, dalloc(&c->nnw.keys2, 2 * M));
+  HIPC(c, dalloc(&c->nnw.vals, std::max<int64_t>(M, Mp)));  // also the run markers of the padded records
+  HIPC(c, dalloc(&c->nnw.vals2, M));
+  c->nnw.tmp_bytes = walk_sort_bytes((int)M);
+  HIPC(c, hipMalloc(&c->nnw.tmp, std::max<size_t>(c->nnw.tmp_bytes, 256)));
+  HIPC(c, dalloc(&c->nnw.Q, Mp));
+  HIPC(c, dalloc(&c->nnw.CE, Mp));
+  HIPC(c, dalloc(&c->nnw.ID, Mp));
+  HIPC(c, dalloc(&c->nnw.HEAD, Mp));
+  HIPC(c, dalloc(&c->nnw.TRIG, Mp));
+  HIPC(c, dalloc(&c->nnw.tiles, Mp / 64 + 1));
+  HIPC(c, dalloc(&c->nnw.supers, Mp / 1024 + 1));
+  HIPC(c, dalloc(&c->nnw.P, Mp));  // last: marks the set complete
+  return CLRRT_OK;
+}
+
 // Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
 static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   hipStream_t st = c->stream;
@@ -1109,6 +1136,15 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   const bool region_ok = std::isfinite(W * H) && W * H > 0;
   const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && region_ok;
   const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && region_ok;
+  if (!use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && region_ok) {
+    int rc = ensure_walk(c);
+    if (rc != CLRRT_OK) return rc;
+    HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, fr, x0, y0, x1, y1, c->nnw, c->cand,
+                           c->ckey, c->ncand, c->ctie, c->work_ctr + 18));
+    if (scratch) HIPC(c, launch_nn_exact_only(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->ctie, scratch,
+                                              c->cand, c->ckey, c->ncand));
+    return CLRRT_OK;
+  }
   if (use_grid || ordered) {
     double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
     // square power-of-two grid (Morton cell numbering), at most kNngMaxCells cells

@@ -144,6 +144,42 @@ struct NnFrame {
   float delta;
   int debug;  // diagnostics only (results change!): 1 = skip the exact pass
 };
+// Bounds of a tile (64 place-ordered records) or super-tile (1024) of the walk search
+// (clrrt_nnwalk.hip), frame coordinates.
+struct WalkTile {
+  float pcx, pcy, pr;  // disc holding the node positions (pr < 0: no records)
+  float rcx, rcy, rr;  // disc holding the ref.back() points
+  float thx, thy, thh; // arc of node headings: unit centre, half width [rad] (>= 3: unbounded)
+  float apx, apy, aph; // arc of ang_par directions
+  float cemin;         // min costE
+  float aopt;          // min (costE - |position - (pcx, pcy)|)
+  int32_t nonfinite;   // a record with a non-finite field: no bound
+  int32_t pad;
+};
+static_assert(sizeof(WalkTile) == 64, "WalkTile layout");
+struct WalkBufs {
+  uint32_t *keys, *keys2;  // [2 max_nodes] 64-bit sort keys (radix sort in/out; samples: 32-bit)
+  int *vals, *vals2;       // [max(max_nodes, max_batch)] node ids (vals2 = place order)
+  int* sorder;             // [max_batch] samples in place order
+  void* tmp;               // radix sort scratch
+  size_t tmp_bytes;
+  float4 *P, *Q;           // [max_nodes + 1024] (x, y, c, s), (bx, by, ca, sa) relative to the frame origin
+  float* CE;               // costE
+  int* ID;                 // node id (-1: padding)
+  int* HEAD;               // first record of the run of records with equal Dubins-key inputs
+  double2* TRIG;           // (cos, sin)(ang_par) in double
+  WalkTile *tiles, *supers;
+};
+size_t walk_sort_bytes(int n);
+// Candidate lists of samples S[0 .. B) (same output as the brute force: cand, ckey, ncand, ctie);
+// (x0, y0, x1, y1) = box holding every finite node position (the Morton frame).
+hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
+                          const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
+                          float* ckey, int* ncand, int* ctie, unsigned long long* stats);
+// Brute-force candidate lists of the samples fb_list[0 .. *fb_count) (the walk search's hand-offs).
+hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
+                                int* ncand, int* ctie, int max_chunks, const int* fb_list, const int* fb_count);
 
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
 // selection involves equal keys are re-sorted with the replay of std::sort.
@@ -151,6 +187,10 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
                      int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
                      int* fb_count, unsigned long long* stats, const NnFrame& fr, bool ordered);
+// EXACT mode after a search that filled ctie: std::sort replay for the tied samples.
+hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
+                                int* ncand);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 // Round rollouts as k_roll_prep + persistent k_roll_run (see clrrt_kernels.hip); prep holds
 // njobs * rollout_prep_bytes(), best B ints, qnext one int.

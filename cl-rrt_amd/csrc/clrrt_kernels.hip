@@ -1553,6 +1553,21 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
   return hipSuccess;
 }
 
+hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
+                                int* ncand, int* ctie, int max_chunks, const int* fb_list, const int* fb_count) {
+  return launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
+}
+
+hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
+                                int* ncand) {
+  hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, scratch, cand, ckey,
+                     ncand);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
                                   float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,

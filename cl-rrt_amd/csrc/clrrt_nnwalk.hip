@@ -1,0 +1,609 @@
+// clrrt_nnwalk.hip — nearest-node search (sortNodesExplore / sortNodesOptimize + feasibleNode,
+// rrtplanner.cpp:227-289) by a bounded walk over a place-ordered tree, one wave per sample.
+//
+// The reference keys every node by its Dubins distance to the sample (explore) or costE + Dubins
+// distance (optimize), sorts, and keeps the first sortLimit feasible nodes.  The result is the
+// sortLimit smallest (key, node index) pairs among the feasible nodes (+ one more entry that
+// reveals a key tie at the selection boundary), which the brute-force kernels find by scanning all
+// N nodes for every sample.  On bench trees a sample's list depends on ~0.1% of the nodes, so:
+//
+// Index (rebuilt every round): nodes sorted by a 16-bit-per-axis Morton code of their position
+// (radix sort), copied into place order as float records relative to the round's frame origin,
+// padded to a multiple of 1024.  Every 32 consecutive records form a tile, every 32 tiles a
+// super-tile; each carries conservative bounds (WalkTile): a disc around the positions and one
+// around the ref.back() points, the arc of headings and the arc of ang_par directions, the minimum
+// costE and the minimum of costE - |position - disc centre|.
+//
+// Search (k_walk_search, one 64-lane wave per sample): lower bounds on the keys of every super-tile
+// are kept in LDS; tiles are visited in passes of growing bound threshold (so the list fills with
+// near nodes first and its 11th key prunes the rest): a super-tile's 32 tile bounds are computed by
+// 32 lanes, the tiles under the threshold are visited two at a time (one node per lane) through the
+// necessary conditions of the brute-force prefilter plus the turning bound below, and the
+// super-tile's bound becomes that of its remaining tiles.  Survivors are queued in LDS and their
+// exact keys computed 64 at a time, so lanes stay converged.
+// The sample's list lives in lanes 0..10 (sorted), the 11th entry (kth, idk) is wave-uniform.
+//
+// Bounds (each lower-bounds the float key the reference computes; margins cover float rounding):
+//   * key >= |q|                 (Dubins length >= Euclidean; |q| (1 - 1e-5) - 1e-4 in float);
+//   * key >= rho * beta          beta = angle between the node heading and the direction to the
+//                                sample: a left-turn-then-straight path ending at bearing beta
+//                                turns by psi >= beta (psi <= pi: the end point lies between the
+//                                arc chord bearing psi / 2 and psi), and the inside-circle case
+//                                has key >= rho * pi (checked numerically by tests/test_nnwalk_bounds.py);
+//   * optimize: key = costE + dubins >= costE - |p - c| + |s - c| for any point c;
+//   * feasibleNode: the direction from ref.back() to the sample must lie within pi/4 of ang_par and
+//     |sample - ref.back()| >= 2.1 ref_res.
+// A skipped node, tile or super-tile can hold no pair that enters the list, so every list equals
+// the brute-force one bit for bit (ties included: pairs are ordered by (key, node index) in both).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "clrrt_dev.hpp"
+#include "clrrt_internal.hpp"
+
+namespace clrrt {
+
+#define CAND_K 10
+#define NN_K (CAND_K + 1)
+#define WALK_TILE 32
+#define WALK_SUPER 32  // tiles per super-tile
+
+#define LAUNCH_CHECK3()                          \
+  do {                                           \
+    hipError_t e_ = hipGetLastError();           \
+    if (e_ != hipSuccess) return e_;             \
+  } while (0)
+
+__device__ __forceinline__ uint32_t w_spread(uint32_t v) {
+  v &= 0xffff;
+  v = (v | (v << 8)) & 0x00ff00ff;
+  v = (v | (v << 4)) & 0x0f0f0f0f;
+  v = (v | (v << 2)) & 0x33333333;
+  v = (v | (v << 1)) & 0x55555555;
+  return v;
+}
+
+// Sort key of each node: Morton code of its position in the frame box (high word; non-finite
+// positions sort last), then the costE bits, so records with equal key inputs (e.g. the root's
+// zero-length children) end up next to each other.
+__global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
+                            uint64_t* __restrict__ keys, int* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const double x = nodes[i].x, y = nodes[i].y;
+  uint32_t k = 0xffffffffu;
+  if (isfinite(x) && isfinite(y)) {
+    const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
+    const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
+    k = w_spread((uint32_t)fx) | (w_spread((uint32_t)fy) << 1);
+  }
+  keys[i] = ((uint64_t)k << 32) | __float_as_uint(nodes[i].costE);
+  vals[i] = i;
+}
+
+// Morton key of each sample (same frame as the nodes).
+__global__ void k_walk_skeys(const clrrt_sample* __restrict__ S, int B, double x0, double y0, double scale,
+                             uint32_t* __restrict__ keys, int* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const double x = S[i].x, y = S[i].y;
+  uint32_t k = 0xffffffffu;
+  if (isfinite(x) && isfinite(y)) {
+    const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
+    const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
+    k = w_spread((uint32_t)fx) | (w_spread((uint32_t)fy) << 1);
+  }
+  keys[i] = k;
+  vals[i] = i;
+}
+
+// Place-ordered float records (relative to the frame origin); entries N .. Npad are padding (id -1).
+__global__ void k_walk_gather(const NnRec* __restrict__ nodes, int N, int Npad, const int* __restrict__ order,
+                              double ox, double oy, float4* __restrict__ P, float4* __restrict__ Q,
+                              float* __restrict__ CE, int* __restrict__ ID, int* __restrict__ dup,
+                              double2* __restrict__ trig) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Npad) return;
+  if (j < N) {
+    const int i = order[j];
+    const NnRec& r = nodes[i];
+    P[j] = make_float4((float)(r.x - ox), (float)(r.y - oy), r.c, r.s);
+    Q[j] = make_float4((float)(r.bx - ox), (float)(r.by - oy), r.ca, r.sa);
+    CE[j] = r.costE;
+    ID[j] = i;
+    double sp, cp;
+    sincos(r.ang_par, &sp, &cp);
+    trig[j] = make_double2(cp, sp);
+    // a record whose Dubins-key inputs equal its predecessor's has the same key for every sample
+    bool same = false;
+    if (j > 0) {
+      const NnRec& o = nodes[order[j - 1]];
+      same = r.x == o.x && r.y == o.y && r.c == o.c && r.s == o.s && r.costE == o.costE;
+    }
+    dup[j] = same ? -1 : j;
+  } else {
+    dup[j] = j;
+    P[j] = make_float4(0.f, 0.f, 1.f, 0.f);
+    Q[j] = make_float4(0.f, 0.f, 1.f, 0.f);
+    CE[j] = 0.f;
+    ID[j] = -1;
+  }
+}
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wmin(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bounds of `size` consecutive records per tile, one wave per tile.  `slack` inflates the discs by
+// the float frame's coordinate error so the bounds hold for the exact positions too.
+__global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P, const float4* __restrict__ Q,
+                                                    const float* __restrict__ CE, const int* __restrict__ ID,
+                                                    int ntiles, int size, float slack, WalkTile* __restrict__ out) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= ntiles) return;
+  const int b = t * size;
+  float spx = 0, spy = 0, srx = 0, sry = 0, sux = 0, suy = 0, sax = 0, say = 0, cnt = 0, bad = 0;
+  for (int k = lane; k < size; k += 64) {
+    const int j = b + k;
+    if (ID[j] < 0) continue;
+    const float4 p = P[j], q = Q[j];
+    const float ce = CE[j];
+    const bool fin = isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w) && isfinite(q.x) &&
+                     isfinite(q.y) && isfinite(q.z) && isfinite(q.w) && isfinite(ce);
+    if (!fin) { bad += 1; continue; }
+    spx += p.x; spy += p.y; srx += q.x; sry += q.y;
+    sux += p.z; suy -= p.w;  // heading direction (cos th, sin th) = (c, -s)
+    sax += q.z; say += q.w;
+    cnt += 1;
+  }
+  cnt = wsum(cnt);
+  bad = wsum(bad);
+  WalkTile w;
+  w.nonfinite = bad > 0;
+  w.pad = 0;
+  if (cnt == 0) {  // padding only (or only non-finite records)
+    w.pcx = w.pcy = w.rcx = w.rcy = 0.f;
+    w.pr = w.rr = -1.f;  // empty
+    w.thx = 1.f; w.thy = 0.f; w.thh = 4.f;
+    w.apx = 1.f; w.apy = 0.f; w.aph = 4.f;
+    w.cemin = w.aopt = 0.f;
+    if (lane == 0) out[t] = w;
+    return;
+  }
+  const float pcx = wsum(spx) / cnt, pcy = wsum(spy) / cnt;
+  const float rcx = wsum(srx) / cnt, rcy = wsum(sry) / cnt;
+  float ux = wsum(sux), uy = wsum(suy), ax = wsum(sax), ay = wsum(say);
+  const float un = sqrtf(ux * ux + uy * uy), an = sqrtf(ax * ax + ay * ay);
+  const bool uok = un > 1e-3f * cnt, aok = an > 1e-3f * cnt;
+  ux = uok ? ux / un : 1.f; uy = uok ? uy / un : 0.f;
+  ax = aok ? ax / an : 1.f; ay = aok ? ay / an : 0.f;
+  float pr = 0, rr = 0, ud = 1, ad = 1, cmin = __builtin_inff(), aopt = __builtin_inff();
+  for (int k = lane; k < size; k += 64) {
+    const int j = b + k;
+    if (ID[j] < 0) continue;
+    const float4 p = P[j], q = Q[j];
+    const float ce = CE[j];
+    const bool fin = isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w) && isfinite(q.x) &&
+                     isfinite(q.y) && isfinite(q.z) && isfinite(q.w) && isfinite(ce);
+    if (!fin) continue;
+    const float dp = sqrtf((p.x - pcx) * (p.x - pcx) + (p.y - pcy) * (p.y - pcy));
+    const float dr = sqrtf((q.x - rcx) * (q.x - rcx) + (q.y - rcy) * (q.y - rcy));
+    pr = fmaxf(pr, dp);
+    rr = fmaxf(rr, dr);
+    // unit-length up to float rounding: normalise before the dot product
+    const float hn = sqrtf(p.z * p.z + p.w * p.w), qn = sqrtf(q.z * q.z + q.w * q.w);
+    ud = fminf(ud, (p.z * ux - p.w * uy) / hn);
+    ad = fminf(ad, (q.z * ax + q.w * ay) / qn);
+    cmin = fminf(cmin, ce);
+    aopt = fminf(aopt, ce - dp);
+  }
+  pr = wmax(pr); rr = wmax(rr); ud = wmin(ud); ad = wmin(ad); cmin = wmin(cmin); aopt = wmin(aopt);
+  w.pcx = pcx; w.pcy = pcy; w.pr = pr * (1.f + 1e-5f) + 2.f * slack + 1e-5f;
+  w.rcx = rcx; w.rcy = rcy; w.rr = rr * (1.f + 1e-5f) + 2.f * slack + 1e-5f;
+  w.thx = ux; w.thy = uy; w.thh = uok ? acosf(fminf(fmaxf(ud, -1.f), 1.f)) + 2e-3f : 4.f;
+  w.apx = ax; w.apy = ay; w.aph = aok ? acosf(fminf(fmaxf(ad, -1.f), 1.f)) + 2e-3f : 4.f;
+  w.cemin = cmin;
+  w.aopt = aopt - 2.f * slack - 1e-4f - 1e-5f * fabsf(aopt);
+  if (lane == 0) out[t] = w;
+}
+
+// acos on [-1, 1] (Abramowitz & Stegun 4.4.45), |error| <= 7e-5 rad (float evaluation included).
+__device__ __forceinline__ float acos_apx(float x) {
+  const float ax = fminf(fabsf(x), 1.f);
+  const float r = sqrtf(1.f - ax) * (1.5707288f + ax * (-0.2121144f + ax * (0.0742610f + ax * -0.0187293f)));
+  return x < 0.f ? 3.14159265f - r : r;
+}
+
+// Lower bound on the keys of a tile's nodes for the sample at (rsx, rsy) (frame coordinates);
+// +inf: no node of the tile can enter the list (empty, or feasibleNode fails for all of them);
+// -inf: no bound (non-finite records).  flen = feasibility length lower limit.  Angles come from
+// acos_apx; each angle test carries 5e-4 rad per approximated term on top of its float margin.
+__device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy, bool ex, float flen) {
+  if (w.nonfinite) return -__builtin_inff();
+  if (w.pr < 0.f) return __builtin_inff();
+  const float rho = 4.77f;
+  // feasibility: direction from the ref.back() disc to the sample vs the ang_par arc
+  const float ex2 = rsx - w.rcx, ey2 = rsy - w.rcy;
+  const float E2 = sqrtf(ex2 * ex2 + ey2 * ey2);
+  if (E2 + w.rr < flen) return __builtin_inff();
+  if (E2 > w.rr && w.aph < 3.f) {
+    const float a2 = 1.57079633f - acos_apx(w.rr / E2);  // asin
+    const float ang2 = acos_apx((ex2 * w.apx + ey2 * w.apy) / E2);
+    if (ang2 - a2 - w.aph > 0.78539816f + 5e-3f) return __builtin_inff();
+  }
+  const float dx = rsx - w.pcx, dy = rsy - w.pcy;
+  const float D = sqrtf(dx * dx + dy * dy);
+  float lb = D - w.pr;
+  if (D > w.pr && w.thh < 3.f) {
+    const float al = 1.57079633f - acos_apx(w.pr / D);
+    const float bmin = acos_apx((dx * w.thx + dy * w.thy) / D) - al - w.thh - 3e-3f;
+    lb = fmaxf(lb, rho * bmin);
+  }
+  lb = lb - 2e-3f - 1e-5f * fabsf(lb);
+  if (!ex) lb = fmaxf(w.aopt + D * (1.f - 1e-5f) - 2e-3f, w.cemin + lb);
+  return lb == lb ? lb : -__builtin_inff();
+}
+
+// Wave-uniform values kept in scalar registers.
+__device__ __forceinline__ float uni(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ bool w_less(float ka, int ia, float kb, int ib) {
+  return (ka < kb) || (ka == kb && ia < ib);
+}
+
+// The sample's list: lane j < NN_K holds entry j (ascending); insert (k, i) when it precedes entry 10.
+__device__ __forceinline__ void w_insert(float& lk, int& li, float k, int i, int lane) {
+  const bool before = w_less(lk, li, k, i) && lane < NN_K;  // entries that stay ahead of the new one
+  const int pos = __popcll(__ballot(before));
+  const float uk = __shfl_up(lk, 1, 64);
+  const int ui = __shfl_up(li, 1, 64);
+  if (lane < NN_K) {
+    if (lane == pos) { lk = k; li = i; }
+    else if (lane > pos) { lk = uk; li = ui; }
+  }
+}
+
+// One wave per sample.  LDS per super-tile: s_lb = lower bound of its not yet visited tiles (+inf:
+// nothing left that can enter the list), s_vis = visited-or-discarded tile mask.  Pass k visits the
+// tiles whose bound is <= min(T_k, kth) (T_k grows geometrically from the smallest bound), two tiles
+// of 32 nodes per step (lanes 0-31 / 32-63), so nodes are visited roughly in the order of their
+// bounds and the list's 11th key prunes the rest.  The search ends after the first pass whose
+// threshold reaches kth: every tile with a bound <= kth has then been visited.
+__global__ void __launch_bounds__(64) k_walk_search(const clrrt_sample* __restrict__ S, int B,
+                                                    const NnRec* __restrict__ nodes, const float4* __restrict__ P,
+                                                    const float4* __restrict__ Q, const float* __restrict__ CE,
+                                                    const int* __restrict__ ID, const int* __restrict__ HEAD,
+                                                    const WalkTile* __restrict__ tiles, int ntiles,
+                                                    const WalkTile* __restrict__ sup, int nsup, DevParams p,
+                                                    NnFrame fr, int* __restrict__ cand, float* __restrict__ ckey,
+                                                    int* __restrict__ ncand, int* __restrict__ ctie,
+                                                    const int* __restrict__ sorder,
+                                                    const double2* __restrict__ TRIG,
+                                                    unsigned long long* __restrict__ stats) {
+  extern __shared__ float s_lb[];  // [nsup] bounds, then [nsup] visited masks
+  uint32_t* s_vis = (uint32_t*)(s_lb + nsup);
+  __shared__ int s_q[64];
+  const int lane = threadIdx.x;
+  // XCD-aware: consecutive blocks go to the 8 XCDs in turn; XCD x takes the x-th eighth of the
+  // place-ordered samples, so its L2 holds the tree region those samples search
+  const int per = (B + 7) >> 3;
+  const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (t >= B) return;
+  const int s = sorder[t];
+  const double sx = S[s].x, sy = S[s].y;
+  const bool ex = S[s].explore != 0;
+  const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
+  const float dl = fr.delta;
+  const float flen = (float)p.feas_len - 2.f * dl;
+  const float fl2 = flen > 0.f ? flen * flen : 0.f;
+  const float c45 = 0.69276f;  // cos(pi/4 + 0.02), rounded down (see k_nn_partial)
+  const float rho = 4.77f, rin = rho - 0.01f - 4.f * dl;
+  const float rin2 = rin > 0.f ? rin * rin : -1.f;
+  const float flen_t = (float)p.feas_len * (1.f - 1e-5f) - 4.f * dl;
+  float lk = __builtin_inff();
+  int li = 0x7fffffff;
+  float kth = __builtin_inff();
+  int idk = 0x7fffffff;
+  float lim = __builtin_inff();  // explore: (prune radius + delta)^2
+  float cb0 = -2.f;             // explore: cos of the largest heading-to-sample angle a node may have
+  int nq = 0;
+#ifdef CLRRT_WALK_PROFILE
+  const bool prof = fr.debug == 2;  // diagnostics: per-phase shader clocks into stats[4..8]
+#else
+  constexpr bool prof = false;
+#endif
+  uint64_t cyc[4] = {0, 0, 0, 0};   // super bounds, visit_super (incl.), visit4 (incl.), drain
+  int hc = -1;       // run head whose key is known ...
+  float kc = 0.f;    // ... and that key
+  unsigned long long n_sup = 0, n_tile = 0, n_q = 0, n_ex = 0;
+
+  auto refresh = [&]() {
+    kth = uni(__shfl(lk, NN_K - 1, 64));
+    idk = uni(__shfl(li, NN_K - 1, 64));
+    if (kth < __builtin_inff()) {
+      const float R = (kth + 2e-4f) * (1.0f / 0.9999f);
+      lim = uni(R < 0.f ? -1.f : (R + dl) * (R + dl));
+      const float b0 = (kth + 0.01f) * (1.f / rho) + 2e-3f;
+      cb0 = uni(b0 < 3.1f ? __cosf(b0) - 1e-4f : -2.f);  // hardware cos (abs error << 1e-4 on [0, pi])
+    }
+  };
+  // Exact keys of the queued records; feasibleNode decided in float where the float angle / length
+  // is far (> 1e-4 rad, relative 1e-5) from the limit, else in double as the reference does.  The key
+  // of the last record is remembered with its run head (records of one run share their key).
+  auto drain = [&]() {
+    if (nq == 0) return;
+    const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    n_ex += nq;
+    bool c = false;
+    float key = 0.f;
+    int id = 0, j = 0;
+    if (lane < nq) {
+      j = s_q[lane];
+      id = ID[j];
+      const NnRec& r = nodes[id];
+      key = dubins_key(sx, sy, r.x, r.y, r.c, r.s);
+      if (!ex) key = r.costE + key;
+      if (w_less(key, id, kth, idk)) {
+        const float vx = (float)(sx - r.bx), vy = (float)(sy - r.by);
+        const float dot = vx * r.ca + vy * r.sa, vv = vx * vx + vy * vy;
+        const float f2 = (float)(p.feas_len * p.feas_len);
+        // float errors: direction of v and (ca, sa) < 1e-6 rad, dot^2 / vv and vv relative < 1e-6
+        const bool yes = dot > 0.f && dot * dot >= (0.5f + 1e-5f) * vv && vv >= f2 * (1.f + 1e-5f);
+        const bool no = dot < 0.f || dot * dot < (0.5f - 1e-5f) * vv || vv < f2 * (1.f - 1e-5f);
+        c = yes;
+        if (!yes && !no) {
+          // within the float error of a limit: feasibleNode in double.  Lref exactly as the
+          // reference forms it (pow(d, 2) = d * d rounded once, IEEE sqrt); the angle test
+          // |angleDiff(atan2(v), angPar)| <= pi/4 as dot >= |cross| against (cos, sin)(angPar)
+          // (agrees with the reference's atan2 / fmod evaluation outside a ~1e-15 rad band)
+          const double dx = sx - r.bx, dy = sy - r.by;
+          const double Lref = sqrt((r.bx - sx) * (r.bx - sx) + (r.by - sy) * (r.by - sy));
+          const double2 tr = TRIG[j];
+          const double dd = dx * tr.x + dy * tr.y, cr = dy * tr.x - dx * tr.y;
+          c = (dd >= fabs(cr)) && !(Lref < p.feas_len);
+        }
+      }
+    }
+    const int jl = __shfl(j, nq - 1, 64);
+    kc = uni(__shfl(key, nq - 1, 64));
+    hc = uni(HEAD[jl]);
+    uint64_t m = __ballot(c);
+    while (m) {
+      const int l = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const float k = __shfl(key, l, 64);
+      const int i = __shfl(id, l, 64);
+      if (w_less(k, i, kth, idk)) {
+        w_insert(lk, li, k, i, lane);
+        refresh();
+      }
+    }
+    nq = 0;
+    if (prof) cyc[3] += __builtin_amdgcn_s_memtime() - c0;
+  };
+  // Necessary conditions for record j to enter the list (the brute-force prefilter + turning bound).
+  auto prefilter = [&](int id, int hd, float4 pp, float4 qq, float ce) -> bool {
+    if (hd == hc && !w_less(kc, id, kth, idk)) return false;  // key known: kc
+    const float qx = rsx - pp.x, qy = rsy - pp.y;
+    const float d2 = qx * qx + qy * qy;
+    float l2 = lim;
+    if (!ex) {
+      const float R = (kth - ce + 2e-4f) * (1.0f / 0.9999f);
+      l2 = R < 0.f ? -1.f : (R + dl) * (R + dl);
+    }
+    if (!(id >= 0 && ((d2 <= l2) || (l2 != l2)))) return false;
+    const float vx = rsx - qq.x, vy = rsy - qq.y;
+    const float dot = vx * qq.z + vy * qq.w, vv = vx * vx + vy * vy;
+    const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
+    const float tx = pp.z * qx - pp.w * qy, ty = fabsf(pp.w * qx + pp.z * qy);
+    const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
+    const bool in_bad = deep && !(ex ? (14.9f <= kth) : (ce + 14.9f <= kth));
+    bool turn_bad = false;
+    if (ex && cb0 > -1.5f) {
+      const float qn = sqrtf(d2);
+      turn_bad = tx + 4.f * dl + 1e-6f * qn < cb0 * qn;
+    }
+    return !ang_bad && !in_bad && !turn_bad;
+  };
+  auto enqueue = [&](bool ok, int j) {
+    const uint64_t m = __ballot(ok);
+    const int cnt = __popcll(m);
+    if (cnt == 0) return;
+    n_q += cnt;
+    if (nq + cnt > 64) drain();
+    if (ok) s_q[nq + __popcll(m & ((1ull << lane) - 1))] = j;
+    nq += cnt;
+    __builtin_amdgcn_wave_barrier();
+    if (nq == 64) drain();
+  };
+  // nodes of up to four tiles: t0 / t1 on lanes 0-31 / 32-63 (first set), t2 / t3 (second set);
+  // -1 = none.  Both sets' records are loaded before either is tested.
+  auto visit4 = [&](int t0, int t1, int t2, int t3) {
+    const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    n_tile += (t0 >= 0) + (t1 >= 0) + (t2 >= 0) + (t3 >= 0);
+    const int ta = lane < 32 ? t0 : t1, tb = lane < 32 ? t2 : t3;
+    const int ja = ta >= 0 ? ta * WALK_TILE + (lane & 31) : -1;
+    const int jb = tb >= 0 ? tb * WALK_TILE + (lane & 31) : -1;
+    int ida = -1, idb = -1, ha = -2, hb = -2;
+    float4 pa = make_float4(0.f, 0.f, 1.f, 0.f), qa = pa, pb = pa, qb = pa;
+    float ca = 0.f, cb = 0.f;
+    if (ja >= 0) { ida = ID[ja]; ha = HEAD[ja]; pa = P[ja]; qa = Q[ja]; ca = CE[ja]; }
+    if (jb >= 0) { idb = ID[jb]; hb = HEAD[jb]; pb = P[jb]; qb = Q[jb]; cb = CE[jb]; }
+    const bool oka = prefilter(ida, ha, pa, qa, ca);
+    const bool okb = prefilter(idb, hb, pb, qb, cb);
+    enqueue(oka, ja);
+    enqueue(okb, jb);
+    if (prof) cyc[2] += __builtin_amdgcn_s_memtime() - c0;
+  };
+  // visit the tiles of super-tile st with bounds <= min(T, kth); returns the bound of what is left
+  auto visit_super = [&](int st, float T) {
+    const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    n_sup++;
+    const uint32_t vis = s_vis[st];
+    const int tl = st * WALK_SUPER + (lane & 31);
+    float lb = __builtin_inff();
+    if (lane < 32 && tl < ntiles && !((vis >> lane) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t);
+    const bool take = lane < 32 && lb <= T && !(lb > kth);
+    const bool drop = lane < 32 && lb > kth;  // never needed again (kth only decreases)
+    uint64_t tm = __ballot(take);
+    const uint32_t nvis = vis | (uint32_t)tm | (uint32_t)__ballot(drop);
+    const float rest = wmin(take || drop || lane >= 32 ? __builtin_inff() : lb);
+    if (lane == 0) { s_vis[st] = nvis; s_lb[st] = rest; }
+    // tiles that the list has pruned since they were selected are skipped
+    auto next_tile = [&]() -> int {
+      while (tm) {
+        const int a = __ffsll((unsigned long long)tm) - 1;
+        tm &= tm - 1;
+        if (!(__shfl(lb, a, 64) > kth)) return st * WALK_SUPER + a;
+      }
+      return -1;
+    };
+    while (tm) {
+      const int t0 = next_tile();
+      const int t1 = next_tile();
+      const int t2 = next_tile();
+      const int t3 = next_tile();
+      if (t0 >= 0) visit4(t0, t1, t2, t3);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (prof) cyc[1] += __builtin_amdgcn_s_memtime() - c0;
+  };
+
+  // 1. super-tile bounds
+  const uint64_t ct0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  float mlb = __builtin_inff();
+  for (int t0 = 0; t0 < nsup; t0 += 64) {
+    const int t = t0 + lane;
+    if (t < nsup) {
+      const float lb = walk_lb(sup[t], rsx, rsy, ex, flen_t);
+      s_lb[t] = lb;
+      s_vis[t] = 0u;
+      mlb = fminf(mlb, lb);
+    }
+  }
+  mlb = wmin(mlb);
+  __builtin_amdgcn_wave_barrier();
+  if (prof) cyc[0] += __builtin_amdgcn_s_memtime() - ct0;
+  // 2. passes of growing threshold
+  const float base = mlb > 0.f && mlb < __builtin_inff() ? mlb : 0.f;
+  float T = base + 0.5f;
+  for (;;) {
+    const float lim_t = fminf(T, kth);
+    for (int t0 = 0; t0 < nsup; t0 += 64) {
+      const int t = t0 + lane;
+      const float lb = t < nsup ? s_lb[t] : __builtin_inff();
+      uint64_t m = __ballot(lb < __builtin_inff() && lb <= lim_t);
+      while (m) {
+        const int st = t0 + __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        if (s_lb[st] > kth) continue;
+        visit_super(st, T);
+      }
+    }
+    drain();
+    if (T == __builtin_inff() || kth <= T) break;
+    T = base + (T - base) * 2.f;
+    if (T > 1e7f) T = __builtin_inff();
+  }
+  // 3. output (k_nn_merge's format)
+  const bool valid = lane < NN_K && li != 0x7fffffff;
+  const int nvalid = __popcll(__ballot(valid));
+  const int sel = min(p.sort_limit, nvalid);
+  const float nk = __shfl_down(lk, 1, 64);
+  const bool tie = lane < CAND_K && lane < sel && lane + 1 < nvalid && lk == nk;
+  const bool anytie = __ballot(tie) != 0;
+  if (lane < CAND_K) {
+    cand[s * CAND_K + lane] = lane < sel ? li : -1;
+    ckey[s * CAND_K + lane] = lk;
+  }
+  if (lane == 0) {
+    ncand[s] = sel;
+    ctie[s] = anytie;
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], n_sup);
+    atomicAdd(&stats[1], n_tile);
+    atomicAdd(&stats[2], n_q);
+    atomicAdd(&stats[3], n_ex);
+    if (prof) {
+      atomicAdd(&stats[4], (unsigned long long)cyc[0]);
+      atomicAdd(&stats[5], (unsigned long long)cyc[1]);
+      atomicAdd(&stats[6], (unsigned long long)cyc[2]);
+      atomicAdd(&stats[7], (unsigned long long)cyc[3]);
+      atomicAdd(&stats[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0));
+    }
+  }
+}
+
+size_t walk_sort_bytes(int n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (const int*)nullptr, (int*)nullptr, n, 0, 64);
+  size_t b2 = 0;
+  hipcub::DeviceScan::InclusiveScan(nullptr, b2, (const int*)nullptr, (int*)nullptr, hipcub::Max(), n + 1024);
+  return bytes > b2 ? bytes : b2;
+}
+
+hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
+                          const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
+                          float* ckey, int* ncand, int* ctie, unsigned long long* stats) {
+  if (N <= 0 || B <= 0) return hipSuccess;
+  const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
+  const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
+  const double span = fmax(x1 - x0, y1 - y0);
+  const double scale = span > 0 ? 65535.0 / span : 1.0;
+  hipLaunchKernelGGL(k_walk_keys, dim3((N + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale, (uint64_t*)w.keys,
+                     w.vals);
+  LAUNCH_CHECK3();
+  size_t bytes = w.tmp_bytes;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, (uint64_t*)w.keys2, w.vals,
+                                                    w.vals2, N, 0, 64, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 255) / 256), dim3(256), 0, st, nodes, N, Npad, w.vals2, fr.ox, fr.oy,
+                     w.P, w.Q, w.CE, w.ID, w.vals, w.TRIG);
+  LAUNCH_CHECK3();
+  // HEAD[j] = first record of j's run of equal key inputs (inclusive max-scan of dup markers)
+  bytes = w.tmp_bytes;
+  e = hipcub::DeviceScan::InclusiveScan(w.tmp, bytes, w.vals, w.HEAD, hipcub::Max(), Npad, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_walk_tiles, dim3((ntiles + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
+                     fr.delta, w.tiles);
+  LAUNCH_CHECK3();
+  hipLaunchKernelGGL(k_walk_tiles, dim3((nsup + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, nsup,
+                     WALK_TILE * WALK_SUPER, fr.delta, w.supers);
+  LAUNCH_CHECK3();
+  const size_t lds = 2 * sizeof(float) * (size_t)nsup;
+  if (lds > 64 * 1024) {
+    e = hipFuncSetAttribute((const void*)&k_walk_search, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  // samples in place order (radix sort of their Morton keys; the node sort's buffers are free again)
+  hipLaunchKernelGGL(k_walk_skeys, dim3((B + 255) / 256), dim3(256), 0, st, S, B, x0, y0, scale, w.keys, w.vals);
+  LAUNCH_CHECK3();
+  bytes = w.tmp_bytes;
+  e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_walk_search, dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q, w.CE, w.ID,
+                     w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, w.TRIG, stats);
+  LAUNCH_CHECK3();
+  return hipSuccess;
+}
+
+}  // namespace clrrt

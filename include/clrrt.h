@@ -333,8 +333,10 @@ int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
  * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget, out[4]
  * samples handed to brute force by the LAST search.  Brute force: out[5] / out[6] node tiles
  * considered / searched (place-ordered strategy), out[7] (sample, node) pairs passing the float
- * prefilter, out[8] exact Dubins keys evaluated. */
-int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[10]);
+ * prefilter, out[8] exact Dubins keys evaluated.  Walk search: out[10] super-tiles visited, out[11]
+ * tiles visited, out[12] nodes passing the prefilter, out[13] exact Dubins keys evaluated, out[14..18]
+ * shader clocks per phase when the "nn_debug" option is 2 (diagnostics). */
+int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[19]);
 
 #ifdef __cplusplus
 }

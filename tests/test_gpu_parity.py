@@ -38,9 +38,11 @@ def _scene(kind):
 
 def _nn_strategy(pl, name):
     """Select the nearest-node search: 'brute' (node order), 'ordered' (place-ordered brute force with
-    tile skipping) or 'grid' (wave-uniform grid search + brute-force fallback)."""
+    tile skipping), 'grid' (wave-uniform grid search + brute-force fallback) or 'walk' (one wave per
+    sample over place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes)."""
     pl.set_nn_grid(0 if name == "grid" else 1 << 40, 3, 0)
     pl.set_option("nn_ordered_min", 0 if name == "ordered" else 1 << 40)
+    pl.set_option("nn_walk_min", 0 if name == "walk" else 1 << 40)
 
 
 def _pair(kind, seed=1, iters=40):
@@ -91,7 +93,8 @@ def test_rollout_parity(kind):
 
 
 @pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "grid"),
-                                           ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered")])
+                                           ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered"),
+                                           ("empty", "walk"), ("obb200", "walk"), ("moving", "walk")])
 def test_nearest_node_parity(kind, strategy):
     o, pl = _pair(kind, seed=4, iters=150)
     _nn_strategy(pl, strategy)
@@ -129,7 +132,8 @@ def _compare_trees(o, pl, label):
                                                       ("empty", 2, 300, "brute"), ("obb200", 5, 300, "brute"),
                                                       ("moving", 4, 250, "brute"), ("obb200", 3, 300, "grid"),
                                                       ("moving", 4, 250, "grid"), ("obb200", 5, 300, "ordered"),
-                                                      ("moving", 4, 250, "ordered")])
+                                                      ("moving", 4, 250, "ordered"), ("empty", 1, 200, "walk"),
+                                                      ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk")])
 def test_exact_mode_tree_parity(kind, seed, iters, strategy):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
@@ -167,7 +171,8 @@ def test_exact_mode_tree_parity(kind, seed, iters, strategy):
                                                              ("moving", 128, "brute", 1), ("obb200", 256, "grid", 1),
                                                              ("moving", 128, "grid", 1), ("obb200", 256, "brute", 0),
                                                              ("obb200", 256, "ordered", 1),
-                                                             ("moving", 128, "ordered", 1)])
+                                                             ("moving", 128, "ordered", 1), ("empty", 64, "walk", 1),
+                                                             ("obb200", 256, "walk", 1), ("moving", 128, "walk", 1)])
 def test_batch_mode_tree_parity(kind, batch, strategy, persistent):
     mode, obs = _scene(kind)
     iters = 4 * batch
@@ -266,8 +271,9 @@ def test_exact_mode_bitwise(kind, seed, iters):
 
 
 def test_nn_grid_matches_brute_force_large_tree():
-    """Full-size property: on a BATCH-grown tree of ~100k nodes the grid search returns exactly the
-    brute-force candidate lists (ids and keys) for every sample of a 16384-sample batch."""
+    """Full-size property: on a BATCH-grown tree of ~100k nodes the grid, place-ordered and walk
+    searches return exactly the brute-force candidate lists (ids and keys) for every sample of a
+    16384-sample batch."""
     mode, obs = _scene("obb200")
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                        max_batch=16384)
@@ -279,7 +285,7 @@ def test_nn_grid_matches_brute_force_large_tree():
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    for strategy in ("grid", "ordered"):
+    for strategy in ("grid", "ordered", "walk"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
