@@ -20,7 +20,7 @@ from .abi import (CLRRT_COLLISION_OBB, CLRRT_COLLISION_STUB, CLRRT_MODE_BATCH,  
                   CLRRT_MODE_EXACT, ROLL_NAMES)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libclrrt.so")
+LIB_PATH = os.environ.get("CLRRT_LIB") or os.path.join(PKG_DIR, "libclrrt.so")  # CLRRT_LIB: diagnostics builds
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "clrrt.h")
 
 _lib = None
@@ -68,6 +68,7 @@ _SIGS = {
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "clrrt_set_nn_grid": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
 }
 
@@ -383,6 +384,11 @@ class Planner:
                 "pairs_queued": out[7], "exact_keys": out[8], "walk_supers": out[10], "walk_tiles": out[11],
                 "walk_queued": out[12], "walk_exact": out[13], "walk_clk_bounds": out[14], "walk_clk_super": out[15],
                 "walk_clk_visit": out[16], "walk_clk_drain": out[17], "walk_clk_total": out[18]}
+
+    def debug_counters(self):
+        out = (C.c_int64 * 40)()
+        self._chk(self.L.clrrt_debug_counters(self.h, out), "debug_counters")
+        return list(out)
 
     def set_nn_grid(self, min_nodes, modes=1, wave_budget=0):
         """Trees of >= min_nodes nodes search the samples of `modes` (1 explore, 2 optimize) through

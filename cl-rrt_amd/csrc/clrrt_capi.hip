@@ -455,8 +455,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
   chk(dalloc(&c->fb_count, 1));
-  chk(dalloc(&c->work_ctr, 32));
-  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 32 * sizeof(unsigned long long)));
+  chk(dalloc(&c->work_ctr, 40));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 40 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
@@ -541,7 +541,8 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
   // 256-lane block per CU (256 VGPRs), so up to ~140 KiB of the CU's 160 KiB serve the grid
   // (launches raise hipFuncAttributeMaxDynamicSharedMemorySize accordingly)
   const size_t lds_cap = 120 * 1024;
-  const size_t lds_budget = b.size() * 36 < lds_cap ? lds_cap - b.size() * 36 : 0;
+  const size_t per_obs = 6 * 16 + 4;  // kernel LDS per obstacle: cull table + SAT geometry (roll_lds_bytes)
+  const size_t lds_budget = b.size() * per_obs < lds_cap ? lds_cap - b.size() * per_obs : 0;
   if (!stat.empty() && std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1) &&
       lds_budget >= 4 * 1024) {
     double W = x1 - x0, H = y1 - y0;
@@ -992,8 +993,18 @@ int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 32 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 40 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_debug_counters(clrrt_ctx* c, int64_t out[40]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  unsigned long long h[40];
+  HIPC(c, hipMemcpy(h, c->work_ctr, sizeof(h), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 40; i++) out[i] = (int64_t)h[i];
   return CLRRT_OK;
 }
 

@@ -364,6 +364,7 @@ struct ObsView {
   const float4* cv;                // LDS: (cx, cy, vx, vy) float
   const float* rad;                // LDS: bounding radius + vehicle radius + margin
   const float4* ob;                // LDS: box axis (ux, uy) and half extents (+ rounding slack)
+  const float4* sat;               // LDS: static obstacles' SAT vertices and normals (vx, vy, nx, ny)
   const uint32_t* gstart;          // LDS: grid cell -> first item (gw*gh + 1)
   const uint16_t* gitems;          // LDS: static obstacle ids per cell, ascending
   const uint16_t* gmov;            // LDS: moving obstacle ids, ascending
@@ -388,6 +389,15 @@ __device__ __forceinline__ bool obs_culled(const ObsView& ov, int j, float ft, f
   const float e2 = fmaxf(fabsf(dy * b.x - dx * b.y) - b.w, 0.f);
   const float vr = VEH_RAD + CULL_MARGIN;
   return e1 * e1 + e2 * e2 > vr * vr;
+}
+
+// A static obstacle's SAT from the LDS copy of its vertices / normals (no global load inside the
+// step loop: with the step's row stores in flight, a global load would wait for all of them).
+__device__ __forceinline__ float obs_sat_static(const Box4& veh, const ObsView& ov, int j) {
+  const float4 a = ov.sat[4 * j], b = ov.sat[4 * j + 1], c = ov.sat[4 * j + 2], d = ov.sat[4 * j + 3];
+  const float vx[4] = {a.x, a.y, a.z, a.w}, vy[4] = {b.x, b.y, b.z, b.w};
+  const float nx[4] = {c.x, c.y, c.z, c.w}, ny[4] = {d.x, d.y, d.z, d.w};
+  return sat_gap(veh, vx, vy, nx, ny);
 }
 
 __device__ __forceinline__ float obs_sat(const Box4& veh, const ObsView& ov, int j, double t) {
@@ -454,7 +464,7 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
           box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
           have_veh = true;
         }
-        if (obs_sat(veh, ov, j, t) == 0) { tests += j + 1; return 0.0; }
+        if (obs_sat_static(veh, ov, j) == 0) { tests += j + 1; return 0.0; }
       }
       tests += ov.n;
       return 10000;
@@ -464,7 +474,8 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       const int ja = a < ae ? (int)ov.gitems[a] : 0x7fffffff;
       const int jb = b < ov.nmov ? (int)ov.gmov[b] : 0x7fffffff;
       int j;
-      if (ja < jb) { j = ja; a++; } else { j = jb; b++; }
+      bool mv;
+      if (ja < jb) { j = ja; a++; mv = false; } else { j = jb; b++; mv = true; }
       if (obs_culled(ov, j, ft, fvx, fvy)) continue;
       if (!have_veh) {
         const float of = (float)r.x2;
@@ -472,7 +483,7 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
         box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
         have_veh = true;
       }
-      if (obs_sat(veh, ov, j, t) == 0) { tests += j + 1; return 0.0; }
+      if ((mv ? obs_sat(veh, ov, j, t) : obs_sat_static(veh, ov, j)) == 0) { tests += j + 1; return 0.0; }
     }
     tests += ov.n;  // the reference tests every obstacle until the first overlap
     return 10000;
@@ -494,15 +505,30 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
   return best;
 }
 
+// Diagnostics (built with -DCLRRT_ROLL_PROFILE only): wave time per phase of k_roll_run, from the
+// shader clock, accumulated into work counters 32..39.
+struct PhaseClk {
+  uint64_t last;
+  uint64_t t[8];
+  __device__ __forceinline__ void mark(int k) {
+#ifdef CLRRT_ROLL_PROFILE
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    t[k] += now - last;
+    last = now;
+#endif
+  }
+};
+
 // One Euler step of Simulation::propagate (simulation.cpp:58-137).  Fills the logged row columns
 // 7..9 and returns CLRRT_ROLL_* or -1 to continue.
 template <bool NEED_GAP>
 __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
-                                         double& col8, double& col9, WorkCtr& w) {
+                                         double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr) {
   double Px, Py;
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
   w.scan += (uint32_t)(r.R.N - r.wp);
   double dla = update_waypoint(r, p, Px, Py, false);
+  if (pc) pc->mark(1);
   double ym = lateral_error(r, Px, Py);
   double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
   double dc = satd(-p.dmax, p.dmax, cmd);
@@ -528,13 +554,16 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   r.x5 = r.x5 + d5 * p.dt;
   r.x6 = r.x6 + 1.0 * p.dt;
   r.x3 = satd(-p.dmax, p.dmax, r.x3);
+  if (pc) pc->mark(2);
   glibc::sincos(r.x2, r.s2, r.c2);
   r.t3 = glibc::tan(r.x3);
+  if (pc) pc->mark(3);
   col7 = (double)r.wp;
   col8 = prof_v(r.P, r.wp + 2);
   col9 = dc;
   // collision (simulation.cpp:83-86)
   double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);
+  if (pc) pc->mark(4);
   if (Dobs == 0) return CLRRT_ROLL_COLLISION;
   // costs (simulation.cpp:89-95)
   r.costE += r.x4 * p.dt;
@@ -638,7 +667,8 @@ template <bool NEED_GAP>
 __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* lds) {
   float4* cv = lds;
   float4* ob = lds + a.p.n_obs;
-  float* rad = (float*)(ob + a.p.n_obs);
+  float4* sat = ob + a.p.n_obs;
+  float* rad = (float*)(sat + 4 * a.p.n_obs);
   uint32_t* gstart = (uint32_t*)(rad + a.p.n_obs);
   const int ncell = a.grid.gw * a.grid.gh;
   uint16_t* gitems = (uint16_t*)(gstart + (a.grid.gw > 0 ? ncell + 1 : 0));
@@ -652,6 +682,10 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
       const float hh = sqrtf(o.P * o.P + o.R * o.R), ww = sqrtf(o.Q * o.Q + o.S * o.S);
       const float ux = hh > 0.f ? o.P / hh : 1.f, uy = hh > 0.f ? o.R / hh : 0.f;
       ob[j] = make_float4(ux, uy, hh * 1.00001f + 1e-4f, ww * 1.00001f + 1e-4f);
+      sat[4 * j] = make_float4(o.vx[0], o.vx[1], o.vx[2], o.vx[3]);
+      sat[4 * j + 1] = make_float4(o.vy[0], o.vy[1], o.vy[2], o.vy[3]);
+      sat[4 * j + 2] = make_float4(o.nx[0], o.nx[1], o.nx[2], o.nx[3]);
+      sat[4 * j + 3] = make_float4(o.ny[0], o.ny[1], o.ny[2], o.ny[3]);
     }
     if (a.grid.gw > 0) {
       for (int j = threadIdx.x; j <= ncell; j += blockDim.x) gstart[j] = a.grid.start[j];
@@ -660,7 +694,7 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
     }
     __syncthreads();
   }
-  return ObsView{a.obs, cv, rad, ob, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
+  return ObsView{a.obs, cv, rad, ob, sat, gstart, gitems, gmov, a.p.coll_mode == CLRRT_COLLISION_OBB ? a.p.n_obs : 0,
                  a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
 }
 
@@ -808,75 +842,102 @@ __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __
   double c7 = 0, c8 = 0, c9 = 0;
   int j = -1, k = 0, s = 0, pass = 0, steps = 0;
   bool exhausted = false;
+  PhaseClk pclk{};
+#ifdef CLRRT_ROLL_PROFILE
+  PhaseClk* pc = &pclk;
+  pclk.last = __builtin_amdgcn_s_memtime();
+#else
+  PhaseClk* pc = nullptr;
+#endif
+  int fin = -1;  // >= 0: the lane's rollout ended with this outcome; finished in the next batch
   for (;;) {
-    const bool idle = j < 0 && !exhausted;
-    const uint64_t m = __ballot(idle);
-    const uint64_t busy = __ballot(j >= 0);
-    if (m && (__popcll(m) >= REFILL_MIN || busy == 0)) {
-      // wave-aggregated fetch: the idle lanes take consecutive queue positions
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      int base = 0;
-      if (lane == leader) base = atomicAdd(qnext, __popcll(m));
-      base = __shfl(base, leader, 64);
-      if (idle) {
-        const int q = base + __popcll(m & ((1ull << lane) - 1));
-        if (q >= a.njobs) {
-          exhausted = true;
+    if (pc) pc->mark(0);
+    // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
+    // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
+    // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
+    // every step for one or two lanes.
+    const uint64_t parked = __ballot(fin >= 0);
+    const uint64_t m0 = __ballot(j < 0 && !exhausted);
+    const uint64_t busy0 = __ballot(j >= 0 && fin < 0);
+    if ((parked | m0) && (__popcll(parked | m0) >= REFILL_MIN || busy0 == 0)) {
+      if (fin >= 0) {
+        RollRes out;
+        finish_rollout(r, c7, c8, c9, fin, steps, out);
+        if (pass == 1) {
+          a.res_gb[j] = out;
+          j = -1;
         } else {
-          k = q / B;
-          s = q - k * B;
-          j = s * CAND_K + k;
-          if (!prep[j].valid || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
-            a.res[j].outcome = -1;
+          a.res[j] = out;
+          const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
+          if (ok) atomicMin(&best[s], k);
+          if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
+            // goal-biased rollout from the node this rollout would append (expandTree :163-173)
+            const RefD R = make_goal_ref(out.bx, out.by, a.p);
+            roll_init(r, out.st, R, out.vback, true, a.p);
+            c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
+            pass = 1;
+            steps = 0;
+            double* rows = a.slots + pass_stride + j * slot;
+#pragma unroll
+            for (int q = 0; q < 10; q++) rows[q] = out.st[q];
+            rows[7] = c7;
+          } else {
             a.res_gb[j].outcome = -1;
             j = -1;
+          }
+        }
+        fin = -1;
+      }
+      if (pc) pc->mark(7);
+      const bool idle = j < 0 && !exhausted;
+      const uint64_t m = __ballot(idle);
+      if (m) {
+        // wave-aggregated fetch: the idle lanes take consecutive queue positions
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(qnext, __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (idle) {
+          const int q = base + __popcll(m & ((1ull << lane) - 1));
+          if (q >= a.njobs) {
+            exhausted = true;
           } else {
-            r = prep[j].r;
-            c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
-            pass = 0;
-            steps = 0;
+            k = q / B;
+            s = q - k * B;
+            j = s * CAND_K + k;
+            if (!prep[j].valid || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+              a.res[j].outcome = -1;
+              a.res_gb[j].outcome = -1;
+              j = -1;
+            } else {
+              r = prep[j].r;
+              c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
+              pass = 0;
+              steps = 0;
+            }
           }
         }
       }
+      if (pc) pc->mark(6);
       continue;
     }
-    if (busy == 0) {
+    if (busy0 == 0) {
       if (__ballot(!exhausted) == 0) break;
       continue;
     }
-    if (j < 0) continue;
+    if (j < 0 || fin >= 0) continue;
     steps++;
-    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w);
+    if (pc) pc->mark(6);
+    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
     w.steps++;
+#ifndef CLRRT_NO_ROWS
     store_row(a.slots + pass * pass_stride + j * slot + (int64_t)steps * 10, 1, r, c7, c8, c9);
+#endif
+    if (pc) pc->mark(5);
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
-      RollRes out;
-      finish_rollout(r, c7, c8, c9, o, steps, out);
-      if (pass == 1) {
-        a.res_gb[j] = out;
-        j = -1;
-        continue;
-      }
-      a.res[j] = out;
-      const bool ok = o == CLRRT_ROLL_END || o == CLRRT_ROLL_GOAL;
-      if (ok) atomicMin(&best[s], k);
-      if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
-        // goal-biased rollout from the node this rollout would append (expandTree :163-173)
-        const RefD R = make_goal_ref(out.bx, out.by, a.p);
-        roll_init(r, out.st, R, out.vback, true, a.p);
-        c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
-        pass = 1;
-        steps = 0;
-        double* rows = a.slots + pass_stride + j * slot;
-#pragma unroll
-        for (int q = 0; q < 10; q++) rows[q] = out.st[q];
-        rows[7] = c7;
-      } else {
-        a.res_gb[j].outcome = -1;
-        j = -1;
-      }
-    } else if ((steps & 7) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+      fin = o;
+    } else if ((steps & 15) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
       // an earlier candidate of this sample succeeded: this result will not be looked at
       if (pass == 0) a.res[j].outcome = -1;
       a.res_gb[j].outcome = -1;
@@ -895,6 +956,10 @@ __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __
     __syncthreads();
     if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
   }
+#ifdef CLRRT_ROLL_PROFILE
+  if (a.ctr && lane == 0)
+    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[32 + q], (unsigned long long)pclk.t[q]);
+#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1264,7 +1329,7 @@ __global__ void __launch_bounds__(256) k_tree_reinit(ReinitArgs a) {
   __shared__ long long s_rows;
   const int tid = threadIdx.x;
   const DevParams& p = a.p;
-  const ObsView ov{a.obs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+  const ObsView ov{a.obs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                    p.coll_mode == CLRRT_COLLISION_OBB ? p.n_obs : 0, 0, 0, 0, 0.f, 0.f, 0.f};
   int* goal = a.kidx + a.n;
   // :51-57 erase(it--) over the path = keep the nodes whose last row has x >= 0 (or NaN)
@@ -1594,7 +1659,7 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
 static size_t roll_lds_bytes(const RollArgs& a) {
   size_t lds = 0;
   if (a.p.coll_mode == CLRRT_COLLISION_OBB) {
-    lds = (size_t)a.p.n_obs * (2 * sizeof(float4) + sizeof(float));
+    lds = (size_t)a.p.n_obs * (6 * sizeof(float4) + sizeof(float));
     if (a.grid.gw > 0)
       lds += sizeof(uint32_t) * ((size_t)a.grid.gw * a.grid.gh + 1) +
              sizeof(uint16_t) * ((size_t)a.grid.nitems + a.grid.nmov);

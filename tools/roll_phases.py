@@ -1,0 +1,23 @@
+"""Per-phase wave time of the rollout kernel (build: make -C cl-rrt_amd/csrc prof; run with
+CLRRT_LIB=build/prof/libclrrt.so): cfg3 scene, BATCH expansion for `ms`."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
+import clrrt
+from clrrt import abi, scenes
+
+ms = float(sys.argv[1]) if len(sys.argv) > 1 else 1000.0
+pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=4 << 20,
+                   max_rows=1 << 26, max_batch=16384)
+pl.set_obstacles(scenes.urban_scene(200))
+pl.tree_init()
+pl.enable_timing(True)
+st = pl.expand(clrrt.Rng(5), n_iters=0, budget_ms=ms, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+d = pl.debug_counters()
+names = ["loop / abandon", "waypoint (cos, sin, scan)", "lateral error + control + ODE", "sincos + tan",
+         "collision", "costs / end checks + row store", "refill", "batched finish + goal-bias init"]
+ph = d[32:40]
+tot = sum(ph)
+print(f"nodes {pl.size()[0]} rounds {st['rounds']} steps {d[0]} rollout ms {pl.kernel_time(1)} nn ms {pl.kernel_time(0)}")
+for nm, v in zip(names, ph):
+    print(f"  {nm:32s} {v / max(1, tot) * 100:5.1f}%  {v / max(1, d[0]):8.1f} clk/step")
