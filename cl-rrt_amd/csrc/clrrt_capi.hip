@@ -1353,6 +1353,17 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
     int L = nb, nn = 0;
     if ((rc = eval_samples(c, nb, exact, &L)) != CLRRT_OK) break;
+    if (!exact) {
+      // BATCH rounds commit every sample, so the next round's samples are known now: draw them
+      // while the GPU evaluates this round (the draw is ~0.05 us per sample on the host)
+      int64_t want = nb + (int64_t)cur;
+      if (n_iters > 0) want = std::min<int64_t>(want, n_iters - st.iterations);
+      while ((int64_t)pending.size() < want) {
+        clrrt_sample smp;
+        clrrt_draw_samples(&c->params, &work, 1, &smp);
+        pending.push_back(smp);
+      }
+    }
     if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     for (int j = 0; j < L; j++) {

@@ -528,6 +528,15 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
   w.scan += (uint32_t)(r.R.N - r.wp);
   double dla = update_waypoint(r, p, Px, Py, false);
+#ifdef CLRRT_DUP_WP
+  {
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    const double Pxb = r.x0 + z + dla * 1.0 * glibc::cos(r.x2 + z);
+    const double Pyb = r.x1 + z + dla * 1.0 * glibc::sin(r.x2 + z);
+    Px = fmin(Px, Pxb); Py = fmin(Py, Pyb);
+  }
+#endif
   if (pc) pc->mark(1);
   double ym = lateral_error(r, Px, Py);
   double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
@@ -557,12 +566,32 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   if (pc) pc->mark(2);
   glibc::sincos(r.x2, r.s2, r.c2);
   r.t3 = glibc::tan(r.x3);
+#ifdef CLRRT_DUP_TRIG  // diagnostics: the phase evaluated twice (same values) to measure its cost
+  {
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    double s2b, c2b;
+    glibc::sincos(r.x2 + z, s2b, c2b);
+    const double t3b = glibc::tan(r.x3 + z);
+    r.s2 = fmin(r.s2, s2b); r.c2 = fmin(r.c2, c2b); r.t3 = fmin(r.t3, t3b);
+  }
+#endif
   if (pc) pc->mark(3);
   col7 = (double)r.wp;
   col8 = prof_v(r.P, r.wp + 2);
   col9 = dc;
   // collision (simulation.cpp:83-86)
   double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);
+#ifdef CLRRT_DUP_COLL
+  {
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    Roll r2 = r;
+    r2.x0 += z;
+    uint32_t tb = 0;
+    Dobs = fmin(Dobs, obs_distance<NEED_GAP>(r2, p, ov, tb));
+  }
+#endif
   if (pc) pc->mark(4);
   if (Dobs == 0) return CLRRT_ROLL_COLLISION;
   // costs (simulation.cpp:89-95)
@@ -826,7 +855,9 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
   rows[7] = ini.c7;
 }
 
-#define REFILL_MIN 8
+#ifndef REFILL_MIN
+#define REFILL_MIN 16
+#endif
 
 template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,

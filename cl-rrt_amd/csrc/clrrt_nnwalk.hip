@@ -286,7 +286,10 @@ __device__ __forceinline__ void w_insert(float& lk, int& li, float k, int i, int
 // of 32 nodes per step (lanes 0-31 / 32-63), so nodes are visited roughly in the order of their
 // bounds and the list's 11th key prunes the rest.  The search ends after the first pass whose
 // threshold reaches kth: every tile with a bound <= kth has then been visited.
-__global__ void __launch_bounds__(64) k_walk_search(const clrrt_sample* __restrict__ S, int B,
+#ifndef CLRRT_WALK_WAVES
+#define CLRRT_WALK_WAVES 4
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_WALK_WAVES))) k_walk_search(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                     const float4* __restrict__ Q, const float* __restrict__ CE,
                                                     const int* __restrict__ ID, const int* __restrict__ HEAD,
