@@ -419,9 +419,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
     const bool in_bad = deep && !(ex ? (14.9f <= kth) : (ce + 14.9f <= kth));
     bool turn_bad = false;
-    if (ex && cb0 > -1.5f) {
-      const float qn = sqrtf(d2);
-      turn_bad = tx + 4.f * dl + 1e-6f * qn < cb0 * qn;
+    if (ex) {
+      if (cb0 > -1.5f) {
+        const float qn = sqrtf(d2);
+        turn_bad = tx + 4.f * dl + 1e-6f * qn < cb0 * qn;
+      }
+    } else if (kth < __builtin_inff()) {
+      // optimize: costE + key <= kth needs rho * beta <= kth - costE (+ margin)
+      const float b0 = (kth - ce + 0.01f) * (1.f / rho) + 2e-3f;
+      if (b0 < 3.1f) {
+        const float cb = __cosf(b0) - 1e-4f;
+        const float qn = sqrtf(d2);
+        turn_bad = tx + 4.f * dl + 1e-6f * qn < cb * qn;
+      }
     }
     return !ang_bad && !in_bad && !turn_bad;
   };
@@ -506,7 +516,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   if (prof) cyc[0] += __builtin_amdgcn_s_memtime() - ct0;
   // 2. passes of growing threshold
   const float base = mlb > 0.f && mlb < __builtin_inff() ? mlb : 0.f;
-  float T = base + 0.5f;
+#ifndef WALK_T0
+#define WALK_T0 0.5f
+#endif
+#ifndef WALK_GROW
+#define WALK_GROW 2.f
+#endif
+  float T = base + WALK_T0;
   for (;;) {
     const float lim_t = fminf(T, kth);
     for (int t0 = 0; t0 < nsup; t0 += 64) {
@@ -522,7 +538,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     }
     drain();
     if (T == __builtin_inff() || kth <= T) break;
-    T = base + (T - base) * 2.f;
+    T = base + (T - base) * WALK_GROW;
     if (T > 1e7f) T = __builtin_inff();
   }
   // 3. output (k_nn_merge's format)
