@@ -94,6 +94,7 @@ struct clrrt_ctx {
   int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
   WalkBufs nnw{};                      // allocated on first use
+  CompactBufs cmp{};                   // round compaction scratch
   int nng_modes = 1;
   int nng_budget = 0;
   // persistent rollouts (k_roll_prep + k_roll_run)
@@ -362,7 +363,8 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
-                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG};
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->cmp.packed, c->cmp.scanned,
+                  c->cmp.tmp};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -425,6 +427,10 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->out_nodes, 2 * B));
   chk(dalloc(&c->jobs, 2 * B));
   chk(dalloc(&c->totals, 8));
+  chk(dalloc(&c->cmp.packed, B));
+  chk(dalloc(&c->cmp.scanned, B));
+  c->cmp.tmp_bytes = compact_scan_bytes((int)B);
+  chk(hipMalloc(&c->cmp.tmp, std::max<size_t>(c->cmp.tmp_bytes, 256)));
   chk(dalloc(&c->nng.cellid, c->cap.max_nodes));
   chk(dalloc(&c->nng.sorted, c->cap.max_nodes));
   chk(dalloc(&c->nng.count, kNngMaxCells + 2));
@@ -1239,7 +1245,7 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   {
     KTimer kt(c, 2);
     HIPC(c, launch_compact(st, L, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
-                           c->out_nodes, c->jobs, c->totals));
+                           c->out_nodes, c->jobs, c->totals, c->cmp));
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
   }
   HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));

@@ -203,9 +203,17 @@ hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* r
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                            const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
                            int* first);
+// Scratch of the multi-block compaction (k_compact_count / hipcub scan / k_compact_scatter).
+struct CompactBufs {
+  uint64_t* packed;   // [max_batch] per-sample (rows << 24 | nodes)
+  uint64_t* scanned;  // [max_batch] exclusive prefix sums
+  void* tmp;
+  size_t tmp_bytes;
+};
+size_t compact_scan_bytes(int n);
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
-                          clrrt_node* out, Job* jobs, int64_t* totals);
+                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb);
 // Bounding box (x0, y0, x1, y1) of the finite positions of recs[0 .. n), n = *n_dev when non-null.
 hipError_t launch_bbox(hipStream_t st, const clrrt_node* recs, const int64_t* n_dev, int n_host, double* out4);
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn);

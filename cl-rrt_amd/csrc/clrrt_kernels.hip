@@ -13,6 +13,7 @@
 //                               replay jobs (wave ballot / block scan)
 //   k_append                  : RRT.addNode for a batch of records (rrtplanner.h:111-113)
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
 #include "clrrt_dev.hpp"
@@ -1093,75 +1094,78 @@ __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ 
 // --------------------------------------------------------------------------------------------
 // compaction of committed samples (one block, sequential chunks + block scan)
 // --------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_compact(int L, const clrrt_sample* __restrict__ S,
-                                                  const int* __restrict__ cand,
-                                                  const clrrt_node* __restrict__ regnodes,
-                                                  const clrrt_node* __restrict__ gbnodes,
-                                                  const SampleOut* __restrict__ so, int64_t row_base,
-                                                  int rank, clrrt_node* __restrict__ out, Job* __restrict__ jobs,
-                                                  int64_t* __restrict__ totals) {
-  __shared__ int64_t s_nodes[1024], s_rows[1024];
-  __shared__ int64_t s_cnt[8];
-  const int t = threadIdx.x;
-  const int per = (L + blockDim.x - 1) / blockDim.x;
-  const int b0 = min(L, t * per), b1 = min(L, b0 + per);
-  int64_t nn = 0, nr = 0;
-  int64_t cnt[6] = {0, 0, 0, 0, 0, 0};
-  for (int s = b0; s < b1; s++) {
+// Compaction of committed samples in three passes: per-sample counts (nodes in the low 24 bits, rows
+// above them; a round has < 2^24 nodes and < 2^40 rows), a device-wide exclusive scan (hipcub), and a
+// scatter of the node records and row-copy jobs.  The round's work counters are block-reduced.
+__global__ void __launch_bounds__(256) k_compact_count(int L, const SampleOut* __restrict__ so,
+                                                       const clrrt_node* __restrict__ regnodes,
+                                                       const clrrt_node* __restrict__ gbnodes,
+                                                       uint64_t* __restrict__ packed, int64_t* __restrict__ totals) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cnt[6] = {0, 0, 0, 0, 0, 0};
+  if (s < L) {
     const SampleOut& o = so[s];
-    if (o.k >= 0) { nn++; nr += o.nrows_reg; cnt[5] += regnodes[s].goal; }
-    if (o.gb_ok) { nn++; nr += o.nrows_gb; cnt[5] += gbnodes[s].goal; }
-    cnt[0] += o.steps; cnt[1] += o.f_col; cnt[2] += o.f_acc; cnt[3] += o.f_it; cnt[4] += o.rollouts;
+    uint64_t nn = 0, nr = 0;
+    if (o.k >= 0) { nn++; nr += (uint64_t)o.nrows_reg; cnt[5] += regnodes[s].goal; }
+    if (o.gb_ok) { nn++; nr += (uint64_t)o.nrows_gb; cnt[5] += gbnodes[s].goal; }
+    cnt[0] = o.steps; cnt[1] = o.f_col; cnt[2] = o.f_acc; cnt[3] = o.f_it; cnt[4] = o.rollouts;
+    packed[s] = (nr << 24) | nn;
   }
-  s_nodes[t] = nn;
-  s_rows[t] = nr;
-  if (t < 8) s_cnt[t] = 0;
+  __shared__ unsigned long long s_cnt[6];
+  if (threadIdx.x < 6) s_cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-    int64_t vn = t >= off ? s_nodes[t - off] : 0;
-    int64_t vr = t >= off ? s_rows[t - off] : 0;
-    __syncthreads();
-    s_nodes[t] += vn;
-    s_rows[t] += vr;
-    __syncthreads();
-  }
-  for (int c = 0; c < 6; c++) atomicAdd((unsigned long long*)&s_cnt[c], (unsigned long long)cnt[c]);
-  int64_t node_off = s_nodes[t] - nn, row_off = s_rows[t] - nr;
-  for (int s = b0; s < b1; s++) {
-    const SampleOut& o = so[s];
-    if (o.k >= 0) {
-      clrrt_node n = regnodes[s];
-      n.owner = rank;
-      n.row_offset = row_base + row_off;
-      out[node_off] = n;
-      Job jb;  // row copy: slot of job (s, k*) pass 0 -> arena
-      jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 0; jb.pad = 0;
-      jb.sx = 0; jb.sy = 0;
-      jb.row_off = row_base + row_off;
-      jobs[node_off] = jb;
-      node_off++;
-      row_off += o.nrows_reg;
-    }
-    if (o.gb_ok) {
-      clrrt_node n = gbnodes[s];
-      n.owner = rank;
-      n.row_offset = row_base + row_off;
-      out[node_off] = n;
-      Job jb;  // row copy: slot of job (s, k*) pass 1 (goal-biased rollout) -> arena
-      jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 1; jb.pad = 0;
-      jb.sx = 0; jb.sy = 0;
-      jb.row_off = row_base + row_off;
-      jobs[node_off] = jb;
-      node_off++;
-      row_off += o.nrows_gb;
-    }
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    unsigned long long v = cnt[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_cnt[c], v);
   }
   __syncthreads();
-  if (t == blockDim.x - 1) {
-    totals[0] = s_nodes[t];
-    totals[1] = s_rows[t];
+  if (threadIdx.x < 6 && s_cnt[threadIdx.x]) atomicAdd((unsigned long long*)&totals[2 + threadIdx.x], s_cnt[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut* __restrict__ so,
+                                                         const clrrt_node* __restrict__ regnodes,
+                                                         const clrrt_node* __restrict__ gbnodes,
+                                                         const uint64_t* __restrict__ packed,
+                                                         const uint64_t* __restrict__ scanned, int64_t row_base,
+                                                         int rank, clrrt_node* __restrict__ out, Job* __restrict__ jobs,
+                                                         int64_t* __restrict__ totals) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= L) return;
+  const uint64_t off = scanned[s];
+  int64_t node_off = (int64_t)(off & 0xffffffu), row_off = (int64_t)(off >> 24);
+  if (s == L - 1) {
+    const uint64_t tot = off + packed[s];
+    totals[0] = (int64_t)(tot & 0xffffffu);
+    totals[1] = (int64_t)(tot >> 24);
   }
-  if (t < 6) totals[2 + t] = s_cnt[t];
+  const SampleOut& o = so[s];
+  if (o.k >= 0) {
+    clrrt_node n = regnodes[s];
+    n.owner = rank;
+    n.row_offset = row_base + row_off;
+    out[node_off] = n;
+    Job jb;  // row copy: slot of job (s, k*) pass 0 -> arena
+    jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 0; jb.pad = 0;
+    jb.sx = 0; jb.sy = 0;
+    jb.row_off = row_base + row_off;
+    jobs[node_off] = jb;
+    node_off++;
+    row_off += o.nrows_reg;
+  }
+  if (o.gb_ok) {
+    clrrt_node n = gbnodes[s];
+    n.owner = rank;
+    n.row_offset = row_base + row_off;
+    out[node_off] = n;
+    Job jb;  // row copy: slot of job (s, k*) pass 1 (goal-biased rollout) -> arena
+    jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 1; jb.pad = 0;
+    jb.sx = 0; jb.sy = 0;
+    jb.row_off = row_base + row_off;
+    jobs[node_off] = jb;
+  }
 }
 
 // Move committed trajectories (Node::tra) from their job slots into the arena: one block per node.
@@ -1774,11 +1778,25 @@ hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrr
   return hipSuccess;
 }
 
+size_t compact_scan_bytes(int n) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, n);
+  return bytes;
+}
+
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
-                          clrrt_node* out, Job* jobs, int64_t* totals) {
-  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, st, L, S, cand, reg, gbn, so, row_base, rank, out, jobs,
-                     totals);
+                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb) {
+  hipError_t e = hipMemsetAsync(totals, 0, sizeof(int64_t) * 8, st);
+  if (e != hipSuccess) return e;
+  if (L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_compact_count, dim3((L + 255) / 256), dim3(256), 0, st, L, so, reg, gbn, cb.packed, totals);
+  LAUNCH_CHECK();
+  size_t bytes = cb.tmp_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(cb.tmp, bytes, cb.packed, cb.scanned, L, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_compact_scatter, dim3((L + 255) / 256), dim3(256), 0, st, L, so, reg, gbn, cb.packed, cb.scanned,
+                     row_base, rank, out, jobs, totals);
   LAUNCH_CHECK();
   return hipSuccess;
 }

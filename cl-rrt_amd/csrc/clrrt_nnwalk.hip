@@ -221,10 +221,16 @@ __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P
   if (lane == 0) out[t] = w;
 }
 
+// Bounds need no correctly rounded division / square root (the build flag makes '/' and sqrtf
+// correctly rounded for the exact keys): hardware reciprocal and square root, ~1 ulp, far inside the
+// bounds' margins.
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 // acos on [-1, 1] (Abramowitz & Stegun 4.4.45), |error| <= 7e-5 rad (float evaluation included).
 __device__ __forceinline__ float acos_apx(float x) {
   const float ax = fminf(fabsf(x), 1.f);
-  const float r = sqrtf(1.f - ax) * (1.5707288f + ax * (-0.2121144f + ax * (0.0742610f + ax * -0.0187293f)));
+  const float r = fsqrt(1.f - ax) * (1.5707288f + ax * (-0.2121144f + ax * (0.0742610f + ax * -0.0187293f)));
   return x < 0.f ? 3.14159265f - r : r;
 }
 
@@ -238,19 +244,21 @@ __device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy
   const float rho = 4.77f;
   // feasibility: direction from the ref.back() disc to the sample vs the ang_par arc
   const float ex2 = rsx - w.rcx, ey2 = rsy - w.rcy;
-  const float E2 = sqrtf(ex2 * ex2 + ey2 * ey2);
+  const float E2 = fsqrt(ex2 * ex2 + ey2 * ey2);
   if (E2 + w.rr < flen) return __builtin_inff();
   if (E2 > w.rr && w.aph < 3.f) {
-    const float a2 = 1.57079633f - acos_apx(w.rr / E2);  // asin
-    const float ang2 = acos_apx((ex2 * w.apx + ey2 * w.apy) / E2);
+    const float iE = frcp(E2);
+    const float a2 = 1.57079633f - acos_apx(w.rr * iE);  // asin
+    const float ang2 = acos_apx((ex2 * w.apx + ey2 * w.apy) * iE);
     if (ang2 - a2 - w.aph > 0.78539816f + 5e-3f) return __builtin_inff();
   }
   const float dx = rsx - w.pcx, dy = rsy - w.pcy;
-  const float D = sqrtf(dx * dx + dy * dy);
+  const float D = fsqrt(dx * dx + dy * dy);
   float lb = D - w.pr;
   if (D > w.pr && w.thh < 3.f) {
-    const float al = 1.57079633f - acos_apx(w.pr / D);
-    const float bmin = acos_apx((dx * w.thx + dy * w.thy) / D) - al - w.thh - 3e-3f;
+    const float iD = frcp(D);
+    const float al = 1.57079633f - acos_apx(w.pr * iD);
+    const float bmin = acos_apx((dx * w.thx + dy * w.thy) * iD) - al - w.thh - 3e-3f;
     lb = fmaxf(lb, rho * bmin);
   }
   lb = lb - 2e-3f - 1e-5f * fabsf(lb);
@@ -421,7 +429,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     bool turn_bad = false;
     if (ex) {
       if (cb0 > -1.5f) {
-        const float qn = sqrtf(d2);
+        const float qn = fsqrt(d2);
         turn_bad = tx + 4.f * dl + 1e-6f * qn < cb0 * qn;
       }
     } else if (kth < __builtin_inff()) {
@@ -429,7 +437,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       const float b0 = (kth - ce + 0.01f) * (1.f / rho) + 2e-3f;
       if (b0 < 3.1f) {
         const float cb = __cosf(b0) - 1e-4f;
-        const float qn = sqrtf(d2);
+        const float qn = fsqrt(d2);
         turn_bad = tx + 4.f * dl + 1e-6f * qn < cb * qn;
       }
     }
