@@ -93,6 +93,7 @@ struct clrrt_ctx {
   int64_t nng_min_nodes = INT64_MAX;  // clrrt_set_nn_grid: off by default (brute force is faster on bench trees)
   int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
+  bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
   WalkBufs nnw{};                      // allocated on first use
   CompactBufs cmp{};                   // round compaction scratch
   int nng_modes = 1;
@@ -546,7 +547,10 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
   // dynamic LDS of the rollout kernels (36 B per obstacle + grid): the rollout kernels run one
   // 256-lane block per CU (256 VGPRs), so up to ~140 KiB of the CU's 160 KiB serve the grid
   // (launches raise hipFuncAttributeMaxDynamicSharedMemorySize accordingly)
-  const size_t lds_cap = 120 * 1024;
+#ifndef CLRRT_OBS_LDS_KB
+#define CLRRT_OBS_LDS_KB 120
+#endif
+  const size_t lds_cap = CLRRT_OBS_LDS_KB * 1024;
   const size_t per_obs = 6 * 16 + 4;  // kernel LDS per obstacle: cull table + SAT geometry (roll_lds_bytes)
   const size_t lds_budget = b.size() * per_obs < lds_cap ? lds_cap - b.size() * per_obs : 0;
   if (!stat.empty() && std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1) &&
@@ -1041,6 +1045,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   if (k == "roll_persistent") c->roll_persistent = value != 0;
   else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
   else if (k == "nn_walk_min" && value >= 0) c->nnw_min_nodes = value;
+  else if (k == "nn_walk_stateless") c->nnw_stateless = value != 0;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
@@ -1157,7 +1162,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     int rc = ensure_walk(c);
     if (rc != CLRRT_OK) return rc;
     HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, fr, x0, y0, x1, y1, c->nnw, c->cand,
-                           c->ckey, c->ncand, c->ctie, c->work_ctr + 18));
+                           c->ckey, c->ncand, c->ctie, c->work_ctr + 18, c->nnw_stateless));
     if (scratch) HIPC(c, launch_nn_exact_only(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->ctie, scratch,
                                               c->cand, c->ckey, c->ncand));
     return CLRRT_OK;

@@ -175,7 +175,7 @@ size_t walk_sort_bytes(int n);
 // (x0, y0, x1, y1) = box holding every finite node position (the Morton frame).
 hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
                           const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
-                          float* ckey, int* ncand, int* ctie, unsigned long long* stats);
+                          float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless);
 // Brute-force candidate lists of the samples fb_list[0 .. *fb_count) (the walk search's hand-offs).
 hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,

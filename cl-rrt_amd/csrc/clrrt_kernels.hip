@@ -861,7 +861,10 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
 #endif
 
 template <bool NEED_GAP>
-__global__ void __launch_bounds__(256) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
+#ifndef CLRRT_ROLL_WAVES
+#define CLRRT_ROLL_WAVES 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLL_WAVES))) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
                                                   int* __restrict__ qnext, int* __restrict__ best, int B) {
   extern __shared__ float4 lds[];
   glibc::stage_tables();

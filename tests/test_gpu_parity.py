@@ -42,7 +42,8 @@ def _nn_strategy(pl, name):
     sample over place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes)."""
     pl.set_nn_grid(0 if name == "grid" else 1 << 40, 3, 0)
     pl.set_option("nn_ordered_min", 0 if name == "ordered" else 1 << 40)
-    pl.set_option("nn_walk_min", 0 if name == "walk" else 1 << 40)
+    pl.set_option("nn_walk_min", 0 if name in ("walk", "walk_stateless") else 1 << 40)
+    pl.set_option("nn_walk_stateless", name == "walk_stateless")
 
 
 def _pair(kind, seed=1, iters=40):
@@ -94,7 +95,8 @@ def test_rollout_parity(kind):
 
 @pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "grid"),
                                            ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered"),
-                                           ("empty", "walk"), ("obb200", "walk"), ("moving", "walk")])
+                                           ("empty", "walk"), ("obb200", "walk"), ("moving", "walk"),
+                                           ("obb200", "walk_stateless")])
 def test_nearest_node_parity(kind, strategy):
     o, pl = _pair(kind, seed=4, iters=150)
     _nn_strategy(pl, strategy)
@@ -133,7 +135,8 @@ def _compare_trees(o, pl, label):
                                                       ("moving", 4, 250, "brute"), ("obb200", 3, 300, "grid"),
                                                       ("moving", 4, 250, "grid"), ("obb200", 5, 300, "ordered"),
                                                       ("moving", 4, 250, "ordered"), ("empty", 1, 200, "walk"),
-                                                      ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk")])
+                                                      ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk"),
+                                                      ("obb200", 5, 300, "walk_stateless")])
 def test_exact_mode_tree_parity(kind, seed, iters, strategy):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
@@ -285,7 +288,7 @@ def test_nn_grid_matches_brute_force_large_tree():
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    for strategy in ("grid", "ordered", "walk"):
+    for strategy in ("grid", "ordered", "walk", "walk_stateless"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
