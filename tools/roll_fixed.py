@@ -10,11 +10,12 @@ from clrrt import abi, scenes
 
 ms = float(sys.argv[1]) if len(sys.argv) > 1 else 1000.0
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=4 << 20,
-                   max_rows=1 << 26, max_batch=16384)
+pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=8 << 20,
+                   max_rows=1 << 28, max_batch=16384)
 pl.set_obstacles(scenes.urban_scene(200))
 pl.tree_init()
-pl.expand(clrrt.Rng(5), n_iters=0, budget_ms=ms, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+st = pl.expand(clrrt.Rng(5), n_iters=0, budget_ms=ms, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+print("grown:", st, flush=True)
 smp = list(clrrt.Rng(77).draw_samples(pl.params, 16384))
 arr = (abi.Sample * len(smp))(*smp)
 out = torch.empty(2 * len(smp) * C_NODE if (C_NODE := 160) else 0, dtype=torch.uint8, device="cuda")
