@@ -540,6 +540,23 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
 #endif
   if (pc) pc->mark(1);
   double ym = lateral_error(r, Px, Py);
+#ifdef CLRRT_DUP_LAT
+  {
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    ym = fmin(ym, lateral_error(r, Px + z, Py));
+  }
+#endif
+#ifdef CLRRT_DUP_SCAN
+  {
+    double z = 0.0;
+    asm volatile("" : "+v"(z));
+    Roll r2 = r;
+    r2.wp = r.wp - (r.wp > 0 ? 1 : 0);  // rescan from the previous waypoint (same argmin region)
+    scan_waypoint(r2, Px + z, Py, false);
+    ym = fmin(ym, ym + (double)(r2.wp - r.wp) * z);
+  }
+#endif
   double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
   double dc = satd(-p.dmax, p.dmax, cmd);
   double E = prof_v(r.P, r.wp + 2) - r.x4;
@@ -608,10 +625,10 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   // end / goal (simulation.cpp:110-133)
   double ex = r.x0 - p.g0, ey = r.x1 - p.g1;
   double dg = sqrt(ex * ex + ey * ey);
-  double he = fabs(angle_diff(r.x2, p.g2));
   double Ve = (r.x4 - r.vback);
   if (r.endr && (Ve < 0.1)) return CLRRT_ROLL_END;
-  if ((dg <= 1) && (he < 0.05)) return CLRRT_ROLL_GOAL;
+  // the heading error (an fmod) only matters within 1 m of the goal; both are side-effect free
+  if ((dg <= 1) && (fabs(angle_diff(r.x2, p.g2)) < 0.05)) return CLRRT_ROLL_GOAL;
   return -1;
 }
 
@@ -885,6 +902,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   PhaseClk* pc = nullptr;
 #endif
   int fin = -1;  // >= 0: the lane's rollout ended with this outcome; finished in the next batch
+#ifdef CLRRT_ROLL_PROFILE
+  unsigned long long scan_sum = 0, scan_wave = 0, scan_long = 0, scan_long_pts = 0;
+#endif
   for (;;) {
     if (pc) pc->mark(0);
     // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
@@ -964,6 +984,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     steps++;
     if (pc) pc->mark(6);
     int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
+#ifdef CLRRT_ROLL_PROFILE
+    {
+      unsigned it = r.scan_it, mx_ = it;
+#pragma unroll
+      for (int q = 32; q > 0; q >>= 1) mx_ = max(mx_, (unsigned)__shfl_xor((int)mx_, q, 64));
+      scan_sum += it;
+      scan_long += it > 8;
+      scan_long_pts += it > 8 ? it : 0;
+      if (lane == __ffsll((unsigned long long)__ballot(true)) - 1) scan_wave += mx_;
+    }
+#endif
     w.steps++;
 #ifndef CLRRT_NO_ROWS
     store_row(a.slots + pass * pass_stride + j * slot + (int64_t)steps * 10, 1, r, c7, c8, c9);
@@ -994,6 +1025,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[32 + q], (unsigned long long)pclk.t[q]);
+  if (a.ctr) {
+    atomicAdd(&a.ctr[30], scan_sum);
+    if (scan_wave) atomicAdd(&a.ctr[31], scan_wave);
+    atomicAdd(&a.ctr[28], scan_long);
+    atomicAdd(&a.ctr[29], scan_long_pts);
+  }
 #endif
 }
 

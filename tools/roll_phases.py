@@ -21,3 +21,6 @@ tot = sum(ph)
 print(f"nodes {pl.size()[0]} rounds {st['rounds']} steps {d[0]} rollout ms {pl.kernel_time(1)} nn ms {pl.kernel_time(0)}")
 for nm, v in zip(names, ph):
     print(f"  {nm:32s} {v / max(1, tot) * 100:5.1f}%  {v / max(1, d[0]):8.1f} clk/step")
+print(f"scan: {d[30] / max(1, d[0]):.2f} points per lane-step, wave-level iterations {d[31]:,} "
+      f"({d[31] * 64 / max(1, d[30]):.1f}x the lane average)")
+print(f"scans longer than 8 points: {d[28] / max(1, d[0]) * 100:.2f}% of lane-steps, {d[29] / max(1, d[28]):.1f} points each")
