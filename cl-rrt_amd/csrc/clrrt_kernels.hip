@@ -455,17 +455,23 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       a = ov.gstart[cell];
       ae = ov.gstart[cell + 1];
     }
-    if (ov.nmov == 0) {  // static obstacles only: plain walk of the cell list
-      for (; a < ae; a++) {
-        const int j = ov.gitems[a];
-        if (obs_culled(ov, j, ft, fvx, fvy)) continue;
+    if (ov.nmov == 0) {  // static obstacles only: walk of the cell list, two entries at a time (their
+                         // LDS loads and cull tests overlap; SATs still run in list order)
+      for (; a < ae; a += 2) {
+        const bool two = a + 1 < ae;
+        const int j0 = ov.gitems[a];
+        const int j1 = two ? (int)ov.gitems[a + 1] : j0;
+        const bool c0 = obs_culled(ov, j0, ft, fvx, fvy);
+        const bool c1 = !two || obs_culled(ov, j1, ft, fvx, fvy);
+        if (c0 && c1) continue;
         if (!have_veh) {
           const float of = (float)r.x2;
           const float cf = cosf(of), sf = sinf(of);
           box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
           have_veh = true;
         }
-        if (obs_sat_static(veh, ov, j) == 0) { tests += j + 1; return 0.0; }
+        if (!c0 && obs_sat_static(veh, ov, j0) == 0) { tests += j0 + 1; return 0.0; }
+        if (!c1 && obs_sat_static(veh, ov, j1) == 0) { tests += j1 + 1; return 0.0; }
       }
       tests += ov.n;
       return 10000;
