@@ -154,7 +154,7 @@ struct WalkTile {
   float cemin;         // min costE
   float aopt;          // min (costE - |position - (pcx, pcy)|)
   int32_t nonfinite;   // a record with a non-finite field: no bound
-  int32_t pad;
+  float eroot;         // min (costE - |position - R|), R = node 0's position (the tree root)
 };
 static_assert(sizeof(WalkTile) == 64, "WalkTile layout");
 struct WalkBufs {

@@ -158,7 +158,11 @@ __device__ __forceinline__ float wmin(float v) {
 // the float frame's coordinate error so the bounds hold for the exact positions too.
 __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P, const float4* __restrict__ Q,
                                                     const float* __restrict__ CE, const int* __restrict__ ID,
-                                                    int ntiles, int size, float slack, WalkTile* __restrict__ out) {
+                                                    int ntiles, int size, float slack,
+                                                    const NnRec* __restrict__ nodes, double ox, double oy,
+                                                    WalkTile* __restrict__ out) {
+  // R = node 0's position in the frame (any fixed point gives a valid bound; the root gives a tight one)
+  const float Rx = (float)(nodes[0].x - ox), Ry = (float)(nodes[0].y - oy);
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= ntiles) return;
@@ -181,13 +185,13 @@ __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P
   bad = wsum(bad);
   WalkTile w;
   w.nonfinite = bad > 0;
-  w.pad = 0;
+  w.eroot = 0.f;
   if (cnt == 0) {  // padding only (or only non-finite records)
     w.pcx = w.pcy = w.rcx = w.rcy = 0.f;
     w.pr = w.rr = -1.f;  // empty
     w.thx = 1.f; w.thy = 0.f; w.thh = 4.f;
     w.apx = 1.f; w.apy = 0.f; w.aph = 4.f;
-    w.cemin = w.aopt = 0.f;
+    w.cemin = w.aopt = w.eroot = 0.f;
     if (lane == 0) out[t] = w;
     return;
   }
@@ -198,7 +202,7 @@ __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P
   const bool uok = un > 1e-3f * cnt, aok = an > 1e-3f * cnt;
   ux = uok ? ux / un : 1.f; uy = uok ? uy / un : 0.f;
   ax = aok ? ax / an : 1.f; ay = aok ? ay / an : 0.f;
-  float pr = 0, rr = 0, ud = 1, ad = 1, cmin = __builtin_inff(), aopt = __builtin_inff();
+  float pr = 0, rr = 0, ud = 1, ad = 1, cmin = __builtin_inff(), aopt = __builtin_inff(), eroot = __builtin_inff();
   for (int k = lane; k < size; k += 64) {
     const int j = b + k;
     if (ID[j] < 0) continue;
@@ -217,14 +221,18 @@ __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P
     ad = fminf(ad, (q.z * ax + q.w * ay) / qn);
     cmin = fminf(cmin, ce);
     aopt = fminf(aopt, ce - dp);
+    eroot = fminf(eroot, ce - sqrtf((p.x - Rx) * (p.x - Rx) + (p.y - Ry) * (p.y - Ry)));
   }
   pr = wmax(pr); rr = wmax(rr); ud = wmin(ud); ad = wmin(ad); cmin = wmin(cmin); aopt = wmin(aopt);
+  eroot = wmin(eroot);
   w.pcx = pcx; w.pcy = pcy; w.pr = pr * (1.f + 1e-5f) + 2.f * slack + 1e-5f;
   w.rcx = rcx; w.rcy = rcy; w.rr = rr * (1.f + 1e-5f) + 2.f * slack + 1e-5f;
   w.thx = ux; w.thy = uy; w.thh = uok ? acosf(fminf(fmaxf(ud, -1.f), 1.f)) + 2e-3f : 4.f;
   w.apx = ax; w.apy = ay; w.aph = aok ? acosf(fminf(fmaxf(ad, -1.f), 1.f)) + 2e-3f : 4.f;
   w.cemin = cmin;
   w.aopt = aopt - 2.f * slack - 1e-4f - 1e-5f * fabsf(aopt);
+  // R is a float frame point (exact as given); the node positions err by the frame's slack
+  w.eroot = eroot - 2.f * slack - 1e-4f - 1e-5f * fabsf(eroot);
   if (lane == 0) out[t] = w;
 }
 
@@ -245,7 +253,8 @@ __device__ __forceinline__ float acos_apx(float x) {
 // +inf: no node of the tile can enter the list (empty, or feasibleNode fails for all of them);
 // -inf: no bound (non-finite records).  flen = feasibility length lower limit.  Angles come from
 // acos_apx; each angle test carries 5e-4 rad per approximated term on top of its float margin.
-__device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy, bool ex, float flen) {
+__device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy, bool ex, float flen,
+                                         float dsR = 0.f) {
   if (w.nonfinite) return -__builtin_inff();
   if (w.pr < 0.f) return __builtin_inff();
   const float rho = 4.77f;
@@ -269,7 +278,10 @@ __device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy
     lb = fmaxf(lb, rho * bmin);
   }
   lb = lb - 2e-3f - 1e-5f * fabsf(lb);
-  if (!ex) lb = fmaxf(w.aopt + D * (1.f - 1e-5f) - 2e-3f, w.cemin + lb);
+  // optimize: costE + key >= costE + |s - p| >= (costE - |p - c|) + |s - c| for c = the tile centre
+  // and for c = R (the root: near-straight branches have costE - |p - R| ~ 0, so only tiles whose
+  // branches bend less than the 11th key allows survive)
+  if (!ex) lb = fmaxf(fmaxf(w.aopt + D * (1.f - 1e-5f) - 2e-3f, w.cemin + lb), w.eroot + dsR);
   return lb == lb ? lb : -__builtin_inff();
 }
 
@@ -342,6 +354,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   const float rho = 4.77f, rin = rho - 0.01f - 4.f * dl;
   const float rin2 = rin > 0.f ? rin * rin : -1.f;
   const float flen_t = (float)p.feas_len * (1.f - 1e-5f) - 4.f * dl;
+  // |sample - R| for the root-anchored optimize bound (R = node 0, as in k_walk_tiles), rounded down
+  const float Rx = (float)(nodes[0].x - fr.ox), Ry = (float)(nodes[0].y - fr.oy);
+  const float dsR = sqrtf((rsx - Rx) * (rsx - Rx) + (rsy - Ry) * (rsy - Ry)) * (1.f - 1e-5f) - 2.f * dl - 1e-4f;
   float lk = __builtin_inff();
   int li = 0x7fffffff;
   float kth = __builtin_inff();
@@ -406,9 +421,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         }
       }
     }
-    const int jl = __shfl(j, nq - 1, 64);
-    kc = uni(__shfl(key, nq - 1, 64));
-    hc = uni(HEAD[jl]);
+    // remember the key of the queued record deepest inside a run of equal records (the longest runs,
+    // e.g. the root's zero-length children, are the ones whose remaining records this saves)
+    {
+      const int hd = lane < nq ? HEAD[j] : 0;
+      const int depth = lane < nq ? j - hd : -1;
+      int best = depth;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+      best = uni(best);
+      if (best > 0) {
+        const int l = __ffsll((unsigned long long)__ballot(depth == best)) - 1;
+        kc = uni(__shfl(key, l, 64));
+        hc = uni(__shfl(hd, l, 64));
+      }
+    }
     uint64_t m = __ballot(c);
     while (m) {
       const int l = __ffsll((unsigned long long)m) - 1;
@@ -497,7 +524,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     uint64_t tm;
     if constexpr (STATE) {
       const uint32_t vis = s_vis[st];
-      if (lane < 32 && tl < ntiles && !((vis >> lane) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t);
+      if (lane < 32 && tl < ntiles && !((vis >> lane) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
       const bool take = lane < 32 && lb <= T && !(lb > kth);
       const bool drop = lane < 32 && lb > kth;  // never needed again (kth only decreases)
       tm = __ballot(take);
@@ -506,9 +533,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       if (lane == 0) { s_vis[st] = nvis; s_lbf[st] = rest; }
     } else {
       if (lane < 32) {
-        if (tl < ntiles) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t);
+        if (tl < ntiles) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
       } else if (lane == 32) {
-        lb = walk_lb(sup[st], rsx, rsy, ex, flen_t);
+        lb = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
       }
       lb = fmaxf(lb, __shfl(lb, 32, 64));  // both bound every node of the tile
       const bool take = lane < 32 && (first || lb > Tp) && lb <= T && !(lb > kth);
@@ -542,7 +569,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   for (int t0 = 0; t0 < nsup; t0 += 64) {
     const int t = t0 + lane;
     if (t < nsup) {
-      const float lb = walk_lb(sup[t], rsx, rsy, ex, flen_t);
+      const float lb = walk_lb(sup[t], rsx, rsy, ex, flen_t, dsR);
       if constexpr (STATE) {
         s_lbf[t] = lb;
         s_vis[t] = 0u;
@@ -645,10 +672,10 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
   e = hipcub::DeviceScan::InclusiveScan(w.tmp, bytes, w.vals, w.HEAD, hipcub::Max(), Npad, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_walk_tiles, dim3((ntiles + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
-                     fr.delta, w.tiles);
+                     fr.delta, nodes, fr.ox, fr.oy, w.tiles);
   LAUNCH_CHECK3();
   hipLaunchKernelGGL(k_walk_tiles, dim3((nsup + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, nsup,
-                     WALK_TILE * WALK_SUPER, fr.delta, w.supers);
+                     WALK_TILE * WALK_SUPER, fr.delta, nodes, fr.ox, fr.oy, w.supers);
   LAUNCH_CHECK3();
   // per-sample LDS: 8 B per super-tile with state, 2 B without; state while it costs no occupancy
   const bool state = nsup <= 1280 && !stateless;
