@@ -11,8 +11,8 @@ from clrrt import abi, scenes
 ms = float(sys.argv[1]) if len(sys.argv) > 1 else 2000.0
 walk_grow = len(sys.argv) > 2 and sys.argv[2] == "walk"
 obs = scenes.urban_scene(200)
-pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=4 << 20,
-                   max_rows=1 << 26, max_batch=16384)
+pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=8 << 20,
+                   max_rows=1 << 28, max_batch=16384)
 pl.set_obstacles(obs)
 pl.tree_init()
 pl.set_option("nn_walk_min", 8192 if walk_grow else 1 << 40)
