@@ -516,39 +516,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   };
   // visit the tiles of super-tile st whose bounds lie in (Tp, min(T, kth)] (pass 0: <= min(T, kth));
   // s_lb[st] becomes the bound of the tiles beyond T
-  auto visit_super = [&](int st, float Tp, float T, bool first) {
+  // half-wave minimum (lanes 0-31 and 32-63 separately)
+  auto hmin = [&](float v) -> float {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+  };
+  // visit the tiles of super-tiles sa (lanes 0-31) and sb (lanes 32-63, -1: none) whose bounds lie in
+  // (Tp, min(T, kth)] (STATE: not visited yet and <= min(T, kth)); the super-tiles' LDS bounds become
+  // those of their tiles beyond T
+  auto visit_supers = [&](int sa, int sb, float Tp, float T, bool first) {
     const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    n_sup++;
+    n_sup += 1 + (sb >= 0);
+    const int st = lane < 32 ? sa : sb;
     const int tl = st * WALK_SUPER + (lane & 31);
     float lb = __builtin_inff();
     uint64_t tm;
     if constexpr (STATE) {
-      const uint32_t vis = s_vis[st];
-      if (lane < 32 && tl < ntiles && !((vis >> lane) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
-      const bool take = lane < 32 && lb <= T && !(lb > kth);
-      const bool drop = lane < 32 && lb > kth;  // never needed again (kth only decreases)
+      const uint32_t vis = st >= 0 ? s_vis[st] : 0xffffffffu;
+      if (st >= 0 && tl < ntiles && !((vis >> (lane & 31)) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
+      const bool take = st >= 0 && lb <= T && !(lb > kth);
+      const bool drop = st >= 0 && lb > kth;  // never needed again (kth only decreases)
       tm = __ballot(take);
-      const uint32_t nvis = vis | (uint32_t)tm | (uint32_t)__ballot(drop);
-      const float rest = wmin(take || drop || lane >= 32 ? __builtin_inff() : lb);
-      if (lane == 0) { s_vis[st] = nvis; s_lbf[st] = rest; }
-    } else {
-      if (lane < 32) {
-        if (tl < ntiles) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
-      } else if (lane == 32) {
-        lb = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
+      const uint64_t dm = __ballot(drop);
+      const float rest = hmin(take || drop || st < 0 ? __builtin_inff() : lb);
+      if ((lane & 31) == 0 && st >= 0) {
+        const int sh = lane;  // 0 or 32
+        s_vis[st] = vis | (uint32_t)(tm >> sh) | (uint32_t)(dm >> sh);
+        s_lbf[st] = rest;
       }
-      lb = fmaxf(lb, __shfl(lb, 32, 64));  // both bound every node of the tile
-      const bool take = lane < 32 && (first || lb > Tp) && lb <= T && !(lb > kth);
+    } else {
+      float sl = __builtin_inff();
+      if ((lane & 31) == 0 && st >= 0) sl = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
+      const float slb = __shfl(sl, lane & 32, 64);
+      if (st >= 0 && tl < ntiles) lb = fmaxf(walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR), slb);  // both bound
+      const bool take = st >= 0 && (first || lb > Tp) && lb <= T && !(lb > kth);
       tm = __ballot(take);
-      const float rest = wmin(lane < 32 && lb > T ? lb : __builtin_inff());
-      if (lane == 0) s_lb[st] = __float2half_rd(rest);
+      const float rest = hmin(st >= 0 && lb > T ? lb : __builtin_inff());
+      if ((lane & 31) == 0 && st >= 0) s_lb[st] = __float2half_rd(rest);
     }
     // tiles that the list has pruned since they were selected are skipped
     auto next_tile = [&]() -> int {
       while (tm) {
         const int a = __ffsll((unsigned long long)tm) - 1;
         tm &= tm - 1;
-        if (!(__shfl(lb, a, 64) > kth)) return st * WALK_SUPER + a;
+        if (!(__shfl(lb, a, 64) > kth)) return (a < 32 ? sa : sb) * WALK_SUPER + (a & 31);
       }
       return -1;
     };
@@ -598,10 +610,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       const float lb = t < nsup ? lds_lb(t) : __builtin_inff();
       uint64_t m = __ballot(lb < __builtin_inff() && lb <= lim_t);
       while (m) {
-        const int st = t0 + __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        if (lds_lb(st) > kth) continue;
-        visit_super(st, Tp, T, pass == 0);
+        // two super-tiles per visit (one per half wave)
+        int sa = -1, sb = -1;
+        while (m && sb < 0) {
+          const int st = t0 + __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          if (lds_lb(st) > kth) continue;
+          if (sa < 0) sa = st; else sb = st;
+        }
+        if (sa >= 0) visit_supers(sa, sb, Tp, T, pass == 0);
       }
     }
     drain();
