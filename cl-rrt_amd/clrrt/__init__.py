@@ -170,6 +170,10 @@ class Planner:
             raise ClrrtError(f"clrrt_create failed ({rc}): no usable HIP device {device}?")
         self.h = h
         self.max_batch = max_batch
+        # engine options for A/B runs: CLRRT_OPTIONS="key=value,key=value" (clrrt_set_option)
+        for kv in filter(None, os.environ.get("CLRRT_OPTIONS", "").split(",")):
+            k, v = kv.split("=")
+            self.set_option(k.strip(), int(v))
 
     def close(self):
         if getattr(self, "h", None):
@@ -320,7 +324,7 @@ class Planner:
             arr[i].parent, arr[i].gb = par, gb
             arr[i].sample[0], arr[i].sample[1] = sx, sy
         out = (abi.RolloutResult * n)()
-        cap = 512
+        cap = 1100 if rows else 1
         buf = np.zeros((n, cap, 10)) if rows else None
         self._chk(self.L.clrrt_rollout_batch(self.h, arr, n, out,
                                              buf.ctypes.data_as(P(C.c_double)) if rows else None, cap),

@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -106,6 +107,12 @@ struct clrrt_ctx {
   void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
+  int roll_handoff = 0;       // option "roll_handoff": donor waves hand their last rollouts to absorbers
+  void* roll_cont = nullptr;  // [roll_cont_cap] RollCont
+  int* roll_ready = nullptr;  // [roll_cont_cap]
+  int* roll_ctl = nullptr;    // [4]
+  int roll_cont_cap = 0;
+  int roll_epoch = 0;
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
   GoalRec* goal_recs = nullptr;
   int* bp_path = nullptr;  // [max_nodes + 2]: chain, then count and length
@@ -121,6 +128,18 @@ struct clrrt_ctx {
   float* ri_cost = nullptr;    // [path_cap]
   double* ri_terms = nullptr;  // [2 * path_rows_cap]
   double reg_x0 = 0, reg_y0 = 0, reg_x1 = 0, reg_y1 = 0;  // sampling region + margin
+  // pipelined BATCH rounds (clrrt_expand): while a round's rollouts run on `stream`, the walk search
+  // of the next round's samples over the same tree runs on `side` into the *2 buffers; the round
+  // then merges in the nodes it appended (launch_nn_delta) and the buffers swap
+  int nn_pipeline = 1;  // option "nn_pipeline"
+  hipStream_t side = nullptr;
+  hipEvent_t ev_tree = nullptr, ev_walk = nullptr;
+  clrrt_sample* d_samples2 = nullptr;
+  clrrt_sample* h_samples2 = nullptr;
+  int* cand2 = nullptr;
+  float* ckey2 = nullptr;
+  int* ncand2 = nullptr;
+  int* ctie2 = nullptr;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -172,15 +191,16 @@ struct KTimer {
   clrrt_ctx* c;
   int which;
   hipEvent_t a = nullptr, b = nullptr;
-  KTimer(clrrt_ctx* c_, int w) : c(c_), which(w) {
+  hipStream_t s;
+  KTimer(clrrt_ctx* c_, int w, hipStream_t s_ = nullptr) : c(c_), which(w), s(s_ ? s_ : c_->stream) {
     if (!c->timing) return;
     a = ev_get(c);
     b = ev_get(c);
-    if (a) hipEventRecord(a, c->stream);
+    if (a) hipEventRecord(a, s);
   }
   ~KTimer() {
     if (!c->timing || !a || !b) return;
-    hipEventRecord(b, c->stream);
+    hipEventRecord(b, s);
     c->ev_pending.push_back({which, {a, b}});
   }
 };
@@ -365,10 +385,15 @@ static void free_all(clrrt_ctx* c) {
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
                   c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->cmp.packed, c->cmp.scanned,
-                  c->cmp.tmp};
+                  c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
+  if (c->h_samples2) hipHostFree(c->h_samples2);
+  if (c->side) hipStreamSynchronize(c->side);
+  if (c->ev_tree) hipEventDestroy(c->ev_tree);
+  if (c->ev_walk) hipEventDestroy(c->ev_walk);
+  if (c->side) hipStreamDestroy(c->side);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
   if (c->h_bbox) hipHostFree(c->h_bbox);
@@ -417,6 +442,14 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->ckey, B * CAND_K));
   chk(dalloc(&c->ncand, B));
   chk(dalloc(&c->ctie, B));
+  chk(dalloc(&c->d_samples2, B));
+  chk(dalloc(&c->cand2, B * CAND_K));
+  chk(dalloc(&c->ckey2, B * CAND_K));
+  chk(dalloc(&c->ncand2, B));
+  chk(dalloc(&c->ctie2, B));
+  chk(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  chk(hipEventCreateWithFlags(&c->ev_tree, hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->res_gb, B * CAND_K));
@@ -459,12 +492,20 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
       c->n_cu = ncu;
   }
+  // hand-off slots: every lane of every wave of the largest persistent grid (roll_blocks <= 4 per CU)
+  c->roll_cont_cap = 4 * c->n_cu * 256;
+  chk(hipMalloc(&c->roll_cont, rollout_cont_bytes() * (size_t)c->roll_cont_cap));
+  chk(dalloc(&c->roll_ready, c->roll_cont_cap));
+  chk(dalloc(&c->roll_ctl, 4));
+  if (rc == CLRRT_OK) chk(hipMemset(c->roll_ready, 0, sizeof(int) * c->roll_cont_cap));
+  if (rc == CLRRT_OK) chk(hipMemset(c->roll_ctl, 0, sizeof(int) * 4));
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
   chk(dalloc(&c->fb_count, 1));
   chk(dalloc(&c->work_ctr, 40));
   if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 40 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
+  chk(hipHostMalloc((void**)&c->h_samples2, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_int, sizeof(int) * 4, hipHostMallocDefault));
   if (rc != CLRRT_OK) {
@@ -1048,6 +1089,8 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_stateless") c->nnw_stateless = value != 0;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
+  else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
+  else if (k == "roll_handoff") c->roll_handoff = value != 0;
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
   return CLRRT_OK;
 }
@@ -1130,13 +1173,15 @@ static int ensure_walk(clrrt_ctx* c) {
   return CLRRT_OK;
 }
 
-// Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
-static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
-  hipStream_t st = c->stream;
-  KTimer kt(c, 0);
-  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
-  NnGrid g{};
+// Search region (the sampling region and the tree's box) and the float frame of the searches.
+struct NnSetup {
+  NnFrame fr;
   double x0, y0, x1, y1;
+  bool region_ok;
+};
+static NnSetup nn_setup(clrrt_ctx* c) {
+  NnSetup su;
+  double& x0 = su.x0; double& y0 = su.y0; double& x1 = su.x1; double& y1 = su.y1;
   sample_region(c->params, x0, y0, x1, y1);
   if (c->bbox[0] <= c->bbox[2]) {  // grid covers the samples and every finite node: no overflow
     x0 = std::min(x0, c->bbox[0] - 1.0); y0 = std::min(y0, c->bbox[1] - 1.0);
@@ -1154,8 +1199,30 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
     const double d = 16.0 * std::ldexp(E, -24) + 1e-5;
     fr.delta = std::isfinite(d) ? (float)d : HUGE_VALF;
   }
+  su.fr = fr;
   const double W = x1 - x0, H = y1 - y0;
-  const bool region_ok = std::isfinite(W * H) && W * H > 0;
+  su.region_ok = std::isfinite(W * H) && W * H > 0;
+  return su;
+}
+
+// The walk search serves the tree as it is now (run_nn's choice).
+static bool walk_serves(clrrt_ctx* c, const NnSetup& su) {
+  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && su.region_ok;
+  const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && su.region_ok;
+  return !use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && su.region_ok;
+}
+
+// Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
+static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
+  hipStream_t st = c->stream;
+  KTimer kt(c, 0);
+  int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
+  NnGrid g{};
+  const NnSetup su = nn_setup(c);
+  const NnFrame fr = su.fr;
+  const double x0 = su.x0, y0 = su.y0, x1 = su.x1, y1 = su.y1;
+  const double W = x1 - x0, H = y1 - y0;
+  const bool region_ok = su.region_ok;
   const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && region_ok;
   const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && region_ok;
   if (!use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && region_ok) {
@@ -1192,8 +1259,10 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
 }
 
 // Stages 1-4 (+5 in EXACT mode) for n samples already in c->d_samples.  Returns the number of
-// samples to commit (n in BATCH mode).
-static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
+// samples to commit (n in BATCH mode).  have_lists: the candidate lists are already in c->cand
+// (pipelined rounds); during_roll runs right after the rollout kernel's launch.
+static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_lists = false,
+                        const std::function<int()>& during_roll = nullptr) {
   hipStream_t st = c->stream;
   KeyId* scratch = nullptr;
   if (exact) {
@@ -1201,10 +1270,13 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
     if (rc != CLRRT_OK) return rc;
     scratch = c->sort_scratch;
   }
-  {
+  if (!have_lists) {
     int rc = run_nn(c, n, scratch);
     if (rc != CLRRT_OK) return rc;
   }
+  // the tree, this round's lists and the walk buffers are final here: work queued by during_roll on
+  // another stream waits for this point only, not for the rollouts
+  if (during_roll) HIPC(c, hipEventRecord(c->ev_tree, st));
   {
     KTimer kt(c, 1);
     RollArgs a = roll_args(c, n * CAND_K);
@@ -1213,11 +1285,21 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out) {
     a.slots = c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
+    const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu) : c->roll_handoff ? c->n_cu : 2 * c->n_cu;
+    if (c->roll_persistent && c->roll_handoff) {
+      a.cont = c->roll_cont;
+      a.cont_ready = c->roll_ready;
+      a.cont_ctl = c->roll_ctl;
+      a.cont_epoch = ++c->roll_epoch;
+    }
     if (c->roll_persistent && c->dp.n_steps_max > 0)
-      HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best,
-                                        c->roll_blocks > 0 ? c->roll_blocks : 2 * c->n_cu));
+      HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(st, SRC_SPEC, a));
+  }
+  if (during_roll) {  // queued behind the rollout kernel, whose persistent blocks take the CUs first
+    int rc = during_roll();
+    if (rc != CLRRT_OK) return rc;
   }
   SelArgs s;
   s.p = c->dp; s.tree = c->tree; s.cand = c->cand; s.ckey = c->ckey; s.ncand = c->ncand; s.res = c->res_spec;
@@ -1254,9 +1336,11 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
   }
   HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_int + 3, c->roll_ctl + 3, sizeof(int), hipMemcpyDeviceToHost, st));
   if (merge_bbox) HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
   if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+  if (c->h_int[3] != 0) return fail(c, CLRRT_EHIP, "rollout hand-off: a donated rollout was never published");
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
   c->counters.sim_count += c->h_totals[2];
@@ -1340,7 +1424,10 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   int cur = exact ? std::min(batch, 16) : batch;
   int64_t nodes_before = c->n_nodes;
   int rc = CLRRT_OK;
+  bool have_next = false;  // this round's samples and lists were prepared by the previous round
+  double last_round_ms = 0;
   for (;;) {
+    const auto tr0 = std::chrono::steady_clock::now();
     if (n_iters > 0 && st.iterations >= n_iters) break;
     if (n_iters == 0) {
       double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1360,10 +1447,52 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
       clrrt_draw_samples(&c->params, &work, 1, &smp);
       pending.push_back(smp);
     }
-    for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
-    HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
+    if (!have_next) {
+      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
+      HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
+    }
+    // Pipelined BATCH rounds: the next round's samples are known now (BATCH rounds commit every
+    // sample), so their walk search over this round's tree runs on the side stream while this round's
+    // rollouts run (the rollout kernel's last waves leave most CUs idle); after the commit, the nodes
+    // this round appended are searched and merged in (launch_nn_delta).  The lists equal a search over
+    // the committed tree, so the rounds' results are unchanged.
+    int nb2 = 0;
+    NnSetup su{};
+    if (!exact && c->nn_pipeline) {
+      nb2 = cur;
+      if (n_iters > 0) nb2 = (int)std::min<int64_t>(nb2, n_iters - st.iterations - nb);
+      if (n_iters == 0) {
+        double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (!(ms + last_round_ms < budget_ms)) nb2 = 0;  // this is probably the last round
+      }
+      if (nb2 > 0) {
+        su = nn_setup(c);
+        if (!walk_serves(c, su)) nb2 = 0;
+      }
+    }
+    auto prefetch = [&]() -> int {
+      while ((int64_t)pending.size() < (int64_t)nb + nb2) {
+        clrrt_sample smp;
+        clrrt_draw_samples(&c->params, &work, 1, &smp);
+        pending.push_back(smp);
+      }
+      for (int j = 0; j < nb2; j++) c->h_samples2[j] = pending[nb + j];
+      HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));  // recorded before the rollouts (eval_samples)
+      HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * nb2, hipMemcpyHostToDevice, c->side));
+      {
+        KTimer kt(c, 0, c->side);
+        const int rw = ensure_walk(c);
+        if (rw != CLRRT_OK) return rw;
+        HIPC(c, launch_nn_walk(c->side, c->d_samples2, nb2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1,
+                               su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
+                               c->nnw_stateless));
+      }
+      HIPC(c, hipEventRecord(c->ev_walk, c->side));
+      return CLRRT_OK;
+    };
     int L = nb, nn = 0;
-    if ((rc = eval_samples(c, nb, exact, &L)) != CLRRT_OK) break;
+    if ((rc = eval_samples(c, nb, exact, &L, have_next, nb2 > 0 ? std::function<int()>(prefetch) : nullptr)) != CLRRT_OK)
+      break;
     if (!exact) {
       // BATCH rounds commit every sample, so the next round's samples are known now: draw them
       // while the GPU evaluates this round (the draw is ~0.05 us per sample on the host)
@@ -1376,7 +1505,26 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
       }
     }
     if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
+    const int64_t first_new = c->n_nodes;
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
+    have_next = false;
+    if (nb2 > 0) {
+      HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
+      if (nn > 0) {
+        KTimer kt(c, 0);
+        const NnSetup su2 = nn_setup(c);  // the box now includes the appended nodes
+        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)nb2 * NN_K));
+        HIPC(c, launch_nn_delta(c->stream, c->d_samples2, nb2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
+                                max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed));
+      }
+      std::swap(c->d_samples, c->d_samples2);
+      std::swap(c->h_samples, c->h_samples2);
+      std::swap(c->cand, c->cand2);
+      std::swap(c->ckey, c->ckey2);
+      std::swap(c->ncand, c->ncand2);
+      std::swap(c->ctie, c->ctie2);
+      have_next = true;
+    }
     for (int j = 0; j < L; j++) {
       pending.pop_front();
       for (int k = 0; k < 3; k++) clrrt_rng_next(&committed);
@@ -1386,7 +1534,9 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     st.speculated += nb;
     st.rounds++;
     if (exact) cur = std::max(8, std::min(batch, L == nb ? 2 * nb : 2 * L));
+    last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
+  HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->stream));
   st.nodes_added = c->n_nodes - nodes_before;
   st.elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

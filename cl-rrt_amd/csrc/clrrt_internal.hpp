@@ -84,6 +84,12 @@ struct RollArgs {
   RollRes* __restrict__ res_gb;            // SPEC: goal-biased rollout (outcome -1 = not run)
   unsigned long long* ctr;  // [3] steps, scan points, box tests (nullable)
   int njobs;
+  // persistent rollouts: hand-off of the last rollouts from donor waves to absorbers (k_roll_run);
+  // cont == nullptr: off.  cont_ctl = {published, claimed, donors alive, hand-off errors}
+  void* cont;
+  int* cont_ready;  // per slot: == cont_epoch once the slot is written
+  int* cont_ctl;
+  int cont_epoch, cont_donors;
 };
 
 struct SelArgs {
@@ -176,6 +182,11 @@ size_t walk_sort_bytes(int n);
 hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
                           const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
                           float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless);
+// Pipelined BATCH rounds: merges into (cand, ckey, ncand) -- the lists over nodes [0, first) -- the
+// nodes [first, first + count) appended since (k_nn_partial over them + k_nn_merge_delta).
+hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
+                           const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
+                           float* ckey, int* ncand, int* ctie, float* seed);
 // Brute-force candidate lists of the samples fb_list[0 .. *fb_count) (the walk search's hand-offs).
 hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
@@ -197,6 +208,7 @@ hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
                                      int blocks);
 size_t rollout_prep_bytes();
+size_t rollout_cont_bytes();
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);

@@ -325,6 +325,66 @@ __global__ void k_nn_merge(int B, int nchunks, int limit, const float* __restric
   ctie[s] = tie;
 }
 
+// Pipelined BATCH rounds (clrrt_expand): the lists (cand, ckey, ncand) already hold the first `limit`
+// feasible nodes of the older nodes [0, id0) in (key, id) order -- the walk search over the tree as it
+// was when the previous round's rollouts started -- and the chunk lists pk/pi the top NN_K of the
+// nodes that round appended, [id0, id0 + n) (ids relative to id0).  Every appended id is larger than
+// every older one, so the first `limit` of the union in (key, id) order -- the list a search over the
+// whole tree returns -- are the first `limit` of the two lists' merge.  ctie is not rebuilt exactly
+// (the older list's entries past `limit` are not kept); only EXACT mode reads it, and EXACT rounds are
+// never pipelined.
+// Upper bound for the appended nodes' search: a node whose key exceeds the current list's `limit`-th
+// key cannot enter the merged list (every listed node has a smaller id), so it seeds k_nn_partial's
+// shared key cap.
+__global__ void k_nn_delta_seed(int B, int limit, const float* __restrict__ ckey, const int* __restrict__ ncand,
+                                float* __restrict__ seed) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B) return;
+  const float k = (limit > 0 && ncand[s] >= limit) ? ckey[s * CAND_K + limit - 1] : __builtin_inff();
+  ((unsigned int*)seed)[s] = ord_enc32(k);
+}
+
+__global__ void k_nn_merge_delta(int B, int nchunks, int limit, const float* __restrict__ pk,
+                                 const int* __restrict__ pi, int id0, int* __restrict__ cand,
+                                 float* __restrict__ ckey, int* __restrict__ ncand, int* __restrict__ ctie) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B) return;
+  float keys[NN_K];
+  int ids[NN_K];
+  const int n0 = ncand[s];
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) {
+    const bool v = j < CAND_K && j < n0;
+    keys[j] = v ? ckey[s * CAND_K + (j < CAND_K ? j : 0)] : __builtin_inff();
+    ids[j] = v ? cand[s * CAND_K + (j < CAND_K ? j : 0)] : 0x7fffffff;
+  }
+  for (int c = 0; c < nchunks; c++) {
+    const size_t base = ((size_t)s * nchunks + c) * NN_K;
+    for (int j = 0; j < NN_K; j++) {
+      const int id = pi[base + j];
+      if (id == 0x7fffffff) break;
+      const float k = pk[base + j];
+      if (lex_less(k, id + id0, keys[NN_K - 1], ids[NN_K - 1])) topk_insert(keys, ids, k, id + id0);
+      else break;  // chunk lists are sorted
+    }
+  }
+  int n = 0, valid = 0;
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) valid += ids[j] != 0x7fffffff;
+  const int sel = min(limit, valid);
+  int tie = 0;
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) {
+    const bool v = j < sel;
+    cand[s * CAND_K + j] = v ? ids[j] : -1;
+    ckey[s * CAND_K + j] = keys[j];
+    n += v;
+    tie |= (j < sel && j + 1 < valid && keys[j] == keys[j + 1]);
+  }
+  ncand[s] = n;
+  ctie[s] = tie;
+}
+
 // EXACT mode, samples whose candidate selection involves equal keys: rebuild the full (id, key)
 // sequence in node order and replay libstdc++'s std::sort on it (one lane per sample), then walk it
 // exactly as sortNodesExplore/Optimize do (rrtplanner.cpp:237-243).
@@ -854,6 +914,11 @@ template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
   glibc::stage_tables();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0 && a.cont) {  // k_roll_run's hand-off counters (the error count accumulates)
+    a.cont_ctl[0] = 0;
+    a.cont_ctl[1] = 0;
+    a.cont_ctl[2] = a.cont_donors;
+  }
   if (j >= a.njobs) return;
   const int id = a.cand[j];
   if (id < 0) {
@@ -882,8 +947,21 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
 #ifndef REFILL_MIN
 #define REFILL_MIN 16
 #endif
+#ifndef CLRRT_DONATE_MAX  // a donor wave hands off its rollouts once at most this many are left
+#define CLRRT_DONATE_MAX 16
+#endif
+struct RollCont {  // a rollout in flight, handed from a donor wave to an absorber (k_roll_run)
+  Roll r;
+  double c7, c8, c9;
+  int32_t j, k, s, pass, steps, pad;
+};
+size_t rollout_cont_bytes() { return sizeof(RollCont); }
 
-template <bool NEED_GAP>
+#ifndef CLRRT_ABANDON_EVERY  // steps between checks for an earlier candidate's success (power of 2)
+#define CLRRT_ABANDON_EVERY 16
+#endif
+
+template <bool NEED_GAP, bool HANDOFF>
 #ifndef CLRRT_ROLL_WAVES
 #define CLRRT_ROLL_WAVES 1
 #endif
@@ -909,48 +987,87 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 #endif
   int fin = -1;  // >= 0: the lane's rollout ended with this outcome; finished in the next batch
 #ifdef CLRRT_ROLL_PROFILE
-  unsigned long long scan_sum = 0, scan_wave = 0, scan_long = 0, scan_long_pts = 0;
+  unsigned long long scan_sum = 0, scan_wave = 0, scan_long = 0, scan_long_pts = 0, chain_steps = 0;
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
+  // Hand-off of the last rollouts (a.cont != nullptr).  Rollout lengths are very uneven (most end
+  // within ~30 steps, the longest run the full 500-step horizon), so once the job queue is empty most
+  // waves keep a few long rollouts and hold their SIMD for the rest of the launch.  Instead, wave 0 of
+  // each block is an absorber and the other waves are donors: a donor whose queue has run out and
+  // which has <= CLRRT_DONATE_MAX rollouts left writes their state to a.cont and exits, freeing its SIMD
+  // for work queued on other streams (the next round's nearest-node search); absorbers take the
+  // donated rollouts into idle lanes and continue them (same job, same rows, same results).
+  constexpr bool cont_on = HANDOFF;  // a.cont != nullptr
+  const bool absorber = !cont_on || (threadIdx.x >> 6) == 0;
+  RollCont* __restrict__ cont = (RollCont*)a.cont;
+  bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
+  int poll = 0;
+  // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
+  // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
+  // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
+  // every step for one or two lanes.
+  auto finish_parked = [&]() {
+    if (fin >= 0) {
+      RollRes out;
+      finish_rollout(r, c7, c8, c9, fin, steps, out);
+      if (pass == 1) {
+        a.res_gb[j] = out;
+        j = -1;
+      } else {
+        a.res[j] = out;
+        const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
+        if (ok) atomicMin(&best[s], k);
+        if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
+          // goal-biased rollout from the node this rollout would append (expandTree :163-173)
+          const RefD R = make_goal_ref(out.bx, out.by, a.p);
+          roll_init(r, out.st, R, out.vback, true, a.p);
+          c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
+          pass = 1;
+          steps = 0;
+          double* rows = a.slots + pass_stride + j * slot;
+#pragma unroll
+          for (int q = 0; q < 10; q++) rows[q] = out.st[q];
+          rows[7] = c7;
+        } else {
+          a.res_gb[j].outcome = -1;
+          j = -1;
+        }
+      }
+      fin = -1;
+    }
+  };
   for (;;) {
     if (pc) pc->mark(0);
-    // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
-    // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
-    // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
-    // every step for one or two lanes.
     const uint64_t parked = __ballot(fin >= 0);
-    const uint64_t m0 = __ballot(j < 0 && !exhausted);
     const uint64_t busy0 = __ballot(j >= 0 && fin < 0);
-    if ((parked | m0) && (__popcll(parked | m0) >= REFILL_MIN || busy0 == 0)) {
-      if (fin >= 0) {
-        RollRes out;
-        finish_rollout(r, c7, c8, c9, fin, steps, out);
-        if (pass == 1) {
-          a.res_gb[j] = out;
-          j = -1;
-        } else {
-          a.res[j] = out;
-          const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
-          if (ok) atomicMin(&best[s], k);
-          if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
-            // goal-biased rollout from the node this rollout would append (expandTree :163-173)
-            const RefD R = make_goal_ref(out.bx, out.by, a.p);
-            roll_init(r, out.st, R, out.vback, true, a.p);
-            c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
-            pass = 1;
-            steps = 0;
-            double* rows = a.slots + pass_stride + j * slot;
-#pragma unroll
-            for (int q = 0; q < 10; q++) rows[q] = out.st[q];
-            rows[7] = c7;
-          } else {
-            a.res_gb[j].outcome = -1;
-            j = -1;
-          }
+    if (cont_on && !absorber && qdone && __popcll(busy0 | parked) <= CLRRT_DONATE_MAX) {
+      finish_parked();  // may start goal-biased rollouts
+      const bool give = j >= 0;
+      const uint64_t gm = __ballot(give);
+      if (gm) {
+        const int leader = __ffsll((unsigned long long)gm) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&a.cont_ctl[0], __popcll(gm));
+        base = __shfl(base, leader, 64);
+        if (give) {
+          const int q = base + __popcll(gm & ((1ull << lane) - 1));
+          RollCont& cc = cont[q];
+          cc.r = r;
+          cc.c7 = c7; cc.c8 = c8; cc.c9 = c9;
+          cc.j = j; cc.k = k; cc.s = s; cc.pass = pass; cc.steps = steps;
+          __hip_atomic_store(&a.cont_ready[q], a.cont_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
-        fin = -1;
       }
+      if (lane == 0) atomicSub(&a.cont_ctl[2], 1);
+      break;
+    }
+    const uint64_t m0 = __ballot(j < 0 && !qdone);
+    // once the queue is empty, finish parked rollouts at once: a goal-biased follow-up (up to the whole
+    // horizon) must not wait for other lanes to end
+    if ((parked | m0) && (__popcll(parked | m0) >= REFILL_MIN || busy0 == 0 || (qdone && parked))) {
+      finish_parked();
       if (pc) pc->mark(7);
-      const bool idle = j < 0 && !exhausted;
+      const bool idle = j < 0 && !qdone;
       const uint64_t m = __ballot(idle);
       if (m) {
         // wave-aggregated fetch: the idle lanes take consecutive queue positions
@@ -978,12 +1095,65 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
             }
           }
         }
+        qdone = qdone || __ballot(exhausted) != 0;
       }
       if (pc) pc->mark(6);
       continue;
     }
+    if (cont_on && absorber && qdone) {
+      const uint64_t idle = __ballot(j < 0);
+      if (idle && (busy0 == 0 || ++poll >= 32)) {
+        poll = 0;
+        // claim up to popcount(idle) donated rollouts (never past the published count)
+        const int leader = __ffsll((unsigned long long)idle) - 1;
+        int got = 0, h = 0;
+        if (lane == leader) {
+          const int want = __popcll(idle);
+          for (;;) {
+            h = __hip_atomic_load(&a.cont_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int t = __hip_atomic_load(&a.cont_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int n = min(want, t - h);
+            if (n <= 0) break;
+            if (atomicCAS(&a.cont_ctl[1], h, h + n) == h) { got = n; break; }
+          }
+        }
+        got = __shfl(got, leader, 64);
+        h = __shfl(h, leader, 64);
+        if (got) {
+          const int rk = __popcll(idle & ((1ull << lane) - 1));
+          if (j < 0 && rk < got) {
+            const int q = h + rk;
+            // the donor published the slot count before writing the slot: wait for its flag
+            int spins = 0;
+            while (__hip_atomic_load(&a.cont_ready[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.cont_epoch) {
+              __builtin_amdgcn_s_sleep(2);
+              if (++spins > (1 << 24)) break;
+            }
+            if (spins > (1 << 24)) {
+              atomicAdd(&a.cont_ctl[3], 1);  // reported by the host as an error
+            } else {
+              const RollCont& cc = cont[q];
+              r = cc.r;
+              c7 = cc.c7; c8 = cc.c8; c9 = cc.c9;
+              j = cc.j; k = cc.k; s = cc.s; pass = cc.pass; steps = cc.steps;
+              fin = -1;
+            }
+          }
+          continue;
+        }
+        if (busy0 == 0) {
+          // nothing to run: done once no donor remains and every donated rollout is claimed
+          const int d = __hip_atomic_load(&a.cont_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int hh = __hip_atomic_load(&a.cont_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int tt = __hip_atomic_load(&a.cont_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (parked == 0 && d <= 0 && hh >= tt) break;
+          __builtin_amdgcn_s_sleep(8);
+          continue;
+        }
+      }
+    }
     if (busy0 == 0) {
-      if (__ballot(!exhausted) == 0) break;
+      if (parked == 0 && qdone) break;
       continue;
     }
     if (j < 0 || fin >= 0) continue;
@@ -996,9 +1166,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 #pragma unroll
       for (int q = 32; q > 0; q >>= 1) mx_ = max(mx_, (unsigned)__shfl_xor((int)mx_, q, 64));
       scan_sum += it;
-      scan_long += it > 8;
-      scan_long_pts += it > 8 ? it : 0;
-      if (lane == __ffsll((unsigned long long)__ballot(true)) - 1) scan_wave += mx_;
+      const uint64_t act = __ballot(true);
+      if (lane == __ffsll((unsigned long long)act) - 1) {
+        scan_wave += mx_;
+        scan_long += __popcll(act);  // active lanes of this wave step
+        scan_long_pts += 1;          // wave steps
+      }
+      chain_steps++;
     }
 #endif
     w.steps++;
@@ -1009,24 +1183,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
       fin = o;
-    } else if ((steps & 15) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+    } else if ((steps & (CLRRT_ABANDON_EVERY - 1)) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
       // an earlier candidate of this sample succeeded: this result will not be looked at
       if (pass == 0) a.res[j].outcome = -1;
       a.res_gb[j].outcome = -1;
       j = -1;
     }
   }
-  if (a.ctr) {
-    __shared__ __attribute__((aligned(16))) unsigned long long s_ctr[4];
-    if (threadIdx.x < 3) s_ctr[threadIdx.x] = 0;
-    __syncthreads();
-    if (w.steps) {
-      atomicAdd(&s_ctr[0], (unsigned long long)w.steps);
-      atomicAdd(&s_ctr[1], (unsigned long long)w.scan);
-      atomicAdd(&s_ctr[2], (unsigned long long)w.box);
+  if (a.ctr) {  // per-wave sums (no block barrier: donor waves leave early)
+    unsigned long long v0 = w.steps, v1 = w.scan, v2 = w.box;
+#pragma unroll
+    for (int q = 32; q > 0; q >>= 1) {
+      v0 += (unsigned long long)__shfl_xor((long long)v0, q, 64);
+      v1 += (unsigned long long)__shfl_xor((long long)v1, q, 64);
+      v2 += (unsigned long long)__shfl_xor((long long)v2, q, 64);
     }
-    __syncthreads();
-    if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
+    if (lane == 0 && v0) {
+      atomicAdd(&a.ctr[0], v0);
+      atomicAdd(&a.ctr[1], v1);
+      atomicAdd(&a.ctr[2], v2);
+    }
   }
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && lane == 0)
@@ -1036,6 +1212,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (scan_wave) atomicAdd(&a.ctr[31], scan_wave);
     atomicAdd(&a.ctr[28], scan_long);
     atomicAdd(&a.ctr[29], scan_long_pts);
+    // load balance: wave lifetimes (sum, max), steps of the busiest lane (max), waves
+    unsigned long long cmax = chain_steps;
+#pragma unroll
+    for (int q = 32; q > 0; q >>= 1) cmax = max(cmax, (unsigned long long)__shfl_xor((long long)cmax, q, 64));
+    if (lane == 0) {
+      const unsigned long long life = __builtin_amdgcn_s_memtime() - t_start;
+      atomicAdd(&a.ctr[24], life);
+      atomicMax(&a.ctr[25], life);
+      atomicMax(&a.ctr[26], cmax);
+      atomicAdd(&a.ctr[27], 1ull);
+    }
   }
 #endif
 }
@@ -1705,6 +1892,28 @@ hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, co
   return launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
 }
 
+hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
+                           const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
+                           float* ckey, int* ncand, int* ctie, float* seed) {
+  if (count <= 0 || B <= 0) return hipSuccess;
+  const int groups = (B + 255) / 256;
+  int nchunks = (count + 255) / 256;
+  const int want = max(1, 2048 / max(1, groups));
+  nchunks = max(1, min(nchunks, min(want, max_chunks)));
+  int chunk = (count + nchunks - 1) / nchunks;
+  chunk = (chunk + 255) & ~255;
+  nchunks = (count + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 255) / 256), dim3(256), 0, st, B, p.sort_limit, ckey, ncand, seed);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes + first, count, chunk,
+                     nchunks, p, fr, pk, pi, nullptr, nullptr, nullptr, nullptr, nullptr, seed, nullptr);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
+                     first, cand, ckey, ncand, ctie);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                 int* ncand) {
@@ -1768,28 +1977,32 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   return hipSuccess;
 }
 
-hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, void* prep, int* qnext, int* best,
                                      int blocks) {
-  if (a.njobs <= 0) return hipSuccess;
+  if (a0.njobs <= 0) return hipSuccess;
   hipError_t e;
   if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
   RollInit* pr = (RollInit*)prep;
-  const size_t lds = roll_lds_bytes(a);
-  const int nb = blocks < (a.njobs + 255) / 256 ? blocks : (a.njobs + 255) / 256;
+  const size_t lds = roll_lds_bytes(a0);
+  const int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
+  RollArgs a = a0;
+  a.cont_donors = nb * 3;  // waves 1..3 of each block (launch_bounds 256)
   if (a.p.need_gap) {
     hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL((k_roll_run<true>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
+    if (a.cont) hipLaunchKernelGGL((k_roll_run<true, true>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
+    else hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
+    const void* fn = a.cont ? (const void*)&k_roll_run<false, true> : (const void*)&k_roll_run<false, false>;
     if (lds > 64 * 1024) {
-      hipError_t e2 = hipFuncSetAttribute((const void*)&k_roll_run<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds);
+      hipError_t e2 = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e2 != hipSuccess) return e2;
     }
-    hipLaunchKernelGGL((k_roll_run<false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    if (a.cont) hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    else hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   }
   LAUNCH_CHECK();
   return hipSuccess;

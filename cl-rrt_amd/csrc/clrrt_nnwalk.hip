@@ -36,6 +36,7 @@
 // A skipped node, tile or super-tile can hold no pair that enters the list, so every list equals
 // the brute-force one bit for bit (ties included: pairs are ordered by (key, node index) in both).
 #include <hip/hip_runtime.h>
+#include <climits>
 #include <hip/hip_fp16.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -666,6 +667,73 @@ size_t walk_sort_bytes(int n) {
   return bytes > b2 ? bytes : b2;
 }
 
+// Inclusive max-scan of the run markers in three plain passes (tile scans, one-block scan of the tile
+// maxima, fix-up).  A single-pass look-back scan waits on its predecessor blocks, which starves when
+// the scan runs beside the rollout kernel (the pipelined rounds) and only a few CUs free up at a time.
+#define WSCAN_TILE 1024
+__global__ void __launch_bounds__(256) k_wscan_tiles(const int* __restrict__ in, int n, int* __restrict__ out,
+                                                     int* __restrict__ tmax) {
+  __shared__ int s_w[4];
+  const int base = blockIdx.x * WSCAN_TILE + threadIdx.x * 4;
+  int v[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) v[q] = base + q < n ? in[base + q] : INT_MIN;
+#pragma unroll
+  for (int q = 1; q < 4; q++) v[q] = max(v[q], v[q - 1]);
+  // inclusive scan of the threads' maxima within the wave, then across the 4 waves
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v[3];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x = max(x, y);
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int pre = INT_MIN;
+  for (int q = 0; q < wv; q++) pre = max(pre, s_w[q]);
+  int ex = __shfl_up(x, 1, 64);
+  if (lane == 0) ex = INT_MIN;
+  ex = max(ex, pre);
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (base + q < n) out[base + q] = max(v[q], ex);
+  if (threadIdx.x == 255) tmax[blockIdx.x] = max(x, pre);
+}
+
+__global__ void __launch_bounds__(1024) k_wscan_top(int* __restrict__ tmax, int nt) {
+  // exclusive max-scan of the tile maxima, one block (sequential chunks per thread)
+  __shared__ int s_t[1024];
+  const int per = (nt + 1023) / 1024;
+  const int b = threadIdx.x * per, e = min(nt, b + per);
+  int m = INT_MIN;
+  for (int i = b; i < e; i++) m = max(m, tmax[i]);
+  s_t[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int y = threadIdx.x >= o ? s_t[threadIdx.x - o] : INT_MIN;
+    __syncthreads();
+    s_t[threadIdx.x] = max(s_t[threadIdx.x], y);
+    __syncthreads();
+  }
+  int run = threadIdx.x > 0 ? s_t[threadIdx.x - 1] : INT_MIN;
+  for (int i = b; i < e; i++) {
+    const int t = tmax[i];
+    tmax[i] = run;
+    run = max(run, t);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_wscan_fix(int* __restrict__ out, int n, const int* __restrict__ tpre) {
+  const int t = blockIdx.x;
+  if (t == 0) return;
+  const int p = tpre[t];
+  for (int i = threadIdx.x; i < WSCAN_TILE; i += 256) {
+    const int j = t * WSCAN_TILE + i;
+    if (j < n) out[j] = max(out[j], p);
+  }
+}
+
 hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
                           const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
                           float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless) {
@@ -685,9 +753,16 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
                      w.P, w.Q, w.CE, w.ID, w.vals, w.TRIG);
   LAUNCH_CHECK3();
   // HEAD[j] = first record of j's run of equal key inputs (inclusive max-scan of dup markers)
-  bytes = w.tmp_bytes;
-  e = hipcub::DeviceScan::InclusiveScan(w.tmp, bytes, w.vals, w.HEAD, hipcub::Max(), Npad, st);
-  if (e != hipSuccess) return e;
+  {
+    const int nt = (Npad + WSCAN_TILE - 1) / WSCAN_TILE;
+    int* tmax = (int*)w.keys2;  // free between the two sorts
+    hipLaunchKernelGGL(k_wscan_tiles, dim3(nt), dim3(256), 0, st, w.vals, Npad, w.HEAD, tmax);
+    LAUNCH_CHECK3();
+    hipLaunchKernelGGL(k_wscan_top, dim3(1), dim3(1024), 0, st, tmax, nt);
+    LAUNCH_CHECK3();
+    hipLaunchKernelGGL(k_wscan_fix, dim3(nt), dim3(256), 0, st, w.HEAD, Npad, tmax);
+    LAUNCH_CHECK3();
+  }
   hipLaunchKernelGGL(k_walk_tiles, dim3((ntiles + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
                      fr.delta, nodes, fr.ox, fr.oy, w.tiles);
   LAUNCH_CHECK3();

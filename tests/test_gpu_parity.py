@@ -301,3 +301,29 @@ def test_nn_grid_matches_brute_force_large_tree():
         s = smp[j]
         cid, _ = o.sort_nodes(s.x, s.y, s.explore, stable=True)
         assert [int(i) for i in ids_g[j] if i >= 0] == cid, j
+
+
+@pytest.mark.gpu
+def test_pipelined_batch_rounds_identical():
+    """Full-size property: BATCH rounds with the next round's walk search overlapped with the current
+    round's rollouts (+ the merge of the appended nodes, launch_nn_delta), and rounds whose last
+    rollouts move between waves (roll_handoff), grow exactly the tree of plain rounds (every node
+    record and trajectory row)."""
+    mode, obs = _scene("obb200")
+    trees = []
+    for pipe, handoff in ((0, 0), (1, 0), (1, 1)):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
+                           max_batch=16384)
+        pl.set_option("nn_pipeline", pipe)
+        pl.set_option("roll_handoff", handoff)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(12), n_iters=16384 * 6, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+        assert st["rounds"] == 6
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n))
+        pl.close()
+    print(f"pipelined rounds: {trees[1][2]} nodes")
+    assert trees[0][2] > 20000
+    for t in trees[1:]:
+        assert trees[0][0] == t[0] and trees[0][1] == t[1]

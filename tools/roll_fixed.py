@@ -1,4 +1,4 @@
-"""Fixed-workload timing of one round's evaluation (nearest-node search + rollouts) on a cfg3 tree:
+"""Fixed-workload (argv[1] = rN: N growth rounds) timing of one round's evaluation (nearest-node search + rollouts) on a cfg3 tree:
 grow the tree for `ms`, then evaluate the same 16384 samples `reps` times without committing and
 report the per-launch kernel times (for A/B builds: CLRRT_LIB=...)."""
 import os, sys
@@ -8,13 +8,16 @@ import torch
 import clrrt
 from clrrt import abi, scenes
 
-ms = float(sys.argv[1]) if len(sys.argv) > 1 else 1000.0
+arg = sys.argv[1] if len(sys.argv) > 1 else "1000"
+# "r40": grow for exactly 40 rounds (same tree for every build); otherwise a wall budget in ms
+rounds = int(arg[1:]) if arg.startswith("r") else 0
+ms = 1e9 if rounds else float(arg)
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=8 << 20,
                    max_rows=1 << 28, max_batch=16384)
 pl.set_obstacles(scenes.urban_scene(200))
 pl.tree_init()
-st = pl.expand(clrrt.Rng(5), n_iters=0, budget_ms=ms, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+st = pl.expand(clrrt.Rng(5), n_iters=rounds * 16384, budget_ms=ms, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
 print("grown:", st, flush=True)
 smp = list(clrrt.Rng(77).draw_samples(pl.params, 16384))
 arr = (abi.Sample * len(smp))(*smp)

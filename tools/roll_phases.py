@@ -23,4 +23,7 @@ for nm, v in zip(names, ph):
     print(f"  {nm:32s} {v / max(1, tot) * 100:5.1f}%  {v / max(1, d[0]):8.1f} clk/step")
 print(f"scan: {d[30] / max(1, d[0]):.2f} points per lane-step, wave-level iterations {d[31]:,} "
       f"({d[31] * 64 / max(1, d[30]):.1f}x the lane average)")
-print(f"scans longer than 8 points: {d[28] / max(1, d[0]) * 100:.2f}% of lane-steps, {d[29] / max(1, d[28]):.1f} points each")
+print(f"active lanes per wave step {d[28] / max(1, d[29]):.1f}; wave steps {d[29]:,}, "
+      f"{d[29] / max(1, d[27]):.0f} per wave")
+print(f"waves {d[27]:,}: mean lifetime {d[24] / max(1, d[27]):,.0f} clk, max {d[25]:,} clk; busiest lane {d[26]} steps "
+      f"(max over all launches)")
