@@ -200,14 +200,17 @@ def main():
         nodes = goals = 0
         cap_stop = 0
         t0 = time.perf_counter()
+        first, count = cdist.shard(world * B, world, rank)
+        nxt = rng.draw_samples(pl.params, world * B)
         while True:
             n_now = pl.size()[0]
             if n_now + 2 * world * B > max_nodes:
                 cap_stop = 1
                 break
-            allsmp = rng.draw_samples(pl.params, world * B)
-            first, count = cdist.shard(world * B, world, rank)
+            allsmp, nxt = nxt, rng.draw_samples(pl.params, world * B)
             mine = (abi.Sample * count).from_buffer(allsmp, first * C_SAMPLE)
+            # the next round's shard is searched beside this round's rollouts (clrrt_round_prefetch)
+            pl.round_prefetch((abi.Sample * count).from_buffer(nxt, first * C_SAMPLE))
             n_local = pl.round_eval(mine, out_buf.data_ptr())
             cat, counts, my_first, t_max = cdist.exchange_round(out_buf, n_local,
                                                                 (time.perf_counter() - t0) * 1e3)

@@ -56,6 +56,7 @@ _SIGS = {
     "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "clrrt_round_prefetch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32]),
     "clrrt_rollout_batch": (C.c_int, [C.c_void_p, P(abi.RolloutJob), C.c_int32, P(abi.RolloutResult),
                                       P(C.c_double), C.c_int32]),
     "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_int32, P(C.c_int32), P(C.c_float)]),
@@ -311,6 +312,11 @@ class Planner:
         self._chk(self.L.clrrt_round_eval(self.h, samples, len(samples), C.c_void_p(dev_out_ptr), C.byref(n_out)),
                   "round_eval")
         return n_out.value
+
+    def round_prefetch(self, next_samples):
+        """Declare the next round_eval's samples: their search runs beside the coming round's rollouts
+        (results unchanged; the next round_eval must pass exactly these samples to use it)."""
+        self._chk(self.L.clrrt_round_prefetch(self.h, next_samples, len(next_samples)), "round_prefetch")
 
     def round_commit(self, dev_nodes_ptr, n, local_first=0, local_count=0):
         self._chk(self.L.clrrt_round_commit(self.h, C.c_void_p(dev_nodes_ptr), n, local_first, local_count),

@@ -140,6 +140,10 @@ struct clrrt_ctx {
   float* ckey2 = nullptr;
   int* ncand2 = nullptr;
   int* ctie2 = nullptr;
+  // clrrt_round_prefetch: declared next samples; pf_state 1 = their walk was launched (lists in the
+  // *2 buffers, merge pending), 2 = merged and swapped in for pf_samples
+  std::vector<clrrt_sample> pf_next, pf_samples;
+  int pf_state = 0;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -158,6 +162,8 @@ struct clrrt_ctx {
 };
 
 // ------------------------------------------------------------------------------------------ util
+static void pf_reset(clrrt_ctx* c);
+
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
@@ -548,6 +554,7 @@ int clrrt_set_rank(clrrt_ctx* c, int32_t rank) {
 
 int clrrt_set_params(clrrt_ctx* c, const clrrt_params* p) {
   if (!c || !p) return CLRRT_EINVAL;
+  pf_reset(c);
   DevParams d;
   derive(*p, d, c->n_obs);
   if (d.n_steps_max + 1 > c->slot_rows) {  // a smaller sim_dt needs longer rollout slots
@@ -721,6 +728,7 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
 
 int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
   if (!c || !root_state) return CLRRT_EINVAL;
+  pf_reset(c);
   HIPC(c, hipSetDevice(c->device));
   double* d_state = nullptr;
   HIPC(c, hipMalloc((void**)&d_state, 10 * sizeof(double)));
@@ -739,6 +747,7 @@ int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
 
 int clrrt_tree_load(clrrt_ctx* c, const clrrt_node* nodes, int64_t n) {
   if (!c || n < 0 || (n > 0 && !nodes)) return CLRRT_EINVAL;
+  pf_reset(c);
   if (n > c->cap.max_nodes) return fail(c, CLRRT_ECAPACITY, "tree_load: too many nodes");
   HIPC(c, hipSetDevice(c->device));
   if (n > 0) {
@@ -958,6 +967,7 @@ int clrrt_path_transform(clrrt_ctx* c, int32_t dir, const double pose[3]) {
 
 int clrrt_tree_init_from_path(clrrt_ctx* c, const double car_state[6], int32_t* outcome) {
   if (!c || !car_state) return CLRRT_EINVAL;
+  pf_reset(c);
   HIPC(c, hipSetDevice(c->device));
   int rc = path_reserve(c, std::max(1, c->path_n), std::max<int64_t>(1, c->path_nrows));
   if (rc != CLRRT_OK) return rc;
@@ -1212,6 +1222,50 @@ static bool walk_serves(clrrt_ctx* c, const NnSetup& su) {
   return !use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && su.region_ok;
 }
 
+// Any tree change other than clrrt_round_commit invalidates a prefetched search.
+static void pf_reset(clrrt_ctx* c) {
+  if (c->pf_state != 0 && c->side) hipStreamSynchronize(c->side);
+  c->pf_state = 0;
+  c->pf_next.clear();
+}
+
+// Launches the walk search of samples h2[0..n2) (host, pinned) over the current tree on the side
+// stream into the *2 buffers; eval_samples records ev_tree before its rollouts.
+static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
+  HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));
+  HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * n2, hipMemcpyHostToDevice, c->side));
+  {
+    KTimer kt(c, 0, c->side);
+    const int rw = ensure_walk(c);
+    if (rw != CLRRT_OK) return rw;
+    HIPC(c, launch_nn_walk(c->side, c->d_samples2, n2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1,
+                           su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
+                           c->nnw_stateless));
+  }
+  HIPC(c, hipEventRecord(c->ev_walk, c->side));
+  return CLRRT_OK;
+}
+
+// After the appended nodes [first_new, first_new + nn) are in the tree: merge them into the side
+// walk's lists and swap the *2 buffers in.
+static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
+  if (nn > 0) {
+    KTimer kt(c, 0);
+    const NnSetup su2 = nn_setup(c);  // the box includes the appended nodes
+    const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n2 * NN_K));
+    HIPC(c, launch_nn_delta(c->stream, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
+                            max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed));
+  }
+  std::swap(c->d_samples, c->d_samples2);
+  std::swap(c->h_samples, c->h_samples2);
+  std::swap(c->cand, c->cand2);
+  std::swap(c->ckey, c->ckey2);
+  std::swap(c->ncand, c->ncand2);
+  std::swap(c->ctie, c->ctie2);
+  return CLRRT_OK;
+}
+
 // Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
 static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   hipStream_t st = c->stream;
@@ -1379,10 +1433,31 @@ int clrrt_round_eval(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, void*
   HIPC(c, hipSetDevice(c->device));
   *n_out = 0;
   if (n == 0) return CLRRT_OK;
-  memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
-  HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
+  // lists prefetched by the previous round (clrrt_round_prefetch) serve exactly the declared samples
+  const bool have = c->pf_state == 2 && (int)c->pf_samples.size() == n &&
+                    memcmp(c->pf_samples.data(), samples, sizeof(clrrt_sample) * n) == 0;
+  if (!have) {
+    if (c->pf_state != 0 && c->side) HIPC(c, hipStreamSynchronize(c->side));
+    memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
+    HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
+  }
+  c->pf_state = 0;
+  const int n2 = (int)std::min<size_t>(c->pf_next.size(), (size_t)c->cap.max_batch);
+  NnSetup su{};
+  bool side = false;
+  if (n2 > 0 && c->nn_pipeline) {
+    su = nn_setup(c);
+    side = walk_serves(c, su);
+  }
+  auto during = [&]() -> int {
+    memcpy(c->h_samples2, c->pf_next.data(), sizeof(clrrt_sample) * n2);
+    c->pf_samples.assign(c->pf_next.begin(), c->pf_next.begin() + n2);
+    c->pf_state = 1;
+    return launch_side_walk(c, n2, su);
+  };
+  c->pf_next.clear();
   int L = n, rc;
-  if ((rc = eval_samples(c, n, false, &L)) != CLRRT_OK) return rc;
+  if ((rc = eval_samples(c, n, false, &L, have, side ? std::function<int()>(during) : nullptr)) != CLRRT_OK) return rc;
   int nn = 0;
   if ((rc = compact_and_copy(c, L, &nn, false)) != CLRRT_OK) return rc;
   if (dev_out && nn > 0)
@@ -1397,6 +1472,7 @@ int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t l
   (void)local_count;  // rows of local records were written to the arena by clrrt_round_eval
   if (!c || n < 0 || (n > 0 && !dev_nodes)) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
+  const int64_t first_new = c->n_nodes;
   int rc = append_nodes(c, (const clrrt_node*)dev_nodes, n);
   if (rc != CLRRT_OK) return rc;
   if (n > 0) {
@@ -1405,12 +1481,24 @@ int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t l
   }
   HIPC(c, hipStreamSynchronize(c->stream));
   if (n > 0) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+  if (c->pf_state == 1) {  // the next round's search ran beside this round's rollouts
+    if ((rc = merge_side_lists(c, (int)c->pf_samples.size(), first_new, n)) != CLRRT_OK) return rc;
+    c->pf_state = 2;
+  }
+  return CLRRT_OK;
+}
+
+int clrrt_round_prefetch(clrrt_ctx* c, const clrrt_sample* next, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !next)) return CLRRT_EINVAL;
+  if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
+  c->pf_next.assign(next, next + n);
   return CLRRT_OK;
 }
 
 int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
                  clrrt_stats* out) {
   if (!c || !rng || n_iters < 0 || (mode != CLRRT_MODE_EXACT && mode != CLRRT_MODE_BATCH)) return CLRRT_EINVAL;
+  pf_reset(c);
   if (n_iters == 0 && !(budget_ms > 0)) return CLRRT_EINVAL;
   if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
   HIPC(c, hipSetDevice(c->device));
@@ -1477,18 +1565,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
         pending.push_back(smp);
       }
       for (int j = 0; j < nb2; j++) c->h_samples2[j] = pending[nb + j];
-      HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));  // recorded before the rollouts (eval_samples)
-      HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * nb2, hipMemcpyHostToDevice, c->side));
-      {
-        KTimer kt(c, 0, c->side);
-        const int rw = ensure_walk(c);
-        if (rw != CLRRT_OK) return rw;
-        HIPC(c, launch_nn_walk(c->side, c->d_samples2, nb2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1,
-                               su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
-                               c->nnw_stateless));
-      }
-      HIPC(c, hipEventRecord(c->ev_walk, c->side));
-      return CLRRT_OK;
+      return launch_side_walk(c, nb2, su);
     };
     int L = nb, nn = 0;
     if ((rc = eval_samples(c, nb, exact, &L, have_next, nb2 > 0 ? std::function<int()>(prefetch) : nullptr)) != CLRRT_OK)
@@ -1509,20 +1586,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     have_next = false;
     if (nb2 > 0) {
-      HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
-      if (nn > 0) {
-        KTimer kt(c, 0);
-        const NnSetup su2 = nn_setup(c);  // the box now includes the appended nodes
-        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)nb2 * NN_K));
-        HIPC(c, launch_nn_delta(c->stream, c->d_samples2, nb2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
-                                max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed));
-      }
-      std::swap(c->d_samples, c->d_samples2);
-      std::swap(c->h_samples, c->h_samples2);
-      std::swap(c->cand, c->cand2);
-      std::swap(c->ckey, c->ckey2);
-      std::swap(c->ncand, c->ncand2);
-      std::swap(c->ctie, c->ctie2);
+      if ((rc = merge_side_lists(c, nb2, first_new, nn)) != CLRRT_OK) break;
       have_next = true;
     }
     for (int j = 0; j < L; j++) {
@@ -1548,6 +1612,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
 int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, clrrt_rollout_result* out,
                         double* rows_out, int32_t rows_cap) {
   if (!c || n < 0 || (n > 0 && (!jobs || !out))) return CLRRT_EINVAL;
+  pf_reset(c);
   if (rows_out && rows_cap < c->dp.n_steps_max + 1) return fail(c, CLRRT_EINVAL, "rows_cap < max steps + 1");
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
@@ -1621,6 +1686,7 @@ int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double*
 int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t mode, int32_t* out_ids,
                    float* out_keys) {
   if (!c || n < 0 || (n > 0 && (!samples || !out_ids))) return CLRRT_EINVAL;
+  pf_reset(c);
   if (mode != CLRRT_MODE_EXACT && mode != CLRRT_MODE_BATCH) return CLRRT_EINVAL;
   if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
   HIPC(c, hipSetDevice(c->device));

@@ -287,6 +287,12 @@ int clrrt_round_eval(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, voi
  * into the arena); records outside that slice are remote nodes whose rows stay on their owner. */
 int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t local_first,
                        int32_t local_count);
+/* Engine extension (no reference counterpart): declares the samples of the NEXT clrrt_round_eval.
+ * The coming clrrt_round_eval then runs their nearest-node search over the current tree beside its
+ * rollouts, and clrrt_round_commit merges the committed nodes into those lists, so the next
+ * clrrt_round_eval called with exactly these samples skips its search.  Results are identical to
+ * calls without it; any other tree change discards the prefetch. */
+int clrrt_round_prefetch(clrrt_ctx* ctx, const clrrt_sample* next_samples, int32_t n);
 
 /* ---- kernel-level parity entries ---- */
 int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n,

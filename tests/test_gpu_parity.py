@@ -327,3 +327,33 @@ def test_pipelined_batch_rounds_identical():
     assert trees[0][2] > 20000
     for t in trees[1:]:
         assert trees[0][0] == t[0] and trees[0][1] == t[1]
+
+
+@pytest.mark.gpu
+def test_round_prefetch_identical():
+    """The multi-GPU round API with clrrt_round_prefetch (the next shard's search beside this round's
+    rollouts, merged with the committed nodes) grows exactly the tree of plain round_eval/commit."""
+    import torch
+    mode, obs = _scene("obb200")
+    B, rounds = 16384, 5
+    trees = []
+    for pre in (False, True):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
+                           max_batch=B)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        out = torch.empty((2 * B, 160), dtype=torch.uint8, device="cuda")
+        rng = clrrt.Rng(14)
+        nxt = rng.draw_samples(pl.params, B)
+        for _ in range(rounds):
+            cur, nxt = nxt, rng.draw_samples(pl.params, B)
+            if pre:
+                pl.round_prefetch(nxt)
+            n = pl.round_eval(cur, out.data_ptr())
+            pl.round_commit(out.data_ptr(), n, 0, n)
+        n_nodes, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n_nodes))
+        pl.close()
+    print(f"round prefetch: {trees[1][2]} nodes")
+    assert trees[0][2] > 20000
+    assert trees[0][0] == trees[1][0] and trees[0][1] == trees[1][1]
