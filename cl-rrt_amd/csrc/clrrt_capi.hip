@@ -1101,6 +1101,19 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_handoff") c->roll_handoff = value != 0;
+  else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
+    int lo = 0, hi = 0;
+    HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPC(c, hipStreamSynchronize(c->side));
+    HIPC(c, hipStreamDestroy(c->side));
+    const int pr = value > 0 ? hi : value < 0 ? lo : 0;
+    HIPC(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, pr));
+    if (value < 0 && c->own_stream) {  // and the main stream gets the highest priority
+      HIPC(c, hipStreamSynchronize(c->stream));
+      HIPC(c, hipStreamDestroy(c->stream));
+      HIPC(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+    }
+  }
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
   return CLRRT_OK;
 }
