@@ -650,6 +650,10 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   if (pc) pc->mark(2);
   glibc::sincos(r.x2, r.s2, r.c2);
   r.t3 = glibc::tan(r.x3);
+#if CLRRT_EARLY_CS
+  r.cwp = glibc::cos(r.x2);  // independent of sincos / tan: their latencies overlap
+  r.swp = glibc::sin(r.x2);
+#endif
 #ifdef CLRRT_DUP_TRIG  // diagnostics: the phase evaluated twice (same values) to measure its cost
   {
     double z = 0.0;
