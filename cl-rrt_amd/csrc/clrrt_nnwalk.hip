@@ -286,6 +286,21 @@ __device__ __forceinline__ float walk_lb(const WalkTile& w, float rsx, float rsy
   return lb == lb ? lb : -__builtin_inff();
 }
 
+// The distance-only part of walk_lb (no feasibility cone, no turning bound): walk_lb >= walk_lb_dist.
+#ifndef WALK_CHEAP_FIRST
+#define WALK_CHEAP_FIRST 1
+#endif
+__device__ __forceinline__ float walk_lb_dist(const WalkTile& w, float rsx, float rsy, bool ex, float dsR = 0.f) {
+  if (w.nonfinite) return -__builtin_inff();
+  if (w.pr < 0.f) return __builtin_inff();
+  const float dx = rsx - w.pcx, dy = rsy - w.pcy;
+  const float D = fsqrt(dx * dx + dy * dy);
+  float lb = D - w.pr;
+  lb = lb - 2e-3f - 1e-5f * fabsf(lb);
+  if (!ex) lb = fmaxf(fmaxf(w.aopt + D * (1.f - 1e-5f) - 2e-3f, w.cemin + lb), w.eroot + dsR);
+  return lb == lb ? lb : -__builtin_inff();
+}
+
 // Wave-uniform values kept in scalar registers.
 __device__ __forceinline__ float uni(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -535,7 +550,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     uint64_t tm;
     if constexpr (STATE) {
       const uint32_t vis = st >= 0 ? s_vis[st] : 0xffffffffu;
-      if (st >= 0 && tl < ntiles && !((vis >> (lane & 31)) & 1u)) lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
+      if (st >= 0 && tl < ntiles && !((vis >> (lane & 31)) & 1u)) {
+#if WALK_CHEAP_FIRST
+        // the distance-only part of the bound first: a tile it already places beyond min(T, kth) skips the
+        // feasibility / turning terms (their arccosines); the weaker value is still a valid bound for
+        // the super-tile's rest (a state tile is never taken twice: visited mask)
+        const WalkTile tt = tiles[tl];
+        lb = walk_lb_dist(tt, rsx, rsy, ex, dsR);
+        if (!(lb > fminf(T, kth))) lb = walk_lb(tt, rsx, rsy, ex, flen_t, dsR);
+#else
+        lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
+#endif
+      }
       const bool take = st >= 0 && lb <= T && !(lb > kth);
       const bool drop = st >= 0 && lb > kth;  // never needed again (kth only decreases)
       tm = __ballot(take);
