@@ -1244,16 +1244,24 @@ static void pf_reset(clrrt_ctx* c) {
 
 // Launches the walk search of samples h2[0..n2) (host, pinned) over the current tree on the side
 // stream into the *2 buffers; eval_samples records ev_tree before its rollouts.
+// The index is built on the main stream before the rollouts (its radix sort's look-back passes starve
+// beside the rollout kernel on large trees: 3+ ms instead of 0.2), the search runs on the side stream.
+static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
+  KTimer kt(c, 0);
+  const int rw = ensure_walk(c);
+  if (rw != CLRRT_OK) return rw;
+  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw));
+  return CLRRT_OK;
+}
+
 static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
   HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));
   HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * n2, hipMemcpyHostToDevice, c->side));
   {
     KTimer kt(c, 0, c->side);
-    const int rw = ensure_walk(c);
-    if (rw != CLRRT_OK) return rw;
-    HIPC(c, launch_nn_walk(c->side, c->d_samples2, n2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1,
-                           su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
-                           c->nnw_stateless));
+    HIPC(c, launch_nn_walk_search(c->side, c->d_samples2, n2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0,
+                                  su.x1, su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
+                                  c->nnw_stateless));
   }
   HIPC(c, hipEventRecord(c->ev_walk, c->side));
   return CLRRT_OK;
@@ -1329,7 +1337,8 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
 // samples to commit (n in BATCH mode).  have_lists: the candidate lists are already in c->cand
 // (pipelined rounds); during_roll runs right after the rollout kernel's launch.
 static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_lists = false,
-                        const std::function<int()>& during_roll = nullptr) {
+                        const std::function<int()>& during_roll = nullptr,
+                        const std::function<int()>& pre_roll = nullptr) {
   hipStream_t st = c->stream;
   KeyId* scratch = nullptr;
   if (exact) {
@@ -1343,6 +1352,10 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
   }
   // the tree, this round's lists and the walk buffers are final here: work queued by during_roll on
   // another stream waits for this point only, not for the rollouts
+  if (pre_roll) {
+    int rc = pre_roll();
+    if (rc != CLRRT_OK) return rc;
+  }
   if (during_roll) HIPC(c, hipEventRecord(c->ev_tree, st));
   {
     KTimer kt(c, 1);
@@ -1470,7 +1483,10 @@ int clrrt_round_eval(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, void*
   };
   c->pf_next.clear();
   int L = n, rc;
-  if ((rc = eval_samples(c, n, false, &L, have, side ? std::function<int()>(during) : nullptr)) != CLRRT_OK) return rc;
+  auto build = [&]() -> int { return pre_roll_build(c, su); };
+  if ((rc = eval_samples(c, n, false, &L, have, side ? std::function<int()>(during) : nullptr,
+                         side ? std::function<int()>(build) : nullptr)) != CLRRT_OK)
+    return rc;
   int nn = 0;
   if ((rc = compact_and_copy(c, L, &nn, false)) != CLRRT_OK) return rc;
   if (dev_out && nn > 0)
@@ -1581,7 +1597,9 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
       return launch_side_walk(c, nb2, su);
     };
     int L = nb, nn = 0;
-    if ((rc = eval_samples(c, nb, exact, &L, have_next, nb2 > 0 ? std::function<int()>(prefetch) : nullptr)) != CLRRT_OK)
+    auto build = [&]() -> int { return pre_roll_build(c, su); };
+    if ((rc = eval_samples(c, nb, exact, &L, have_next, nb2 > 0 ? std::function<int()>(prefetch) : nullptr,
+                           nb2 > 0 ? std::function<int()>(build) : nullptr)) != CLRRT_OK)
       break;
     if (!exact) {
       // BATCH rounds commit every sample, so the next round's samples are known now: draw them

@@ -182,6 +182,13 @@ size_t walk_sort_bytes(int n);
 hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
                           const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
                           float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless);
+// launch_nn_walk's two halves: the index of nodes [0, N), then the search of samples over it
+hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const NnFrame& fr, double x0, double y0,
+                                double x1, double y1, WalkBufs& w);
+hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                 const DevParams& p, const NnFrame& fr, double x0, double y0, double x1, double y1,
+                                 WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
+                                 bool stateless);
 // Pipelined BATCH rounds: merges into (cand, ckey, ncand) -- the lists over nodes [0, first) -- the
 // nodes [first, first + count) appended since (k_nn_partial over them + k_nn_merge_delta).
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,

@@ -764,6 +764,15 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
                           const NnFrame& fr, double x0, double y0, double x1, double y1, WalkBufs& w, int* cand,
                           float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless) {
   if (N <= 0 || B <= 0) return hipSuccess;
+  hipError_t e = launch_nn_walk_build(st, nodes, N, fr, x0, y0, x1, y1, w);
+  if (e != hipSuccess) return e;
+  return launch_nn_walk_search(st, S, B, nodes, N, p, fr, x0, y0, x1, y1, w, cand, ckey, ncand, ctie, stats, stateless);
+}
+
+// The place-ordered index of nodes [0, N) (Morton sort, gathered records, run heads, tile bounds).
+hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const NnFrame& fr, double x0, double y0,
+                                double x1, double y1, WalkBufs& w) {
+  if (N <= 0) return hipSuccess;
   const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   const double span = fmax(x1 - x0, y1 - y0);
@@ -795,6 +804,21 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
   hipLaunchKernelGGL(k_walk_tiles, dim3((nsup + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, nsup,
                      WALK_TILE * WALK_SUPER, fr.delta, nodes, fr.ox, fr.oy, w.supers);
   LAUNCH_CHECK3();
+  return hipSuccess;
+}
+
+// The walk search of samples S[0, B) over the index launch_nn_walk_build made of nodes [0, N).
+hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                 const DevParams& p, const NnFrame& fr, double x0, double y0, double x1, double y1,
+                                 WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
+                                 bool stateless) {
+  if (N <= 0 || B <= 0) return hipSuccess;
+  const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
+  const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
+  const double span = fmax(x1 - x0, y1 - y0);
+  const double scale = span > 0 ? 65535.0 / span : 1.0;
+  hipError_t e = hipSuccess;
+  size_t bytes = 0;
   // per-sample LDS: 8 B per super-tile with state, 2 B without; state while it costs no occupancy
   const bool state = nsup <= 1280 && !stateless;
   const size_t lds = (state ? 2 * sizeof(float) : sizeof(__half)) * (size_t)nsup;
