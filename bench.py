@@ -76,9 +76,18 @@ def measured_traffic():
     try:
         f = json.load(open(fetch[-1]))
         w = json.load(open(write[-1]))
+        def per_dispatch(summary, prefix, counter):
+            # every template instantiation of the kernel (e.g. k_roll_run<false, false>), weighted
+            # by its dispatch count
+            rows = [v for k, v in summary.items() if k.startswith(prefix + "<")]
+            n = sum(v["dispatches"] for v in rows)
+            if not n:
+                raise KeyError(prefix)
+            return sum(v["total"][counter] for v in rows) / n
+
         kb = 0.0
-        for name in ("void clrrt::k_roll_prep<false>", "void clrrt::k_roll_run<false>"):
-            kb += 2.0 * f[name]["per_dispatch"]["FETCH_SIZE"] + w[name]["per_dispatch"]["WRITE_SIZE"]
+        for name in ("void clrrt::k_roll_prep", "void clrrt::k_roll_run"):
+            kb += 2.0 * per_dispatch(f, name, "FETCH_SIZE") + per_dispatch(w, name, "WRITE_SIZE")
         return kb * 1024.0, (f"{os.path.basename(fetch[-1])} + {os.path.basename(write[-1])}: "
                              "(2 x FETCH_SIZE [gfx950 half-count correction] + WRITE_SIZE) KiB per launch")
     except (KeyError, OSError, ValueError) as e:
