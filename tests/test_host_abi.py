@@ -70,3 +70,19 @@ def test_create_without_gpu_fails_loudly():
     except clrrt.ClrrtError:
         return
     raise AssertionError("Planner() must raise without a HIP device")
+
+
+def test_bench_reads_committed_pmc_traffic():
+    """bench.py's roofline.traffic comes from the newest committed FETCH_SIZE/WRITE_SIZE summaries;
+    the kernel names carry template arguments that change between builds (k_roll_run<false, false>),
+    so the reader must match every instantiation rather than one spelling."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("clrrt_bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    traffic, note = bench.measured_traffic()
+    assert traffic is not None, note
+    # a cfg3 rollout launch writes ~0.4-0.5 GB of trajectory rows
+    assert 1e8 < traffic < 5e9, (traffic, note)
