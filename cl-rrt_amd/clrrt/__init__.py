@@ -62,6 +62,7 @@ _SIGS = {
     "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_int32, P(C.c_int32), P(C.c_float)]),
     "clrrt_selftest_math": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double), C.c_int32,
                                       P(C.c_double)]),
+    "clrrt_selftest_units": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), C.c_int32, P(C.c_double)]),
     "clrrt_get_counters": (C.c_int, [C.c_void_p, P(abi.Counters)]),
     "clrrt_reset_counters": (C.c_int, [C.c_void_p]),
     "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
@@ -370,6 +371,18 @@ class Planner:
         self._chk(self.L.clrrt_selftest_math(self.h, fn, a.ctypes.data_as(P(C.c_double)),
                                              b.ctypes.data_as(P(C.c_double)), len(a),
                                              out.ctypes.data_as(P(C.c_double))), "selftest_math")
+        return out
+
+    # in/out widths per CLRRT_UNIT_* (include/clrrt.h)
+    UNIT_IN = {0: 11, 1: 9, 2: 9, 3: 12, 4: 2}
+    UNIT_OUT = {0: 1, 1: 8, 2: 1, 3: 1 + 3 * abi.UNIT_PROFILE_NMAX, 4: 2}
+
+    def selftest_units(self, unit, cases):
+        """Device evaluation of a hot-path unit (clrrt_selftest_units): cases [n, UNIT_IN] -> [n, UNIT_OUT]."""
+        cases = np.ascontiguousarray(cases, dtype=np.float64).reshape(-1, self.UNIT_IN[unit])
+        out = np.zeros((cases.shape[0], self.UNIT_OUT[unit]))
+        self._chk(self.L.clrrt_selftest_units(self.h, unit, cases.ctypes.data_as(P(C.c_double)), cases.shape[0],
+                                              out.ctypes.data_as(P(C.c_double))), "selftest_units")
         return out
 
     def work_counters(self):

@@ -6,6 +6,8 @@ header documents so a drift between the two fails at import time.
 import ctypes as C
 
 CLRRT_ABI_VERSION = 6  # include/clrrt.h
+UNIT_OBB, UNIT_ODE, UNIT_LATERAL, UNIT_PROFILE, UNIT_ANGLE = 0, 1, 2, 3, 4  # CLRRT_UNIT_*
+UNIT_PROFILE_NMAX = 1024
 CLRRT_MODE_EXACT = 0
 CLRRT_PARENT_PREV = -2  # goal-biased record: parent = the record before it (include/clrrt.h)
 CLRRT_MODE_BATCH = 1

@@ -679,6 +679,37 @@ static int build_grid(clrrt_ctx* c, const std::vector<BakedObs>& b) {
   return CLRRT_OK;
 }
 
+// getOBBvector old_collisioncheck.cpp:14-16 + OBB::setVertices/setNorms :56-76 for one obstacle, hoisted
+// out of the step loop: the float products (P, Q, R, S) always, the float SAT geometry of a static one.
+static void bake_obstacle(const clrrt_obstacle& o, BakedObs& d) {
+  memset(&d, 0, sizeof(d));
+  float w = (float)(o.size_x / 2), h = (float)(o.size_y / 2), th = (float)o.theta;
+  float cf, sf;
+  ::sincosf(th, &sf, &cf);  // OBB::setVertices: float cos/sin of one argument -> glibc sincosf
+  float hh = h / 2, ww = w / 2;
+  d.P = cf * hh; d.Q = sf * ww; d.R = sf * hh; d.S = cf * ww;
+  d.cx = o.cx; d.cy = o.cy; d.vlx = o.vx; d.vly = o.vy;
+  d.moving = (o.vx != 0.0 || o.vy != 0.0);
+  // static geometry: centre + 0*t (t >= 0) == centre + 0.0
+  double px = o.cx + 0.0, py = o.cy + 0.0;
+  d.vx[0] = (float)((px + (double)d.P) - (double)d.Q);
+  d.vy[0] = (float)((py + (double)d.R) + (double)d.S);
+  d.vx[1] = (float)((px + (double)d.P) - (double)(-d.Q));
+  d.vy[1] = (float)((py + (double)d.R) + (double)(-d.S));
+  d.vx[2] = (float)((px + (double)(-d.P)) - (double)(-d.Q));
+  d.vy[2] = (float)((py + (double)(-d.R)) + (double)(-d.S));
+  d.vx[3] = (float)((px + (double)(-d.P)) - (double)d.Q);
+  d.vy[3] = (float)((py + (double)(-d.R)) + (double)d.S);
+  for (int k = 0; k < 3; k++) {
+    d.nx[k] = d.vy[k + 1] - d.vy[k];
+    d.ny[k] = -(d.vx[k + 1] - d.vx[k]);
+  }
+  d.nx[3] = d.vy[0] - d.vy[3];
+  d.ny[3] = -(d.vx[0] - d.vx[3]);
+  d.bcx = (float)o.cx; d.bcy = (float)o.cy;
+  d.brad = std::sqrt(hh * hh + ww * ww);
+}
+
 extern "C" {
 
 // getOBBvector old_collisioncheck.cpp:6-22, evaluated once per query instead of once per step.
@@ -687,35 +718,7 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
   if (m > c->cap.max_obstacles) return fail(c, CLRRT_ECAPACITY, "too many obstacles");
   if (m > 1400) return fail(c, CLRRT_ECAPACITY, "at most 1400 obstacles (rollout LDS cull table)");
   std::vector<BakedObs> b(m);
-  for (int i = 0; i < m; i++) {
-    BakedObs& d = b[i];
-    memset(&d, 0, sizeof(d));
-    float w = (float)(o[i].size_x / 2), h = (float)(o[i].size_y / 2), th = (float)o[i].theta;
-    float cf, sf;
-    ::sincosf(th, &sf, &cf);  // OBB::setVertices: float cos/sin of one argument -> glibc sincosf
-    float hh = h / 2, ww = w / 2;
-    d.P = cf * hh; d.Q = sf * ww; d.R = sf * hh; d.S = cf * ww;
-    d.cx = o[i].cx; d.cy = o[i].cy; d.vlx = o[i].vx; d.vly = o[i].vy;
-    d.moving = (o[i].vx != 0.0 || o[i].vy != 0.0);
-    // static geometry: centre + 0*t (t >= 0) == centre + 0.0
-    double px = o[i].cx + 0.0, py = o[i].cy + 0.0;
-    d.vx[0] = (float)((px + (double)d.P) - (double)d.Q);
-    d.vy[0] = (float)((py + (double)d.R) + (double)d.S);
-    d.vx[1] = (float)((px + (double)d.P) - (double)(-d.Q));
-    d.vy[1] = (float)((py + (double)d.R) + (double)(-d.S));
-    d.vx[2] = (float)((px + (double)(-d.P)) - (double)(-d.Q));
-    d.vy[2] = (float)((py + (double)(-d.R)) + (double)(-d.S));
-    d.vx[3] = (float)((px + (double)(-d.P)) - (double)d.Q);
-    d.vy[3] = (float)((py + (double)(-d.R)) + (double)d.S);
-    for (int k = 0; k < 3; k++) {
-      d.nx[k] = d.vy[k + 1] - d.vy[k];
-      d.ny[k] = -(d.vx[k + 1] - d.vx[k]);
-    }
-    d.nx[3] = d.vy[0] - d.vy[3];
-    d.ny[3] = -(d.vx[0] - d.vx[3]);
-    d.bcx = (float)o[i].cx; d.bcy = (float)o[i].cy;
-    d.brad = std::sqrt(hh * hh + ww * ww);
-  }
+  for (int i = 0; i < m; i++) bake_obstacle(o[i], b[i]);
   HIPC(c, hipSetDevice(c->device));
   if (m > 0) {
     HIPC(c, hipMemcpyAsync(c->obs, b.data(), sizeof(BakedObs) * m, hipMemcpyHostToDevice, c->stream));
@@ -1711,6 +1714,41 @@ int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double*
   hipFree(db);
   hipFree(dout);
   if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("selftest_math: ") + hipGetErrorString(e));
+  return CLRRT_OK;
+}
+
+int clrrt_selftest_units(clrrt_ctx* c, int32_t unit, const double* in, int32_t n, double* out) {
+  static const int kin[5] = {11, 9, 9, 12, 2};
+  static const int kout[5] = {1, 8, 1, 1 + 3 * CLRRT_UNIT_PROFILE_NMAX, 2};
+  if (!c || n < 0 || (n > 0 && (!in || !out)) || unit < 0 || unit > 4) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  const size_t nin = (size_t)kin[unit] * n, nout = (size_t)kout[unit] * n;
+  std::vector<BakedObs> baked;
+  if (unit == CLRRT_UNIT_OBB) {
+    baked.resize(n);
+    for (int i = 0; i < n; i++) {
+      const double* a = in + 11 * (size_t)i;
+      clrrt_obstacle o = {a[4], a[5], a[6], a[7], a[8], a[9], a[10]};
+      bake_obstacle(o, baked[i]);
+    }
+  }
+  double *din = nullptr, *dout = nullptr;
+  BakedObs* dobs = nullptr;
+  hipError_t e = hipMalloc((void**)&din, sizeof(double) * nin);
+  if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * nout);
+  if (e == hipSuccess && !baked.empty()) e = hipMalloc((void**)&dobs, sizeof(BakedObs) * baked.size());
+  if (e == hipSuccess) e = hipMemcpyAsync(din, in, sizeof(double) * nin, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && dobs)
+    e = hipMemcpyAsync(dobs, baked.data(), sizeof(BakedObs) * baked.size(), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(dout, 0, sizeof(double) * nout, c->stream);
+  if (e == hipSuccess) e = launch_selftest_units(c->stream, unit, din, dobs, n, c->dp, dout);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(din);
+  hipFree(dout);
+  if (dobs) hipFree(dobs);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("selftest_units: ") + hipGetErrorString(e));
   return CLRRT_OK;
 }
 

@@ -462,11 +462,7 @@ __device__ __forceinline__ float obs_sat_static(const Box4& veh, const ObsView& 
 }
 
 __device__ __forceinline__ float obs_sat(const Box4& veh, const ObsView& ov, int j, double t) {
-  const BakedObs& o = ov.g[j];
-  if (!o.moving) return sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
-  float bvx[4], bvy[4], bnx[4], bny[4];
-  box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
-  return sat_gap(veh, bvx, bvy, bnx, bny);
+  return obs_sat_baked(veh, ov.g[j], t);
 }
 
 __device__ __forceinline__ float obs_gap(const Box4& veh, const ObsView& ov, int j, double t, float ft,
@@ -484,11 +480,7 @@ __device__ __forceinline__ float obs_gap(const Box4& veh, const ObsView& ov, int
     const float vr = VEH_RAD + CULL_MARGIN;
     if (e1 * e1 + e2 * e2 > vr * vr) { culled = true; return 1.0f; }
   }
-  const BakedObs& o = ov.g[j];
-  if (!o.moving) return sat_gap(veh, o.vx, o.vy, o.nx, o.ny);
-  float bvx[4], bvy[4], bnx[4], bny[4];
-  box_from(o.cx + o.vlx * t, o.cy + o.vly * t, o.P, o.Q, o.R, o.S, bvx, bvy, bnx, bny);
-  return sat_gap(veh, bvx, bvy, bnx, bny);
+  return obs_sat_baked(veh, ov.g[j], t);
 }
 
 // checkObsDistance (stub collisioncheck.cpp:6-8 | OBB old_collisioncheck.cpp:24-51).
@@ -503,7 +495,6 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
   if (p.coll_mode == CLRRT_COLLISION_STUB) return 100.0;
   const double t = p.obs_use_pred ? r.x6 : 0.0;
   const double vpx = r.x0 + 1.424 * r.c2, vpy = r.x1 + 1.424 * r.s2;
-  const float hh = 4.848f / 2, ww = 2.0f / 2;
   const float fvx = (float)vpx, fvy = (float)vpy, ft = (float)t;
   Box4 veh;
   if (!NEED_GAP && ov.gw > 0 && isfinite(fvx) && isfinite(fvy) && isfinite(ft)) {
@@ -525,9 +516,7 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
         const bool c1 = !two || obs_culled(ov, j1, ft, fvx, fvy);
         if (c0 && c1) continue;
         if (!have_veh) {
-          const float of = (float)r.x2;
-          const float cf = cosf(of), sf = sinf(of);
-          box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
+          veh_box(vpx, vpy, r.x2, veh);
           have_veh = true;
         }
         if (!c0 && obs_sat_static(veh, ov, j0) == 0) { tests += j0 + 1; return 0.0; }
@@ -545,9 +534,7 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
       if (ja < jb) { j = ja; a++; mv = false; } else { j = jb; b++; mv = true; }
       if (obs_culled(ov, j, ft, fvx, fvy)) continue;
       if (!have_veh) {
-        const float of = (float)r.x2;
-        const float cf = cosf(of), sf = sinf(of);
-        box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
+        veh_box(vpx, vpy, r.x2, veh);
         have_veh = true;
       }
       if ((mv ? obs_sat(veh, ov, j, t) : obs_sat_static(veh, ov, j)) == 0) { tests += j + 1; return 0.0; }
@@ -555,11 +542,7 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
     tests += ov.n;  // the reference tests every obstacle until the first overlap
     return 10000;
   }
-  {
-    const float of = (float)r.x2;
-    const float cf = cosf(of), sf = sinf(of);
-    box_from(vpx, vpy, cf * hh, sf * ww, sf * hh, cf * ww, veh.vx, veh.vy, veh.nx, veh.ny);
-  }
+  veh_box(vpx, vpy, r.x2, veh);
   double best = 10000;
   for (int j = 0; j < ov.n; j++) {
     bool culled;
@@ -628,32 +611,13 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   double E = prof_v(r.P, r.wp + 2) - r.x4;
   r.iE = r.iE + E * p.dt;
   double ac = satd(p.amin, p.amax, p.Kp * E + p.Ki * r.iE);
-  // VehicleODE (simulation.cpp:11-25)
-  double q = r.x4 / p.Vch;
-  double Gss = 1 / (1 + q * q);
-  double d0 = r.x4 * r.c2, d1 = r.x4 * r.s2;
-  double d2 = (r.x4 / p.L) * r.t3 * Gss;
-  double d3 = (1 / p.Td) * (dc - r.x3);
-  double d4 = r.x5;
-  double d5 = (1 / p.Ta) * (ac - r.x5);
-  d4 = satd(p.amin, p.amax, d4);
-  d3 = satd(-p.ddmax, p.ddmax, d3);
-  // IntegrateEuler (simulation.cpp:27-34)
-  r.x0 = r.x0 + d0 * p.dt;
-  r.x1 = r.x1 + d1 * p.dt;
-  r.x2 = r.x2 + d2 * p.dt;
-  r.x3 = r.x3 + d3 * p.dt;
-  r.x4 = r.x4 + d4 * p.dt;
-  r.x5 = r.x5 + d5 * p.dt;
-  r.x6 = r.x6 + 1.0 * p.dt;
-  r.x3 = satd(-p.dmax, p.dmax, r.x3);
+  // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
+  const double d2 = ode_euler(r, p, dc, ac);
   if (pc) pc->mark(2);
   glibc::sincos(r.x2, r.s2, r.c2);
   r.t3 = glibc::tan(r.x3);
-#if CLRRT_EARLY_CS
   r.cwp = glibc::cos(r.x2);  // independent of sincos / tan: their latencies overlap
   r.swp = glibc::sin(r.x2);
-#endif
 #ifdef CLRRT_DUP_TRIG  // diagnostics: the phase evaluated twice (same values) to measure its cost
   {
     double z = 0.0;
@@ -1740,6 +1704,68 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
   out[i] = r;
 }
 
+// Hot-path units exactly as the kernels evaluate them, one case per lane (test hook: bit-compared with
+// the reference's own code through tests/golden/ref_units.npz).  Formats: clrrt_selftest_units.
+__global__ void k_selftest_units(int unit, const double* __restrict__ in, const BakedObs* __restrict__ obs, int n,
+                                 DevParams p, double* __restrict__ out) {
+  glibc::stage_tables();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (unit) {
+    case CLRRT_UNIT_OBB: {  // checkObsDistance's vehicle box vs one obstacle (getOBBdist)
+      const double* a = in + 11 * (int64_t)i;
+      double s2, c2;
+      glibc::sincos(a[2], s2, c2);
+      Box4 veh;
+      veh_box(a[0] + 1.424 * c2, a[1] + 1.424 * s2, a[2], veh);
+      out[i] = (double)obs_sat_baked(veh, obs[i], a[3]);
+    } break;
+    case CLRRT_UNIT_ODE: {  // VehicleODE + IntegrateEuler
+      const double* a = in + 9 * (int64_t)i;
+      Roll r;
+      r.x0 = a[0]; r.x1 = a[1]; r.x2 = a[2]; r.x3 = a[3]; r.x4 = a[4]; r.x5 = a[5]; r.x6 = a[6];
+      r.cwp = glibc::cos(r.x2);
+      r.swp = glibc::sin(r.x2);
+      r.t3 = glibc::tan(r.x3);
+      const double d2 = ode_euler(r, p, a[7], a[8]);
+      double* o = out + 8 * (int64_t)i;
+      o[0] = r.x0; o[1] = r.x1; o[2] = r.x2; o[3] = r.x3; o[4] = r.x4; o[5] = r.x5; o[6] = r.x6; o[7] = d2;
+    } break;
+    case CLRRT_UNIT_LATERAL: {  // transformToVehicle + interpolate
+      const double* a = in + 9 * (int64_t)i;
+      double s, c;
+      glibc::sincos(a[8], s, c);
+      out[i] = transform_interp(a, a + 3, a[6], a[7], c, s);
+    } break;
+    case CLRRT_UNIT_PROFILE: {  // getReference's line + generateVelocityProfile
+      const double* a = in + 12 * (int64_t)i;
+      DevParams q = p;
+      q.ref_res = a[4]; q.vmax = a[6];
+      q.g0 = a[7]; q.g1 = a[8]; q.g2 = a[9]; q.g3 = a[10];
+      RefD R = make_ref(a[0], a[1], a[2], a[3], q);
+      double* row = out + (int64_t)(1 + 3 * CLRRT_UNIT_PROFILE_NMAX) * i;
+      row[0] = (double)R.N;
+      double x = R.a1x, y = R.a1y;
+      for (int j = 0; j < R.N; j++) {
+        if (j < CLRRT_UNIT_PROFILE_NMAX) {
+          row[1 + CLRRT_UNIT_PROFILE_NMAX + j] = x;
+          row[1 + 2 * CLRRT_UNIT_PROFILE_NMAX + j] = y;
+        }
+        if (j == R.N - 1) { R.bx = x; R.by = y; }
+        ref_next(R, j, x, y);
+      }
+      const Prof P = make_profile(R, a[5], q, a[11] != 0.0);
+      for (int j = 0; j < R.N && j < CLRRT_UNIT_PROFILE_NMAX; j++) row[1 + j] = prof_v(P, j);
+    } break;
+    case CLRRT_UNIT_ANGLE: {  // angleDiff, wrapToPi
+      const double* a = in + 2 * (int64_t)i;
+      out[2 * (int64_t)i] = angle_diff(a[0], a[1]);
+      out[2 * (int64_t)i + 1] = wrap_pi(a[0]);
+    } break;
+    default: break;
+  }
+}
+
 // ============================================================================================
 // launch wrappers (host)
 // ============================================================================================
@@ -2080,6 +2106,14 @@ hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t ba
 hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, st, fn, a, b, n, out);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_selftest_units(hipStream_t st, int unit, const double* in, const BakedObs* obs, int n,
+                                 const DevParams& p, double* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_selftest_units, dim3((n + 255) / 256), dim3(256), 0, st, unit, in, obs, n, p, out);
   LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -309,6 +309,25 @@ int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32
  * 16 sin and 17 cos of glibc's generic sincos
  * (float functions take (float)a, (float)b and return the float widened to double). */
 int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const double* b, int32_t n, double* out);
+/* Test hook: the hot-path units exactly as the kernels evaluate them, n cases (tests/test_ref_units.py
+ * bit-compares them with the reference's own code).  Per case, in -> out (doubles):
+ *   CLRRT_UNIT_OBB      x, y, theta, t, obstacle cx, cy, theta, size_x, size_y, vx, vy -> getOBBdist of the
+ *                       vehicle box (old_collisioncheck.cpp:34-36) and the obstacle box at t  [11 -> 1]
+ *   CLRRT_UNIT_ODE      x0..x6, dc, ac -> x0..x6 after VehicleODE + IntegrateEuler, dx[2]  [9 -> 8]
+ *                       (simulation.cpp:11-34, vehicle and sim_dt of the context's params)
+ *   CLRRT_UNIT_LATERAL  xval[3], yval[3], (Px, Py, heading) -> interpolate(transformToVehicle(..))
+ *                       (controller.cpp:115-148)  [9 -> 1]
+ *   CLRRT_UNIT_PROFILE  ax, ay, sx, sy, ref_res, v0, vmax, goal[4], GB -> N, v[NMAX], x[NMAX], y[NMAX] of
+ *                       getReference's line (reference.cpp:13-18) and generateVelocityProfile
+ *                       (reference.cpp:73-170)  [12 -> 1 + 3 * CLRRT_UNIT_PROFILE_NMAX]
+ *   CLRRT_UNIT_ANGLE    a, b -> angleDiff(a, b), wrapToPi(a) (functions.h:43-57)  [2 -> 2] */
+#define CLRRT_UNIT_OBB 0
+#define CLRRT_UNIT_ODE 1
+#define CLRRT_UNIT_LATERAL 2
+#define CLRRT_UNIT_PROFILE 3
+#define CLRRT_UNIT_ANGLE 4
+#define CLRRT_UNIT_PROFILE_NMAX 1024
+int clrrt_selftest_units(clrrt_ctx* ctx, int32_t unit, const double* in, int32_t n, double* out);
 
 int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);
 int clrrt_reset_counters(clrrt_ctx* ctx);

@@ -128,15 +128,8 @@ static int closest_point(const Ref& r, const Pt& q, int from) {  // controller.c
   return arg;
 }
 
-// transformToVehicle controller.cpp:115-132 then interpolate :134-148
-static double lateral_error(const Ref& r, const Row& x, int wp, const Pt& P) {  // :70-93
-  int lo, hi;
-  if (wp == 0) { lo = wp; hi = wp + 2; }
-  else if (wp == (int)r.x.size()) { lo = wp - 2; hi = wp; }
-  else { lo = wp - 1; hi = wp + 1; }
-  double xv[3] = {at0(r.x, lo), at0(r.x, lo + 1), at0(r.x, hi)};
-  double yv[3] = {at0(r.y, lo), at0(r.y, lo + 1), at0(r.y, hi)};
-  double X0 = P.x, X1 = P.y, X2 = x[2];
+// transformToVehicle controller.cpp:115-132 then interpolate :134-148 (X = preview point + heading)
+static double transform_interp(const double xv[3], const double yv[3], double X0, double X1, double X2) {
   double tx[3], ty[3];
   double sX, cX;
   lm_sincos(X2, &sX, &cX);  // transformToVehicle: sin/cos of one argument -> sincos
@@ -152,6 +145,16 @@ static double lateral_error(const Ref& r, const Row& x, int wp, const Pt& P) {  
     y = y + ty[i] * L;
   }
   return y;
+}
+
+static double lateral_error(const Ref& r, const Row& x, int wp, const Pt& P) {  // getLateralError :70-93
+  int lo, hi;
+  if (wp == 0) { lo = wp; hi = wp + 2; }
+  else if (wp == (int)r.x.size()) { lo = wp - 2; hi = wp; }
+  else { lo = wp - 1; hi = wp + 1; }
+  double xv[3] = {at0(r.x, lo), at0(r.x, lo + 1), at0(r.x, hi)};
+  double yv[3] = {at0(r.y, lo), at0(r.y, lo + 1), at0(r.y, hi)};
+  return transform_interp(xv, yv, P.x, P.y, x[2]);
 }
 
 struct Ctrl {  // class Controller controller.h:8-28
@@ -337,18 +340,23 @@ static double box_gap(Box a, Box b) {  // getOBBdist :98-148 (first separating g
   return 0;
 }
 
+// getOBBvector old_collisioncheck.cpp:14-16: one obstacle's OBB at time t
+static Box obs_box(const Obs& d, double t) { return Box(d.cx + d.vx * t, d.cy + d.vy * t, d.sx / 2, d.sy / 2, d.th); }
+
+// checkObsDistance :34-36: the vehicle OBB centred 1.424 m ahead of the rear axle
+static Box veh_box(const Row& x) {
+  double sv, cv;
+  lm_sincos(x[2], &sv, &cv);
+  return Box(x[0] + 1.424 * cv, x[1] + 1.424 * sv, 2, 4.848, x[2]);
+}
+
 // checkObsDistance: stub collisioncheck.cpp:6-8, or the obstacle form old_collisioncheck.cpp:24-51
 static double obs_distance(Oracle& o, const Row& x) {
   if (o.p.collision_mode == CLRRT_COLLISION_STUB) return 100;
   double t = o.p.obs_use_pred ? x[6] : 0;
   vector<Box> boxes;  // getOBBvector :6-22 (rebuilt every call, as the reference does)
-  for (size_t i = 0; i != o.det.size(); i++) {
-    const Obs& d = o.det[i];
-    boxes.push_back(Box(d.cx + d.vx * t, d.cy + d.vy * t, d.sx / 2, d.sy / 2, d.th));
-  }
-  double sv, cv;
-  lm_sincos(x[2], &sv, &cv);
-  Box veh(x[0] + 1.424 * cv, x[1] + 1.424 * sv, 2, 4.848, x[2]);
+  for (size_t i = 0; i != o.det.size(); i++) boxes.push_back(obs_box(o.det[i], t));
+  Box veh = veh_box(x);
   double best = 10000;
   for (size_t j = 0; j != boxes.size(); j++) {
     double D = box_gap(veh, boxes[j]);
@@ -372,6 +380,29 @@ static double dist_to_lane(double x, double y, double S, const double* C) {  // 
   return sqrt(pow(Lx - x, 2) + pow(Ly - y, 2));
 }
 
+// VehicleODE simulation.cpp:11-25 then IntegrateEuler :27-34 on x[0..6] (the loop's indices 7..10
+// read dx past its 7 elements: zero under the canonical zero-fill, so x[7..9] keep their values and
+// are overwritten by propagate).  dx is returned for the lateral-acceleration test (:98).
+static void ode_euler(const Oracle& o, Row& x, double dc, double ac, double dx[7]) {
+  const clrrt_vehicle& veh = o.p.veh;
+  const double dt = o.p.sim_dt;
+  double Gss = 1 / (1 + pow((x[4] / veh.Vch), 2));
+  // the store to dx[0] may alias x (both are vector<double> storage), so x[2] is reloaded and GCC
+  // cannot merge cos and sin into sincos here: glibc cos() then sin() (checked against the
+  // reference's own VehicleODE compiled at -O2/-O3, tests/test_ref_units.py)
+  dx[0] = x[4] * lm_cos(x[2]);
+  dx[1] = x[4] * lm_sin(x[2]);
+  dx[2] = (x[4] / veh.L) * lm_tan(x[3]) * Gss;
+  dx[3] = (1 / veh.Td) * (dc - x[3]);
+  dx[4] = x[5];
+  dx[5] = (1 / veh.Ta) * (ac - x[5]);
+  dx[6] = 1;
+  dx[4] = sat(veh.amin, veh.amax, dx[4]);
+  dx[3] = sat(-veh.ddmax, veh.ddmax, dx[3]);
+  for (int k = 0; k < 7; k++) x[k] = x[k] + dx[k] * dt;
+  x[3] = sat(-veh.dmax, veh.dmax, x[3]);
+}
+
 static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
   const clrrt_vehicle& veh = o.p.veh;
   const double dt = o.p.sim_dt;
@@ -382,23 +413,8 @@ static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
     c.update_waypoint(o, r, x);
     double dc = c.steer(o, r, x);
     double ac = c.accel(o, r, x);
-    // VehicleODE :11-25
     double dx[7];
-    double Gss = 1 / (1 + pow((x[4] / veh.Vch), 2));
-    double s2, c2;
-    lm_sincos(x[2], &s2, &c2);
-    dx[0] = x[4] * c2;
-    dx[1] = x[4] * s2;
-    dx[2] = (x[4] / veh.L) * lm_tan(x[3]) * Gss;
-    dx[3] = (1 / veh.Td) * (dc - x[3]);
-    dx[4] = x[5];
-    dx[5] = (1 / veh.Ta) * (ac - x[5]);
-    dx[6] = 1;
-    dx[4] = sat(veh.amin, veh.amax, dx[4]);
-    dx[3] = sat(-veh.ddmax, veh.ddmax, dx[3]);
-    // IntegrateEuler :27-34 (indices 7.. read zero dx and are overwritten below)
-    for (int k = 0; k < 7; k++) x[k] = x[k] + dx[k] * dt;
-    x[3] = sat(-veh.dmax, veh.dmax, x[3]);
+    ode_euler(o, x, dc, ac, dx);
     x[7] = c.IDwp;
     x[8] = at0(r.v, c.IDwp + 2);
     x[9] = dc;
@@ -917,6 +933,78 @@ int orc_eval_iteration(void* h, double sx, double sy, int explore, int stable, c
   if (r.gb_added) { tmp.tree.push_back(r.gb_node); n++; }
   if (n) orc_get_nodes(&tmp, 0, n, out2);
   return n;
+}
+
+
+// ---- unit hooks (tests/test_ref_units.py): the same functions the tree path runs, one case per row.
+// OBB gap of the vehicle box at (x, y, th) against one obstacle at time t.
+// in: x, y, th, t, cx, cy, oth, size_x, size_y, vx, vy (11 doubles per case).
+void orc_unit_obb(int n, const double* in, double* out) {
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 11 * k;
+    Row x(10, 0.0);
+    x[0] = a[0]; x[1] = a[1]; x[2] = a[2]; x[6] = a[3];
+    Obs d{a[4], a[5], a[6], a[7], a[8], a[9], a[10]};
+    out[k] = box_gap(veh_box(x), obs_box(d, a[3]));
+  }
+}
+// OBB geometry (px, py, w, h, o) -> vertices x4, y4, normals x4, y4 (floats, axis 3 canonical).
+void orc_unit_obb_geom(int n, const double* in, float* out) {
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 5 * k;
+    Box b(a[0], a[1], (float)a[2], (float)a[3], (float)a[4]);
+    float* o = out + 16 * k;
+    for (int i = 0; i < 4; i++) { o[i] = b.vx[i]; o[4 + i] = b.vy[i]; o[8 + i] = b.nx[i]; o[12 + i] = b.ny[i]; }
+  }
+}
+// VehicleODE + IntegrateEuler. in: x0..x6, dc, ac; out: x0..x6, dx[2].
+void orc_unit_ode(void* h, int n, const double* in, double* out) {
+  Oracle* o = (Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    Row x(in + 9 * k, in + 9 * k + 7);
+    x.resize(10, 0.0);
+    double dx[7];
+    ode_euler(*o, x, in[9 * k + 7], in[9 * k + 8], dx);
+    for (int i = 0; i < 7; i++) out[8 * k + i] = x[i];
+    out[8 * k + 7] = dx[2];
+  }
+}
+// transformToVehicle + interpolate. in: xval[3], yval[3], X[3].
+void orc_unit_lateral(int n, const double* in, double* out) {
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 9 * k;
+    out[k] = transform_interp(a, a + 3, a[6], a[7], a[8]);
+  }
+}
+void orc_unit_linspace(double a, double b, long N, double* out) {
+  vector<double> v = linspace(a, b, (size_t)N);
+  for (long i = 0; i < N; i++) out[i] = v[i];
+}
+// getReference's straight line from (ax, ay) to (sx, sy) at resolution res, then its velocity profile.
+// in: ax, ay, sx, sy, res, v0, vmax, goal[4], GB (12 doubles); out row (stride 1 + nmax): N, v[0..N).
+void orc_unit_profile(void* h, int n, const double* in, int nmax, double* out) {
+  Oracle o = *(Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 12 * k;
+    o.p.ref_res = a[4];
+    Node par;
+    par.ref.x.assign(1, a[0]);
+    par.ref.y.assign(1, a[1]);
+    Pt s; s.x = a[2]; s.y = a[3];
+    Ref r = get_reference(o, s, par, 1);
+    vector<double> g(a + 7, a + 11);
+    velocity_profile(o, r, a[5], a[6], g, a[11] != 0);
+    double* row = out + (size_t)(1 + nmax) * k;
+    row[0] = (double)r.v.size();
+    for (size_t i = 0; i < r.v.size() && (int)i < nmax; i++) row[1 + i] = r.v[i];
+  }
+}
+// angleDiff(a, b), wrapToPi(a)
+void orc_unit_angle(int n, const double* in, double* out) {
+  for (int k = 0; k < n; k++) {
+    out[2 * k] = angle_diff(in[2 * k], in[2 * k + 1]);
+    out[2 * k + 1] = wrap_pi(in[2 * k]);
+  }
 }
 
 }  // extern "C"
