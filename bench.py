@@ -193,7 +193,7 @@ def main():
 
     if world > 1:
         from clrrt import dist as cdist
-        out_buf = torch.empty((2 * B, cdist.REC_BYTES), dtype=torch.uint8, device="cuda")
+        ex = cdist.RoundExchange(2 * B, "cuda")
 
     replanning = bool(cfg.get("replan"))
     if replanning:
@@ -206,7 +206,8 @@ def main():
         if world == 1:
             st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
             return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
-        nodes = goals = 0
+        nodes = 0
+        goals = torch.zeros((), dtype=torch.int64, device="cuda")
         cap_stop = 0
         t0 = time.perf_counter()
         first, count = cdist.shard(world * B, world, rank)
@@ -220,15 +221,15 @@ def main():
             mine = (abi.Sample * count).from_buffer(allsmp, first * C_SAMPLE)
             # the next round's shard is searched beside this round's rollouts (clrrt_round_prefetch)
             pl.round_prefetch((abi.Sample * count).from_buffer(nxt, first * C_SAMPLE))
-            n_local = pl.round_eval(mine, out_buf.data_ptr())
-            cat, counts, my_first, t_max = cdist.exchange_round(out_buf, n_local,
-                                                                (time.perf_counter() - t0) * 1e3)
+            n_local = pl.round_eval(mine, ex.records_ptr())
+            # one count-prefixed all-gather of the accepted-node records (RCCL over xGMI)
+            cat, counts, my_first, t_max = ex.exchange(n_local, (time.perf_counter() - t0) * 1e3)
             pl.round_commit(cat.data_ptr() if cat.shape[0] else 0, cat.shape[0], my_first, counts[rank])
             nodes += cat.shape[0]
-            goals += cdist.goal_count(cat)
+            goals += cdist.goal_sum(cat)
             if t_max >= horizon:
                 break
-        return nodes, goals, cap_stop
+        return nodes, int(goals.item()), cap_stop
 
     def query(seed):
         """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""

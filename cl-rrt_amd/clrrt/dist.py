@@ -13,41 +13,85 @@ REC_BYTES = 160
 GOAL_OFFSET = 140  # clrrt_node.goal (int32)
 
 
-def exchange_round(out_buf, n_local, elapsed_ms, group=None):
-    """All-gather one round.
+class RoundExchange:
+    """All-gather of one round's accepted-node records, count-prefixed.
 
-    out_buf: uint8 tensor (cap, 160) whose first n_local rows are this rank's records.
-    elapsed_ms: this rank's elapsed query time (the horizon test uses the maximum over ranks, so
-    every rank stops after the same round).
-    Returns (records (total, 160) uint8 in global sample order, counts per rank, first row of this
-    rank's records, max elapsed ms).
+    Row 0 of `buf` is a header (int64 record count, float64 elapsed query ms); clrrt_round_eval writes
+    this rank's records from row 1 on (`records_ptr`).  One all-gather moves header + the first `bound`
+    record rows of every rank, so no count exchange (and no host sync) precedes the data; the headers
+    are read back once afterwards.  `bound` adapts to 1.25x the largest count seen; a round whose count
+    exceeds it (rare) moves the excess with a second all-gather.  gloo (CPU rehearsal of the path)
+    stages device buffers through the host.
     """
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    dev = out_buf.device
-    # gloo moves host tensors only: stage device buffers through the host (CPU rehearsal of the path)
-    host = dist.get_backend(group) == "gloo" and dev.type != "cpu"
-    cdev = torch.device("cpu") if host else dev
-    meta = torch.tensor([float(n_local), float(elapsed_ms)], dtype=torch.float64, device=cdev)
-    metas = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    counts = [int(m[0].item()) for m in metas]
-    t_max = max(float(m[1].item()) for m in metas)
-    src = out_buf.to(cdev) if host else out_buf.contiguous()
-    bufs = [torch.empty_like(src) for _ in range(world)]
-    dist.all_gather(bufs, src, group=group)
-    parts = [bufs[r][:counts[r]] for r in range(world)]
-    cat = torch.cat(parts, 0).contiguous() if sum(counts) else src[:0]
-    if host:
-        cat = cat.to(dev)
-    return cat, counts, sum(counts[:rank]), t_max
+
+    HDR = 16
+
+    def __init__(self, cap_records, device, group=None, first_bound=1024):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.cap = int(cap_records)
+        self.dev = torch.device(device)
+        self.buf = torch.zeros((self.cap + 1, REC_BYTES), dtype=torch.uint8, device=self.dev)
+        self.bound = min(self.cap, first_bound)
+        self.host = dist.get_backend(group) == "gloo" and self.dev.type != "cpu"
+        self.second_gathers = 0
+
+    def records_ptr(self):
+        """Device address where this rank's clrrt_round_eval output goes (row 1 of the buffer)."""
+        return self.buf.data_ptr() + REC_BYTES
+
+    def records(self):
+        return self.buf[1:]
+
+    def _gather(self, t):
+        src = t.cpu() if self.host else t.contiguous()
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src, group=self.group)
+        return parts
+
+    def exchange(self, n_local, elapsed_ms):
+        """Returns (records (total, 160) uint8 on the buffer's device in global sample order, counts
+        per rank, first row of this rank's records, max elapsed ms over ranks)."""
+        import numpy as np
+        hdr = np.zeros(2, dtype=np.float64)
+        hdr.view(np.int64)[0] = int(n_local)
+        hdr[1] = float(elapsed_ms)
+        self.buf[0, :self.HDR].copy_(torch.from_numpy(hdr.view(np.uint8)))
+        parts = self._gather(self.buf[:self.bound + 1])
+        heads = torch.stack([q[0, :self.HDR] for q in parts]).cpu().numpy()
+        counts = [int(c) for c in heads[:, :8].copy().view(np.int64)[:, 0]]
+        t_max = float(heads[:, 8:].copy().view(np.float64).max())
+        maxc = max(counts)
+        extra = None
+        if maxc > self.bound:
+            # the excess rows of every rank (padded to the largest count) in a second collective
+            self.second_gathers += 1
+            extra = self._gather(self.buf[1 + self.bound:1 + maxc])
+        pieces = []
+        for r in range(self.world):
+            c = counts[r]
+            pieces.append(parts[r][1:1 + min(c, self.bound)])
+            if c > self.bound:
+                pieces.append(extra[r][:c - self.bound])
+        self.bound = min(self.cap, max(self.bound, int(maxc * 1.25) + 64))
+        total = sum(counts)
+        cat = torch.cat(pieces, 0) if total else self.buf[1:1]
+        if self.host and total:
+            cat = cat.to(self.dev)
+        return cat.contiguous(), counts, sum(counts[:self.rank]), t_max
+
+
+def goal_sum(records):
+    """Appended nodes with goalReached set (feasible paths) among the records, as a device tensor (no
+    host sync: accumulate per query, read once)."""
+    if records.shape[0] == 0:
+        return torch.zeros((), dtype=torch.int64, device=records.device)
+    return records[:, GOAL_OFFSET:GOAL_OFFSET + 4].contiguous().view(torch.int32).sum(dtype=torch.int64)
 
 
 def goal_count(records):
-    """Appended nodes with goalReached set (feasible paths) among the records."""
-    if records.shape[0] == 0:
-        return 0
-    return int(records[:, GOAL_OFFSET:GOAL_OFFSET + 4].contiguous().view(torch.int32).sum().item())
+    return int(goal_sum(records).item())
 
 
 def shard(n_total, world, rank):

@@ -382,6 +382,7 @@ int clrrt_draw_samples(const clrrt_params* p, clrrt_rng* rng, int32_t n, clrrt_s
 const char* clrrt_last_error(const clrrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 static void free_all(clrrt_ctx* c) {
+  if (c->side) hipStreamSynchronize(c->side);  // side-stream work (prefetched search) uses the *2 buffers
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,

@@ -316,5 +316,92 @@ CLRRT_HD inline void sincos(double x, double& sx, double& cx) {
   cx = cos(x);
 }
 
+// ------------------------------------------------------------------------------- float sincosf
+// glibc 2.35 sincosf (sysdeps/ieee754/flt-32/s_sincosf.c + sincosf.h; the FMA variant libm's ifunc
+// selects on FMA+AVX2 hosts): the float argument is widened to double, reduced by a Cody-Waite step
+// (|y| < 120) or the Payne-Hanek reduce_large (2/pi bits __inv_pio4), and sin/cos come from two
+// double polynomials rounded once to float.  The reference's OBB::setVertices calls cos(o) and
+// sin(o) of its float angle, which GCC merges into sincosf (rrt/src/old_collisioncheck.cpp:56-65).
+// The second table of glibc (quadrants 2 and 3) is the first with c0..c4 negated; as every rounding
+// is symmetric, the cos polynomial is evaluated with the first table and negated.  Checked against
+// the host libm on all 2^32 floats (tests/native/sincosf_check.cpp).
+constexpr double kSincosf[28] = CLRRT_GLIBC_SINCOSF_TAB;
+constexpr double sf_hpi_inv = kSincosf[4], sf_hpi = kSincosf[5];
+constexpr double sf_c0 = kSincosf[6], sf_c1 = kSincosf[7], sf_s1 = kSincosf[8], sf_c2 = kSincosf[9];
+constexpr double sf_s2 = kSincosf[10], sf_c3 = kSincosf[11], sf_s3 = kSincosf[12], sf_c4 = kSincosf[13];
+
+CLRRT_HD inline uint32_t fbits(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  return u;
+}
+CLRRT_HD inline uint32_t abstop12f(float x) { return (fbits(x) >> 20) & 0x7ff; }
+
+// sincosf_poly (sincosf.h) with x the reduced argument times the quadrant sign; negc: table 1
+CLRRT_HD inline void sincosf_poly(double x, double x2, int n, bool negc, float& sinp, float& cosp) {
+  const double x4 = x2 * x2;
+  const double x3 = x2 * x;
+  const double c2 = fma_(x2, sf_c4, sf_c3);
+  const double s1 = fma_(x2, sf_s3, sf_s2);
+  const double c1 = fma_(x2, sf_c1, sf_c0);
+  const double x5 = x3 * x2;
+  const double x6 = x4 * x2;
+  const double s = fma_(x3, sf_s1, x);
+  const double c = fma_(x4, sf_c2, c1);
+  const float sv = (float)fma_(x5, s1, s);
+  float cv = (float)fma_(x6, c2, c);
+  if (negc) cv = -cv;
+  if (n & 1) { sinp = cv; cosp = sv; }
+  else { sinp = sv; cosp = cv; }
+}
+
+CLRRT_HD inline void sincosf(float y, float& sinp, float& cosp) {
+  double x = y;
+  const uint32_t t = abstop12f(y);
+  if (t < abstop12f(0x1.921FB6p-1f)) {  // |y| < pi/4
+    const double x2 = x * x;
+    if (t < abstop12f(0x1p-12f)) { sinp = y; cosp = 1.0f; return; }
+    sincosf_poly(x, x2, 0, false, sinp, cosp);
+  } else if (t < abstop12f(120.0f)) {
+    // reduce_fast (no TOINT intrinsics on x86-64): the quadrant lands in bits 24..31 of r
+    const double r = x * sf_hpi_inv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = fma_(-(double)n, sf_hpi, x);
+    const double sg = (((n >> 1) ^ n) & 1) ? -1.0 : 1.0;  // sign[n & 3] = {1, -1, -1, 1}
+    sincosf_poly(x * sg, x * x, n, (n & 2) != 0, sinp, cosp);
+  } else if (t < abstop12f(__builtin_inff())) {
+    // reduce_large: Payne-Hanek with 96 bits of 2/pi selected by the exponent
+    constexpr uint32_t inv_pio4[24] = CLRRT_GLIBC_INV_PIO4;
+    uint32_t xi = fbits(y);
+    const int sign = xi >> 31;
+    const int k = (xi >> 26) & 15;
+    const int shift = (xi >> 23) & 7;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    uint64_t res0 = (uint32_t)(xi * inv_pio4[k]);
+    const uint64_t res1 = (uint64_t)xi * inv_pio4[k + 4];
+    const uint64_t res2 = (uint64_t)xi * inv_pio4[k + 8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    const uint64_t nn = (res0 + (1ULL << 61)) >> 62;
+    res0 -= nn << 62;
+    const int n = (int)nn;
+    x = (double)(int64_t)res0 * 0x1.921FB54442D18p-62;
+    const int q = n + sign;
+    const double sg = (((q >> 1) ^ q) & 1) ? -1.0 : 1.0;
+    sincosf_poly(x * sg, x * x, n, (q & 2) != 0, sinp, cosp);
+  } else {
+    sinp = cosp = y - y;
+  }
+}
+
+// glibc sinf (s_sinf.c): the same reduction and sin polynomial as sincosf (checked bit for bit on all
+// floats by tests/native/sincosf_check.cpp)
+CLRRT_HD inline float sinf(float y) {
+  float s, c;
+  sincosf(y, s, c);
+  return s;
+}
+
 }  // namespace glibc
 }  // namespace clrrt

@@ -970,6 +970,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   RollCont* __restrict__ cont = (RollCont*)a.cont;
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
   int poll = 0;
+  uint32_t idle_polls = 0;  // hand-off absorber: polls without work (spin limit)
   // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
   // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
   // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
@@ -1088,6 +1089,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         got = __shfl(got, leader, 64);
         h = __shfl(h, leader, 64);
         if (got) {
+          idle_polls = 0;
           const int rk = __popcll(idle & ((1ull << lane) - 1));
           if (j < 0 && rk < got) {
             const int q = h + rk;
@@ -1115,6 +1117,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           const int hh = __hip_atomic_load(&a.cont_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const int tt = __hip_atomic_load(&a.cont_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (parked == 0 && d <= 0 && hh >= tt) break;
+          // backstop (the launcher keeps the grid resident): ~1 s of polling without a donor finishing
+          // ends the wave and is reported by the host as an error instead of hanging the GPU
+          if (++idle_polls > (1 << 22)) {
+            if (lane == 0) atomicAdd(&a.cont_ctl[3], 1);
+            break;
+          }
           __builtin_amdgcn_s_sleep(8);
           continue;
         }
@@ -1280,7 +1288,8 @@ __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ 
     for (int w = 0; w < 2; w++) {
       if (w == 1 && !so[k].gb_ok) break;
       const clrrt_node& n = w == 0 ? regnodes[k] : gbnodes[k];
-      float c = cosf((float)(-n.state[2] - 0.0)), s = sinf((float)(-n.state[2] - 0.0));
+      float c, s;
+      glibc::sincosf((float)(-n.state[2] - 0.0), s, c);  // dubinsDistance: cos/sin of one float -> sincosf
       float key = dubins_key(sx, sy, n.state[0], n.state[1], c, s);
       if (!ex) key = n.costE + key;
       if (!(key > thr) && feasible_node(n.ref_back[0], n.ref_back[1], n.ang_par, sx, sy, p.feas_len)) {
@@ -1420,7 +1429,7 @@ __global__ void k_append(const clrrt_node* __restrict__ in, int n, int64_t base,
   r.bx = d.ref_back[0]; r.by = d.ref_back[1];
   r.ang_par = d.ang_par;
   float ang = (float)(-d.state[2] - 0.0);
-  r.c = cosf(ang); r.s = sinf(ang);
+  glibc::sincosf(ang, r.s, r.c);  // dubinsDistance rrtplanner.cpp:376-378: glibc sincosf
   r.costE = d.costE;
   r.id = (int32_t)(base + i);
   r.ca = cosf((float)d.ang_par); r.sa = sinf((float)d.ang_par);
@@ -1434,7 +1443,7 @@ __device__ __forceinline__ NnRec nn_record(const clrrt_node& d, int64_t id) {
   r.bx = d.ref_back[0]; r.by = d.ref_back[1];
   r.ang_par = d.ang_par;
   float ang = (float)(-d.state[2] - 0.0);
-  r.c = cosf(ang); r.s = sinf(ang);
+  glibc::sincosf(ang, r.s, r.c);  // dubinsDistance rrtplanner.cpp:376-378: glibc sincosf
   r.costE = d.costE;
   r.id = (int32_t)id;
   r.ca = cosf((float)d.ang_par); r.sa = sinf((float)d.ang_par);
@@ -1689,11 +1698,11 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 5: r = atan2(x, y); break;
     case 6: r = exp(x); break;
     case 7: r = x / y; break;
-    case 8: r = (double)cosf(xf); break;
-    case 9: r = (double)sinf(xf); break;
-    case 10: r = (double)atan2f(xf, yf); break;
-    case 11: r = (double)acosf(xf); break;
-    case 12: r = (double)asinf(xf); break;
+    case 8: { float sf, cf; glibc::sincosf(xf, sf, cf); r = (double)cf; } break;
+    case 9: r = (double)glibc::sinf(xf); break;
+    case 10: r = (double)glibcf::atan2f(xf, yf); break;
+    case 11: r = (double)glibcf::acosf(xf); break;
+    case 12: r = (double)glibcf::asinf(xf); break;
     case 13: r = (double)sqrtf(xf); break;
     case 14: r = (double)(xf / yf); break;
     case 15: r = round(x); break;
@@ -2015,7 +2024,20 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
   RollInit* pr = (RollInit*)prep;
   const size_t lds = roll_lds_bytes(a0);
-  const int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
+  int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
+  if (a0.cont) {
+    // hand-off absorbers wait for every donor wave of the grid: the grid must be resident at once
+    const void* fn = a0.p.need_gap ? (const void*)&k_roll_run<true, true> : (const void*)&k_roll_run<false, true>;
+    int occ = 0, dev = 0, ncu = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    if (!a0.p.need_gap && lds > 64 * 1024 &&
+        (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+      return e;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, a0.p.need_gap ? 0 : lds)) != hipSuccess)
+      return e;
+    nb = std::max(1, std::min(nb, std::max(1, occ) * ncu));
+  }
   RollArgs a = a0;
   a.cont_donors = nb * 3;  // waves 1..3 of each block (launch_bounds 256)
   if (a.p.need_gap) {

@@ -282,9 +282,11 @@ int clrrt_expand(clrrt_ctx* ctx, clrrt_rng* rng, int64_t n_iters, double budget_
  * *n_out receives the count. */
 int clrrt_round_eval(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, void* dev_out,
                      int32_t* n_out);
-/* Append `n` node records (device pointer) to the tree; `local_first`/`local_count` name the
- * slice of them that this context produced in its last clrrt_round_eval (their rows are moved
- * into the arena); records outside that slice are remote nodes whose rows stay on their owner. */
+/* Append `n` node records (device pointer) to the tree in their order.  `local_first`/`local_count`
+ * name the slice of them that this context produced in its last clrrt_round_eval (informational:
+ * clrrt_round_eval already wrote those records' rows into this context's arena, at the row_offset
+ * the records carry); records outside the slice are remote nodes whose rows stay on their owner
+ * (`owner`; clrrt_path_commit + a gather of the path's rows complete a committed path). */
 int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t local_first,
                        int32_t local_count);
 /* Engine extension (no reference counterpart): declares the samples of the NEXT clrrt_round_eval.
@@ -305,7 +307,8 @@ int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32
 
 /* Test hook: evaluates, on the device, the elementary functions exactly as the kernels call them,
  * out[i] = f(a[i], b[i]) for fn = 0 sin, 1 cos, 2 tan (glibc restatements), 3 sqrt, 4 fmod, 5 atan2,
- * 6 exp, 7 a/b, 8 cosf, 9 sinf, 10 atan2f, 11 acosf, 12 asinf, 13 sqrtf, 14 float a/b, 15 round,
+ * 6 exp, 7 a/b, 8 cosf, 9 sinf (glibc sincosf restatement), 10 atan2f, 11 acosf, 12 asinf (glibc
+ * restatements), 13 sqrtf, 14 float a/b, 15 round,
  * 16 sin and 17 cos of glibc's generic sincos
  * (float functions take (float)a, (float)b and return the float widened to double). */
 int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const double* b, int32_t n, double* out);

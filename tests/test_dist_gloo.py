@@ -1,6 +1,6 @@
 """World-size-2 test of the multi-GPU round protocol on CPU (gloo): every rank evaluates its slice of
 each round's samples against the frozen tree, the accepted-node records are exchanged with
-clrrt.dist.exchange_round (the path bench.py runs over RCCL), and every rank appends the union in
+clrrt.dist.RoundExchange (the count-prefixed all-gather bench.py runs over RCCL), and every rank appends the union in
 global sample order.  The CPU oracle stands in for the GPU evaluator (test infrastructure only).
 
 Checks: both ranks end with the identical tree, and it equals the single-process BATCH expansion
@@ -48,7 +48,7 @@ def _worker(rank, port, out_dir):
     from clrrt import dist as cdist
     obs = scenes.urban_scene(200)
     o = _oracle(obs)
-    out_buf = torch.zeros((2 * PER_RANK, cdist.REC_BYTES), dtype=torch.uint8)
+    rx = cdist.RoundExchange(2 * PER_RANK, "cpu", first_bound=4)  # small bound: exercises the second gather
     for _ in range(ROUNDS):
         xy, ex = o.draw_samples(WORLD * PER_RANK)   # the single glibc stream, drawn by every rank
         first, count = cdist.shard(WORLD * PER_RANK, WORLD, rank)
@@ -56,11 +56,11 @@ def _worker(rank, port, out_dir):
         for j in range(first, first + count):         # frozen tree: nothing appended yet
             recs += o.eval_iteration(xy[j][0], xy[j][1], ex[j], stable=True)
         raw = bytes((abi.Node * len(recs))(*recs)) if recs else b""
-        out_buf.zero_()
+        rx.records().zero_()
         if raw:
-            out_buf[:len(recs)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8).view(len(recs), cdist.REC_BYTES)
-        cat, counts, my_first, _ = cdist.exchange_round(out_buf, len(recs), 0.0)
-        assert my_first == sum(counts[:rank]) and cat.shape[0] == sum(counts)
+            rx.records()[:len(recs)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8).view(len(recs), cdist.REC_BYTES)
+        cat, counts, my_first, t_max = rx.exchange(len(recs), 10.0 * (rank + 1))
+        assert my_first == sum(counts[:rank]) and cat.shape[0] == sum(counts) and t_max == 10.0 * WORLD
         # commit in global order: goal-biased records name the record before them as parent
         base = o.size()
         cur = list(o.nodes_raw())
@@ -70,6 +70,7 @@ def _worker(rank, port, out_dir):
                 nd.parent = base + k - 1
             cur.append(nd)
         o.load_tree((abi.Node * len(cur))(*cur))
+    assert rx.second_gathers >= 1  # the first round's counts exceeded the initial bound of 4
     n = o.nodes()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), state=n["state"], parent=n["parent"], goal=n["goal"],
              nrows=n["nrows"], costE=n["costE"], costS=n["costS"])

@@ -1,0 +1,117 @@
+"""The multi-GPU round protocol through libclrrt with two ranks — GPU (both processes share device 0; the
+gloo backend stages the exchange through the host, the rest is the path bench.py runs over RCCL).
+
+Each rank evaluates its contiguous half of every round's 2B samples with clrrt_round_prefetch /
+clrrt_round_eval, the records are exchanged with clrrt.dist.RoundExchange (one count-prefixed
+all-gather), and clrrt_round_commit appends the union in global sample order; trajectory rows stay on
+the rank that grew them (`owner`).  After 4 rounds at B = 4096 per rank each rank commits the best path
+(extractBestPath, rrtplanner.cpp:318-368) and completes its rows with clrrt.dist.fetch_path_rows.
+
+Checks against ONE process expanding the same stream with 2B samples per round (SURVEY.md §8(e):
+sharding by samples does not change the result): identical node headers on both ranks (owner and
+row_offset aside), the rows of every node equal on its owner, and the committed path's rows equal on
+both ranks.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD, B, ROUNDS, SEED = 2, 4096, 4, 17
+HDR = 148  # clrrt_node bytes before owner / row_offset
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _planner():
+    import clrrt
+    from clrrt import abi, scenes
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), device=0, max_nodes=1 << 18,
+                       max_rows=1 << 25, max_batch=WORLD * B)
+    pl.set_obstacles(scenes.urban_scene(200))
+    pl.tree_init()
+    return pl
+
+
+def _worker(rank, port, out_dir):
+    sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    import clrrt
+    from clrrt import abi
+    from clrrt import dist as cdist
+    pl = _planner()
+    pl.set_rank(rank)
+    pl.set_stream(torch.cuda.current_stream().cuda_stream)
+    rx = cdist.RoundExchange(2 * B, "cuda", first_bound=256)
+    rng = clrrt.Rng(SEED)
+    first, count = cdist.shard(WORLD * B, WORLD, rank)
+    nxt = rng.draw_samples(pl.params, WORLD * B)
+    for _ in range(ROUNDS):
+        cur, nxt = nxt, rng.draw_samples(pl.params, WORLD * B)
+        mine = (abi.Sample * count).from_buffer(cur, first * 24)
+        pl.round_prefetch((abi.Sample * count).from_buffer(nxt, first * 24))
+        n_local = pl.round_eval(mine, rx.records_ptr())
+        cat, counts, my_first, _ = rx.exchange(n_local, 0.0)
+        pl.round_commit(cat.data_ptr() if cat.shape[0] else 0, cat.shape[0], my_first, counts[rank])
+    raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
+    g = pl.nodes()
+    own = np.nonzero(g["owner"] == rank)[0]
+    rows = [pl.rows(int(g["row_offset"][i]), int(g["nrows"][i])) for i in own]
+    ids, _, _ = pl.extract_best_path()
+    pl.path_commit(ids)
+    moved = cdist.fetch_path_rows(pl, rank)
+    _, prow = pl.path_download()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), hdr=raw[:, :HDR], own=own,
+             rows=np.concatenate(rows) if rows else np.zeros((0, 10)), ids=np.array(ids, dtype=np.int64),
+             prow=prow, moved=moved, second=rx.second_gathers)
+    dist.barrier()
+    dist.destroy_process_group()
+    pl.close()
+
+
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    import clrrt
+    pl = _planner()
+    st = pl.expand(clrrt.Rng(SEED), n_iters=ROUNDS * WORLD * B, mode=clrrt.CLRRT_MODE_BATCH, batch=WORLD * B)
+    assert st["rounds"] == ROUNDS
+    ref_raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
+    g = pl.nodes()
+    ranks = [np.load(tmp_path / f"rank{r}.npz") for r in range(WORLD)]
+    print(f"2 ranks x {B} samples x {ROUNDS} rounds: {ref_raw.shape[0]} nodes; owned "
+          f"{[len(r['own']) for r in ranks]}; path {len(ranks[0]['ids'])} nodes, rows moved "
+          f"{[int(r['moved']) for r in ranks]}, second gathers {[int(r['second']) for r in ranks]}")
+    assert ref_raw.shape[0] > 2000
+    for r in ranks:
+        assert np.array_equal(r["hdr"], ref_raw[:, :HDR])
+    assert sum(len(r["own"]) for r in ranks) == ref_raw.shape[0]  # the root is owned by rank 0 only
+    for rk, r in enumerate(ranks):
+        want = [pl.rows(int(g["row_offset"][i]), int(g["nrows"][i])) for i in r["own"]]
+        want = np.concatenate(want) if want else np.zeros((0, 10))
+        assert np.array_equal(r["rows"].view(np.uint64), want.view(np.uint64)), rk
+    ids, _, _ = pl.extract_best_path()
+    pl.path_commit(ids)
+    _, prow = pl.path_download()
+    assert len(ids) >= 2
+    for r in ranks:
+        assert list(r["ids"]) == list(ids)
+        assert np.array_equal(r["prow"].view(np.uint64), prow.view(np.uint64))
+    assert sum(int(r["moved"]) for r in ranks) > 0  # the path crossed ranks
+    pl.close()

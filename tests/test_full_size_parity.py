@@ -1,0 +1,137 @@
+"""Parity at the benchmarked sizes (BASELINE.json configs[1], configs[2], configs[4]) — GPU.
+
+* cfg3 (200 static obstacles, B = 16384 samples per round): BATCH rounds through the multi-GPU round API
+  (clrrt_round_eval / clrrt_round_commit, the path bench.py times).  On rounds 1, 3, 6 and 12, 512 (128)
+  samples drawn at random from the round's 16384 are evaluated by the oracle against the same frozen
+  tree (eval_iteration = one expandTree iteration, rrtplanner.cpp:123-174, BATCH tie order) and the
+  records the GPU produced for them INSIDE the full batch must be identical: count, parent, nrows, goal
+  flag, state bits and float cost bits; for 48 of them the committed trajectory rows too.
+* cfg2 (50 static obstacles, B = 4096): two BATCH rounds, whole tree against the oracle's expand_batch,
+  bit for bit (states, costs, rows).
+The 20-mover config-5 scene runs in tests/test_replan.py (test_replanning_queries_parity[moving20]).
+"""
+import numpy as np
+import pytest
+
+import clrrt
+from clrrt import abi, scenes
+from oracle_binding import Oracle
+
+pytestmark = pytest.mark.gpu
+
+REC = 160
+
+
+def _records(raw, n):
+    if n == 0:
+        return None
+    return clrrt.nodes_to_numpy((abi.Node * n).from_buffer_copy(raw[:n * REC]))
+
+
+def _per_sample(rec, samples, picks):
+    """Map the compacted round records back to their samples: a regular record's reference ends at its
+    sample (the accumulated linspace's last point, within 1e-6 m); a goal-biased record (parent =
+    CLRRT_PARENT_PREV) follows its regular record."""
+    out = {j: [] for j in picks}
+    if rec is None:
+        return out
+    sx = np.array([samples[j].x for j in picks])
+    sy = np.array([samples[j].y for j in picks])
+    for i in range(len(rec["parent"])):
+        if rec["parent"][i] == abi.CLRRT_PARENT_PREV:
+            continue
+        d = np.hypot(sx - rec["ref_back"][i, 0], sy - rec["ref_back"][i, 1])
+        k = int(np.argmin(d))
+        if d[k] < 1e-6:
+            out[picks[k]].append(i)
+            if i + 1 < len(rec["parent"]) and rec["parent"][i + 1] == abi.CLRRT_PARENT_PREV:
+                out[picks[k]].append(i + 1)
+    return out
+
+
+def _same_node(g, i, r):
+    """GPU record i (numpy view) vs oracle node r (abi.Node): exact."""
+    st = np.array(list(r.state), dtype=np.float64)
+    return (int(g["parent"][i]) == r.parent and int(g["nrows"][i]) == r.nrows and int(g["goal"][i]) == r.goal
+            and np.array_equal(g["state"][i].view(np.uint64), st.view(np.uint64))
+            and float(g["costE"][i]) == r.costE and float(g["costS"][i]) == r.costS)
+
+
+def test_cfg3_full_batch_rounds_match_oracle():
+    import torch
+    B = 16384
+    obs = scenes.urban_scene(200)
+    params = abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 20,
+                       max_rows=1 << 26, max_batch=B)
+    pl.set_obstacles(obs)
+    pl.tree_init()
+    o = Oracle(params, obs)
+    out = torch.empty((2 * B, REC), dtype=torch.uint8, device="cuda")
+    rng = clrrt.Rng(31)
+    pick_rng = np.random.default_rng(5)
+    checked = {"samples": 0, "nodes": 0, "rows": 0}
+    check_rounds = {1: 512, 3: 512, 6: 512, 12: 128}
+    for rnd in range(1, max(check_rounds) + 1):
+        smp = rng.draw_samples(pl.params, B)
+        n_before = pl.size()[0]
+        n = pl.round_eval(smp, out.data_ptr())
+        raw = out[:n].cpu().numpy().tobytes()
+        rec = _records(raw, n)
+        picks = sorted(pick_rng.choice(B, check_rounds.get(rnd, 0), replace=False).tolist())
+        if picks:
+            o.load_tree(pl.nodes_raw())
+            mine = _per_sample(rec, smp, picks)
+            bad = []
+            for j in picks:
+                want = o.eval_iteration(smp[j].x, smp[j].y, smp[j].explore, stable=True)
+                got = mine[j]
+                ok = len(got) == len(want) and all(_same_node(rec, i, r) for i, r in zip(got, want))
+                checked["samples"] += 1
+                checked["nodes"] += len(want)
+                if not ok:
+                    bad.append((j, len(want), len(got)))
+            assert not bad, f"round {rnd} ({n_before} nodes): {len(bad)} of {len(picks)} samples differ {bad[:5]}"
+        pl.round_commit(out.data_ptr(), n, 0, n)
+        if picks:
+            # committed trajectories (Node::tra) of 48 accepted regular nodes vs the oracle's Simulation
+            g = pl.nodes()
+            for j in picks[:48]:
+                for i in mine[j][:1]:
+                    par = int(rec["parent"][i])
+                    want = o.simulate(par, 0, smp[j].x, smp[j].y, rows=True, rows_cap=600)
+                    t = n_before + i
+                    rows = pl.rows(int(g["row_offset"][t]), int(g["nrows"][t]))
+                    assert np.array_equal(rows.view(np.uint64), want["rows"].view(np.uint64)), (rnd, j)
+                    checked["rows"] += 1
+    print(f"cfg3 full-batch rounds: {pl.size()[0]} nodes; oracle-checked {checked}")
+    assert checked["nodes"] > 500 and checked["rows"] > 50
+    pl.close()
+
+
+def test_cfg2_batch_tree_parity():
+    B, rounds = 4096, 2
+    obs = scenes.urban_scene(50)
+    o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+    Oracle.srand(21)
+    o.init_tree()
+    o.expand_batch(B * rounds, B, stable=True)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 16,
+                       max_rows=1 << 24, max_batch=B)
+    pl.set_obstacles(obs)
+    pl.tree_init()
+    st = pl.expand(clrrt.Rng(21), n_iters=B * rounds, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+    assert st["rounds"] == rounds
+    on, gn = o.nodes(), pl.nodes()
+    print(f"cfg2 BATCH: oracle {len(on['parent'])} nodes, gpu {len(gn['parent'])}")
+    assert len(on["parent"]) == len(gn["parent"]) > 500
+    assert np.array_equal(on["parent"], gn["parent"]) and np.array_equal(on["goal"], gn["goal"])
+    assert np.array_equal(gn["state"].view(np.uint64), on["state"].view(np.uint64))
+    assert np.array_equal(gn["costE"].view(np.uint32), on["costE"].view(np.uint32))
+    assert np.array_equal(gn["costS"].view(np.uint32), on["costS"].view(np.uint32))
+    for i in range(1, len(on["parent"]), 7):
+        rows = pl.rows(int(gn["row_offset"][i]), int(gn["nrows"][i]))
+        assert np.array_equal(rows.view(np.uint64), np.ascontiguousarray(o.rows(i)).view(np.uint64)), i
+    oc, gc = o.counters(), pl.counters()
+    assert oc["rollouts"] > 0 and gc["rollouts"] > 0
+    pl.close()

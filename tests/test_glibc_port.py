@@ -25,3 +25,28 @@ def test_glibc_data_header_is_current():
         subprocess.run(["python3", os.path.join(root, "tools", "gen_glibc_libm.py"), "--out", out], check=True,
                        capture_output=True)
         assert open(out).read() == open(os.path.join(root, "cl-rrt_amd", "csrc", "clrrt_glibc_data.hpp")).read()
+
+
+def test_glibc_sincosf_bit_exact():
+    """clrrt::glibc::sincosf / sinf (OBB::setVertices and dubinsDistance's float cos/sin) against the host
+    libm's sincosf, sinf and cosf on every 7th float bit pattern (pass 1 for all 2^32: 0 mismatches)."""
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "sincosf_check")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", exe,
+                        os.path.join(HERE, "native", "sincosf_check.cpp")], check=True)
+        out = subprocess.run([exe, "7"], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "mismatches 0" in out.stdout
+
+
+def test_glibc_float_inverse_trig_bit_exact():
+    """clrrt::glibcf::atanf / acosf / asinf / atan2f (dubinsDistance's float libm calls) against the host
+    libm on every 7th float and 2*10^6 random/edge pairs (pass 1 and 10^8 pairs: 0 mismatches)."""
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "glibcf_check")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", exe,
+                        os.path.join(HERE, "native", "glibcf_check.cpp")], check=True)
+        out = subprocess.run([exe, "7", "2000000"], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "atanf mismatches 0, acosf mismatches 0, asinf mismatches 0" in out.stdout
+        assert "atan2f mismatches 0" in out.stdout

@@ -19,10 +19,12 @@ from oracle_binding import Oracle, nodes_to_numpy
 GOAL_W = (40.0, 0.0, 0.0, 0.0)
 
 
-def _moving_scene():
-    """200 static + 20 moving obstacles (the config-5 generator) without moving obstacle 8, which
-    crosses the lane in front of the car and leaves the goal unreachable in short test runs."""
-    return np.delete(scenes.urban_scene(200, 20), 208, axis=0)
+def _moving_scene(drop_208=True):
+    """200 static + 20 moving obstacles (the config-5 generator).  drop_208: without moving obstacle 8,
+    which crosses the lane in front of the car and can leave the goal unreachable in short runs (the
+    full scene runs as kind "moving20")."""
+    s = scenes.urban_scene(200, 20)
+    return np.delete(s, 208, axis=0) if drop_208 else s
 
 
 def _make(mode):
@@ -224,12 +226,13 @@ def test_path_transform_parity():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["stub", "obb", "moving"])
+@pytest.mark.parametrize("kind", ["stub", "obb", "moving", "moving20"])
 def test_replanning_queries_parity(kind):
     """Five 5 Hz queries (EXACT expansion, 150 iterations each): after every re-init and every
     expansion the GPU tree equals the oracle's; poses come from the oracle's committed path."""
     mode = abi.CLRRT_COLLISION_STUB if kind == "stub" else abi.CLRRT_COLLISION_OBB
-    obs = {"stub": np.zeros((0, 7)), "obb": scenes.urban_scene(200), "moving": _moving_scene()}[kind]
+    obs = {"stub": np.zeros((0, 7)), "obb": scenes.urban_scene(200), "moving": _moving_scene(),
+           "moving20": _moving_scene(drop_208=False)}[kind]
     make = _make(mode)
     o = Oracle(abi.default_params(collision_mode=mode), None)
     pl = _planner(mode)
@@ -238,7 +241,7 @@ def test_replanning_queries_parity(kind):
     Oracle.srand(seed)
     rng = clrrt.Rng(seed)
     pose = np.array([0.0, 0.0, 0.0, 0.0, 1.0, 0.0])
-    outcomes = []
+    outcomes, path_lens = [], []
     for q in range(5):
         t = q * replan.QUERY_PERIOD
         goal_c = replan.goal_in_car_frame(GOAL_W, pose)
@@ -254,13 +257,18 @@ def test_replanning_queries_parity(kind):
         ids_o, rows_o = ob.end_query(pose)
         ids_g, rows_g = gb.end_query(pose)
         assert ids_o == ids_g
+        path_lens.append(len(ids_o))
         assert np.array_equal(rows_g.view(np.uint64), rows_o.view(np.uint64))
         for filtered in (False, True):
             mo, mg = o.path_mpc_message(filtered), pl.path_mpc_message(filtered)
             assert mo.shape == mg.shape and np.array_equal(mg.view(np.uint64), mo.view(np.uint64)), (q, filtered)
         pose = replan.advance_pose(pose, rows_o)
-    print(kind, "outcomes", outcomes)
+    print(kind, "outcomes", outcomes, "committed path lengths", path_lens)
     assert outcomes[0] == abi.REINIT_EMPTY
+    # a query without a goal-reaching node commits nothing and the next one restarts from the root
+    for q in range(1, 5):
+        if path_lens[q - 1] == 0:
+            assert outcomes[q] == abi.REINIT_EMPTY, (q, outcomes)
 
 
 @pytest.mark.gpu

@@ -44,6 +44,10 @@ CONSTS = {
 }
 SINCOSTAB = (0xAEB80, 440)
 XFG = (0xC15C0, 186)
+# sysdeps/ieee754/flt-32 (sincosf.h, sincosf_data.c): __sincosf_table[2] (sign[4], hpi_inv, hpi, c0, c1,
+# s1, c2, s2, c3, s3, c4: 14 doubles each) and __inv_pio4[24] (32-bit windows of the bits of 2/pi)
+SINCOSF_TABLE = (0xB30C0, 2 * 14)
+INV_PIO4 = (0xB3060, 24)
 
 
 def dbl(b, a):
@@ -78,6 +82,54 @@ def split(v):
     return hi, lo
 
 
+def two_over_pi_hex(digits):
+    """Hex digits of the fraction of 2/pi (Machin's formula, decimal arithmetic)."""
+    decimal.getcontext().prec = digits * 2 + 40
+
+    def arctan_inv(n):
+        x = decimal.Decimal(1) / n
+        x2 = x * x
+        total, term, k = decimal.Decimal(0), x, 1
+        while term != 0:
+            total += term / k if (k // 2) % 2 == 0 else -term / k
+            term *= x2
+            k += 2
+        return total
+
+    pi = 4 * (4 * arctan_inv(5) - arctan_inv(239))
+    f = 2 / pi
+    out = ""
+    for _ in range(digits):
+        f *= 16
+        d = int(f)
+        out += "0123456789abcdef"[d]
+        f -= d
+    return out
+
+
+def check_sincosf(tab, inv):
+    """hpi_inv / hpi are 2^24 * 2/pi and pi/2 rounded to double; the two tables differ only in the signs
+    of c0..c4 (quadrants 2 and 3); __inv_pio4[k] is the 32-bit window of 2/pi's bits ending at byte k."""
+    h = two_over_pi_hex(64)
+    for k in range(24):
+        lo = max(0, 2 * (k - 3))
+        want = int(h[lo:2 * (k + 1)], 16)
+        if inv[k] != want:
+            sys.exit(f"__inv_pio4[{k}] = {inv[k]:#x}, 2/pi gives {want:#x}")
+    decimal.getcontext().prec = 60
+    t0, t1 = tab[:14], tab[14:]
+    if t0[:4] != [1.0, -1.0, -1.0, 1.0] or t1[:4] != t0[:4]:
+        sys.exit("__sincosf_table sign rows")
+    if t0[4] != float.fromhex("0x1.45f306dc9c883p+23") or t0[5] != math.pi / 2 or t1[4:6] != t0[4:6]:
+        sys.exit("__sincosf_table hpi_inv / hpi")
+    for i, name in ((6, "c0"), (7, "c1"), (9, "c2"), (11, "c3"), (13, "c4")):
+        if t1[i] != -t0[i]:
+            sys.exit(f"__sincosf_table[1].{name} is not -__sincosf_table[0].{name}")
+    for i, name in ((8, "s1"), (10, "s2"), (12, "s3")):
+        if t1[i] != t0[i]:
+            sys.exit(f"__sincosf_table[1].{name} differs")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libm", default=LIBM)
@@ -107,6 +159,9 @@ def main():
         if got[0] != sh or got[2] != ch or not lows_ok:
             sys.exit(f"__sincostab row {k}: image {got} != derived {[sh, sl, ch, cl]}")
     xfg = [dbl(b, XFG[0] + 8 * i) for i in range(4 * XFG[1])]
+    sctab = [dbl(b, SINCOSF_TABLE[0] + 8 * i) for i in range(SINCOSF_TABLE[1])]
+    inv = list(struct.unpack_from(f"<{INV_PIO4[1]}I", b, INV_PIO4[0]))
+    check_sincosf(sctab, inv)
     lines = [
         "// clrrt_glibc_data.hpp — GENERATED by tools/gen_glibc_libm.py; do not edit.",
         "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c) and tan (s_tan.c) as loaded by",
@@ -126,6 +181,15 @@ def main():
     lines.append("#define CLRRT_GLIBC_XFG { \\")
     for i in range(0, len(xfg), 4):
         lines.append("  " + ", ".join(hexf(v) for v in xfg[i:i + 4]) + ", \\")
+    lines.append("}")
+    lines.append("// float sincosf (flt-32/sincosf_data.c): per table sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4")
+    lines.append("#define CLRRT_GLIBC_SINCOSF_TAB { \\")
+    for i in range(0, len(sctab), 7):
+        lines.append("  " + ", ".join(hexf(v) for v in sctab[i:i + 7]) + ", \\")
+    lines.append("}")
+    lines.append("#define CLRRT_GLIBC_INV_PIO4 { \\")
+    for i in range(0, len(inv), 8):
+        lines.append("  " + ", ".join(f"{v:#010x}u" for v in inv[i:i + 8]) + ", \\")
     lines.append("}")
     lines.append("}}  // namespace clrrt::glibc")
     open(args.out, "w").write("\n".join(lines) + "\n")
