@@ -43,6 +43,7 @@ PEAK_HBM_GBS = 8000.0
 # Algorithmic FLOP per unit: FP64 per simulated step = 160 + 6 per reference
 # point scanned by findClosestPoint; FP32 per OBB box test = 36.
 FLOP_STEP, FLOP_SCAN, FLOP_BOX = 160, 6, 36
+FLOP_KEY = 40  # FP32 FLOP per nearest-node (Dubins) key
 
 
 def parse():
@@ -57,25 +58,30 @@ def parse():
     ap.add_argument("--rows-per-node", type=int, default=64)
     ap.add_argument("--cpu-queries", type=int, default=5, help="oracle queries timed for cpu_baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-exact", action="store_true", help="skip the secondary EXACT-mode figure")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path (e.g. several ranks sharing one GPU)")
     return ap.parse_args()
 
 
-def measured_traffic():
-    """HBM bytes per rollout launch from the committed rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE
-    collected in separate runs, MI355X_MICROARCH.md HBM section); bench.py cannot collect counters
-    itself.  Returns (bytes or None, note)."""
+def measured_traffic(config):
+    """HBM bytes per rollout launch from the committed rocprofv3 PMC passes of THIS config
+    (profiles/r*_<config>_pmc_{fetch,write}.json: FETCH_SIZE and WRITE_SIZE collected in separate runs,
+    MI355X_MICROARCH.md HBM section); bench.py cannot collect counters itself.  The newest pass that has
+    both files is used and named in the note.  Returns (bytes or None, note)."""
     import glob
     prof = os.path.join(ROOT, "profiles")
-    fetch = sorted(glob.glob(os.path.join(prof, "r*_cfg3_pmc_fetch.json")))
-    write = sorted(glob.glob(os.path.join(prof, "r*_cfg3_pmc_write.json")))
-    if not fetch or not write:
-        return None, "no PMC profile committed"
+    fetch = sorted(glob.glob(os.path.join(prof, f"r*_{config}_pmc_fetch.json")))
+    write = {os.path.basename(w).split("_")[0]: w for w in glob.glob(os.path.join(prof, f"r*_{config}_pmc_write.json"))}
+    fetch = [f for f in fetch if os.path.basename(f).split("_")[0] in write]
+    if not fetch:
+        return None, f"no PMC profile committed for {config}"
+    tag = os.path.basename(fetch[-1]).split("_")[0]
     try:
         f = json.load(open(fetch[-1]))
-        w = json.load(open(write[-1]))
+        w = json.load(open(write[tag]))
+
         def per_dispatch(summary, prefix, counter):
             # every template instantiation of the kernel (e.g. k_roll_run<false, false>), weighted
             # by its dispatch count
@@ -88,7 +94,8 @@ def measured_traffic():
         kb = 0.0
         for name in ("void clrrt::k_roll_prep", "void clrrt::k_roll_run"):
             kb += 2.0 * per_dispatch(f, name, "FETCH_SIZE") + per_dispatch(w, name, "WRITE_SIZE")
-        return kb * 1024.0, (f"{os.path.basename(fetch[-1])} + {os.path.basename(write[-1])}: "
+        build = f.get("_build", "unrecorded build")
+        return kb * 1024.0, (f"{os.path.basename(fetch[-1])} + {os.path.basename(write[tag])} ({build}): "
                              "(2 x FETCH_SIZE [gfx950 half-count correction] + WRITE_SIZE) KiB per launch")
     except (KeyError, OSError, ValueError) as e:
         return None, f"PMC profile unreadable: {e}"
@@ -104,10 +111,11 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cfg, horizon_ms, n_queries, seed):
-    """The reference-faithful CPU restatement (oracle/, kind 'port'), 1 thread, same scene and
-    horizon: nodes appended per second of wall time, n_queries queries (fresh trees; config 5: the
-    replanning sequence with the tree re-initialised from the committed path)."""
+def _cpu_queries(cfg, horizon_ms, n_queries, seed):
+    """The reference-faithful CPU restatement (oracle/, kind 'port'), 1 thread: n_queries planning
+    queries of the same scene and horizon (fresh trees; config 5: the replanning sequence with the tree
+    re-initialised from the committed path).  Returns (nodes appended, goal nodes, wall seconds)."""
+    sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     from clrrt import abi, replan, scenes
@@ -148,11 +156,57 @@ def cpu_baseline(cfg, horizon_ms, n_queries, seed):
         n = o.nodes()
         nodes += len(n["goal"]) - 1
         goals += int(n["goal"].sum())
+    return nodes, goals, t_total
+
+
+def _replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
+    _cpu_queries(CONFIGS[cfg_name], 1.0, 1, seed)  # imports and library loads before the start line
+    barrier.wait()
+    t0 = time.perf_counter()
+    nodes, goals, _ = _cpu_queries(CONFIGS[cfg_name], horizon_ms, n_queries, seed)
+    out.put((nodes, goals, time.perf_counter() - t0))
+
+
+def cpu_share():
+    """Host cores this job may use: the affinity set, capped by OMP_NUM_THREADS where the GPU box sets
+    the job's CPU share (16 per GPU) — os.cpu_count() there is the whole machine's."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(cfg_name, horizon_ms, n_queries, seed, replica_queries=2):
+    """(1) one planner on 1 thread (the reference's execution model); (2) `cpu_share()` independent
+    planner replicas in separate processes, seeds seed..seed+R-1, aggregate nodes/s over the slowest
+    replica's wall time (SURVEY.md §8(d) CPU baseline)."""
+    import multiprocessing as mp
+    cfg = CONFIGS[cfg_name]
+    nodes, goals, t_total = _cpu_queries(cfg, horizon_ms, n_queries, seed)
+    R = cpu_share()
+    ctx = mp.get_context("spawn")
+    barrier, out = ctx.Barrier(R), ctx.Queue()
+    procs = [ctx.Process(target=_replica, args=(cfg_name, horizon_ms, replica_queries, seed + 100 * k, barrier, out))
+             for k in range(R)]
+    for p in procs:
+        p.start()
+    res = [out.get() for _ in range(R)]
+    for p in procs:
+        p.join()
+    wall = max(r[2] for r in res)
     return {
         "value": nodes / t_total, "unit": "nodes/s", "cores": 1, "kind": "port",
         "feasible_paths_per_s": goals / t_total,
         "sample": f"{n_queries} planMotion queries x {horizon_ms:.0f} ms wall budget, {cfg['obstacles']}+"
                   f"{cfg['moving']} obstacles, srand({seed}..{seed + n_queries - 1}), 1 thread, {cpu_model()}",
+        "replicas": {
+            "value": sum(r[0] for r in res) / wall, "unit": "nodes/s", "cores": R,
+            "feasible_paths_per_s": sum(r[1] for r in res) / wall,
+            "sample": f"{R} independent planner processes x {replica_queries} queries x {horizon_ms:.0f} ms, "
+                      f"seeds {seed}+100k, started together, aggregate nodes over the slowest replica's {wall:.2f} s, "
+                      f"{cpu_model()}",
+        },
     }
 
 
@@ -164,6 +218,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # the CPU baseline runs first, before this process touches the GPU (its replicas are separate
+    # processes; nothing else competes for the host cores while it runs)
+    cpu_line = None
+    if world == 1 and not args.no_cpu:
+        cpu_line = cpu_baseline(args.config, horizon, args.cpu_queries, args.seed)
 
     import torch
     import torch.distributed as dist
@@ -301,6 +361,20 @@ def main():
     other_ms, other_n = pl.kernel_time(2)
     work = pl.work_counters()
     cnt = pl.counters()
+    sw = pl.search_work()
+
+    exact_line = None
+    if world == 1 and not replanning and not args.no_exact:
+        # secondary figure: EXACT mode (the reference's sequential expandTree tree, bit for bit) on the
+        # same scene and horizon, one query from a fresh tree
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(args.seed), n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_EXACT, batch=B)
+        exact_line = {"value": st["nodes_added"] / (st["elapsed_ms"] * 1e-3), "unit": "nodes/s",
+                      "feasible_paths_per_s": st["goal_nodes_added"] / (st["elapsed_ms"] * 1e-3),
+                      "iterations": st["iterations"], "rounds": st["rounds"], "speculated": st["speculated"],
+                      "horizon_ms": horizon,
+                      "note": "EXACT mode: trees identical to the reference's sequential expandTree (same seed); "
+                              "1 query, wall clock"}
 
     if rank != 0:
         if world > 1:
@@ -308,12 +382,20 @@ def main():
             dist.destroy_process_group()
         return
 
-    traffic, traffic_note = measured_traffic()
-    fp64 = FLOP_STEP * work["steps"] + FLOP_SCAN * work["scan_points"]
-    fp32 = FLOP_BOX * work["box_tests"]
+    traffic, traffic_note = measured_traffic(args.config)
+    # Algorithmic work credited to the rollout kernel: the reference's own steps (sim_count: the
+    # candidates expandTree simulates, up to the first success), not the speculative candidates the
+    # kernel also started; scan points and box tests are counted on executed steps and scaled by the
+    # same ratio (they are per-step quantities).
+    spec = work["steps"] / cnt["sim_count"] if cnt["sim_count"] else 1.0
+    fp64 = FLOP_STEP * cnt["sim_count"] + FLOP_SCAN * work["scan_points"] / spec
+    fp32 = FLOP_BOX * work["box_tests"] / spec
     achieved_tf = (fp64 + fp32) / (roll_ms * 1e-3) / 1e12 if roll_ms > 0 else 0.0
     t_mix = fp64 / PEAK_FP64_VALU_TF + fp32 / PEAK_FP32_VALU_TF
     peak_tf = (fp64 + fp32) / t_mix if t_mix > 0 else PEAK_FP32_VALU_TF
+    avg_launch_ms = roll_ms / roll_n if roll_n else 0.0
+    hbm_gbs = traffic / (avg_launch_ms * 1e-3) / 1e9 if traffic and avg_launch_ms > 0 else None
+    nn_tf = sw["bf_keys"] * FLOP_KEY / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     value = tot_nodes / elapsed
     line = {
         "metric": "nodes expanded/sec (200-obstacle scene)",
@@ -349,11 +431,33 @@ def main():
             "traffic": traffic,
             "traffic_note": traffic_note,
             "launches": roll_n,
-            "avg_launch_ms": roll_ms / roll_n if roll_n else 0.0,
+            "avg_launch_ms": avg_launch_ms,
             "flop_per_launch": (fp64 + fp32) / roll_n if roll_n else 0.0,
             "fp64_flop": fp64,
             "fp32_flop": fp32,
+            "work_basis": "reference-semantic steps (sim_count); executed steps incl. speculative candidates "
+                          "= speculative_overhead x sim_count",
+            "speculative_overhead": spec,
+            "hbm_gbs": hbm_gbs,
+            "hbm_frac": hbm_gbs / PEAK_HBM_GBS if hbm_gbs else None,
+            "hbm_note": "traffic (PMC bytes per launch) / avg_launch_ms vs 8 TB/s HBM3E peak",
             "peak_note": "mix-weighted VALU peak: FP64 78.6 TF/s, FP32 157.3 TF/s (MI355X_MICROARCH.md)",
+        },
+        "roofline_nn": {
+            "bound": "valu",
+            "kernel": "nearest-node search (walk index build + k_walk_search + appended-node merge)",
+            "achieved": nn_tf,
+            "peak": PEAK_FP32_VALU_TF,
+            "unit": "TFLOP/s",
+            "frac": nn_tf / PEAK_FP32_VALU_TF,
+            "work_basis": "brute-force-equivalent Dubins keys (samples x tree nodes, SURVEY §8(d): 40 FP32 FLOP "
+                          "per key) over the search kernels' HIP-event time",
+            "bf_keys": sw["bf_keys"],
+            "samples": sw["samples"],
+            "tiles_per_sample": sw["tiles"] / sw["samples"] if sw["samples"] else 0.0,
+            "exact_keys_per_sample": sw["exact_keys"] / sw["samples"] if sw["samples"] else 0.0,
+            "launches": nn_n,
+            "kernel_ms": nn_ms,
         },
         "kernel_ms": {"rollout": roll_ms, "nn": nn_ms, "select_commit": other_ms,
                       "launches": {"rollout": roll_n, "nn": nn_n, "other": other_n}},
@@ -366,8 +470,10 @@ def main():
             "path_lengths": rp["path_len"][-args.steps:], "goal_nodes": rp["goal_nodes"][-args.steps:],
             "tree_nodes_last": pl.size()[0], "reinit_ms_avg": rp["reinit_ms"] / nq,
             "note": "outcome 0 empty, 1 all erased, 2 committed path collides, 3 re-initialised from the path"}
-    if not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(cfg, horizon, args.cpu_queries, args.seed)
+    if exact_line:
+        line["exact_mode"] = exact_line
+    if cpu_line:
+        line["cpu_baseline"] = cpu_line
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -70,6 +70,7 @@ _SIGS = {
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "clrrt_set_nn_grid": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
 }
@@ -389,6 +390,11 @@ class Planner:
         out = (C.c_int64 * 3)()
         self._chk(self.L.clrrt_work_counters(self.h, out), "work_counters")
         return {"steps": out[0], "scan_points": out[1], "box_tests": out[2]}
+
+    def search_work(self):
+        out = (C.c_int64 * 4)()
+        self._chk(self.L.clrrt_search_work(self.h, out), "search_work")
+        return {"bf_keys": out[0], "samples": out[1], "tiles": out[2], "exact_keys": out[3]}
 
     def reset_counters(self):
         self._chk(self.L.clrrt_reset_counters(self.h), "reset_counters")

@@ -153,6 +153,7 @@ struct clrrt_ctx {
   int64_t last_goal_nodes = 0;
   // counters
   clrrt_counters counters{};
+  int64_t nn_bf_keys = 0, nn_samples = 0;  // search work: brute-force-equivalent keys, samples searched
   // timing
   bool timing = false;
   double kt_ms[3] = {0, 0, 0};
@@ -1057,6 +1058,7 @@ int clrrt_get_counters(clrrt_ctx* c, clrrt_counters* out) {
 int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
+  c->nn_bf_keys = c->nn_samples = 0;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipMemsetAsync(c->work_ctr, 0, 40 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
@@ -1080,6 +1082,20 @@ int clrrt_work_counters(clrrt_ctx* c, int64_t out[3]) {
   HIPC(c, hipMemcpyAsync(h, c->work_ctr, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   for (int i = 0; i < 3; i++) out[i] = (int64_t)h[i];
+  return CLRRT_OK;
+}
+
+int clrrt_search_work(clrrt_ctx* c, int64_t out[4]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->side) HIPC(c, hipStreamSynchronize(c->side));
+  unsigned long long h[19];
+  HIPC(c, hipMemcpy(h, c->work_ctr + 8, sizeof(h), hipMemcpyDeviceToHost));
+  out[0] = c->nn_bf_keys;
+  out[1] = c->nn_samples;
+  out[2] = (int64_t)h[11];
+  out[3] = (int64_t)h[13];
   return CLRRT_OK;
 }
 
@@ -1259,6 +1275,8 @@ static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
 }
 
 static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
+  c->nn_bf_keys += (int64_t)n2 * c->n_nodes;
+  c->nn_samples += n2;
   HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));
   HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * n2, hipMemcpyHostToDevice, c->side));
   {
@@ -1277,6 +1295,7 @@ static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
   HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
   if (nn > 0) {
     KTimer kt(c, 0);
+    c->nn_bf_keys += (int64_t)n2 * nn;
     const NnSetup su2 = nn_setup(c);  // the box includes the appended nodes
     const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n2 * NN_K));
     HIPC(c, launch_nn_delta(c->stream, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
@@ -1295,6 +1314,8 @@ static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
 static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   hipStream_t st = c->stream;
   KTimer kt(c, 0);
+  c->nn_bf_keys += (int64_t)n * c->n_nodes;
+  c->nn_samples += n;
   int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
   NnGrid g{};
   const NnSetup su = nn_setup(c);

@@ -365,6 +365,11 @@ int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
  * tiles visited, out[12] nodes passing the prefilter, out[13] exact Dubins keys evaluated, out[14..18]
  * shader clocks per phase when the "nn_debug" option is 2 (diagnostics). */
 int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[19]);
+/* Nearest-node search work since the last clrrt_reset_counters (SURVEY §8(d) roofline basis of
+ * sortNodesExplore/Optimize, rrtplanner.cpp:227-268): out[0] = brute-force-equivalent Dubins keys
+ * (samples x tree nodes of every search, plus the appended nodes merged into prefetched lists),
+ * out[1] = samples searched, out[2] = walk-search tiles visited, out[3] = exact keys evaluated. */
+int clrrt_search_work(clrrt_ctx* ctx, int64_t out[4]);
 /* Diagnostics: the context's 40 raw work counters (0..2 rollout work, 8..26 search statistics,
  * 32..39 per-phase rollout clocks in a -DCLRRT_ROLL_PROFILE build). */
 int clrrt_debug_counters(clrrt_ctx* ctx, int64_t out[40]);

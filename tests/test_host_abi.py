@@ -73,7 +73,8 @@ def test_create_without_gpu_fails_loudly():
 
 
 def test_bench_reads_committed_pmc_traffic():
-    """bench.py's roofline.traffic comes from the newest committed FETCH_SIZE/WRITE_SIZE summaries;
+    """bench.py's roofline.traffic comes from the newest committed FETCH_SIZE/WRITE_SIZE summaries of the
+    benchmarked config;
     the kernel names carry template arguments that change between builds (k_roll_run<false, false>),
     so the reader must match every instantiation rather than one spelling."""
     import importlib.util
@@ -82,7 +83,20 @@ def test_bench_reads_committed_pmc_traffic():
     spec = importlib.util.spec_from_file_location("clrrt_bench", os.path.join(root, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    traffic, note = bench.measured_traffic()
+    traffic, note = bench.measured_traffic("cfg3")
     assert traffic is not None, note
-    # a cfg3 rollout launch writes ~0.4-0.5 GB of trajectory rows
-    assert 1e8 < traffic < 5e9, (traffic, note)
+    assert 1e7 < traffic < 5e9, (traffic, note)
+    # a config without committed PMC passes gets no traffic figure (not another config's)
+    traffic, note = bench.measured_traffic("cfg_none")
+    assert traffic is None and "no PMC profile" in note
+
+
+def test_bench_cpu_share_is_bounded():
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("clrrt_bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    n = bench.cpu_share()
+    assert 1 <= n <= (os.cpu_count() or 1)
