@@ -71,6 +71,7 @@ _SIGS = {
     "clrrt_set_nn_grid": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_obstacle_distance": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32, P(C.c_double)]),
     "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
 }
@@ -390,6 +391,14 @@ class Planner:
         out = (C.c_int64 * 3)()
         self._chk(self.L.clrrt_work_counters(self.h, out), "work_counters")
         return {"steps": out[0], "scan_points": out[1], "box_tests": out[2]}
+
+    def check_obs_distance(self, states):
+        """checkObsDistance (collision.h:41) for states [n, 10] -> [n] (clrrt_obstacle_distance)."""
+        x = np.ascontiguousarray(states, dtype=np.float64).reshape(-1, 10)
+        out = np.zeros(x.shape[0])
+        self._chk(self.L.clrrt_obstacle_distance(self.h, x.ctypes.data_as(P(C.c_double)), x.shape[0],
+                                                 out.ctypes.data_as(P(C.c_double))), "obstacle_distance")
+        return out
 
     def search_work(self):
         out = (C.c_int64 * 4)()

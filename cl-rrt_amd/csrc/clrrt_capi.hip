@@ -1739,6 +1739,23 @@ int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double*
   return CLRRT_OK;
 }
 
+int clrrt_obstacle_distance(clrrt_ctx* c, const double* states, int32_t n, double* out) {
+  if (!c || n < 0 || (n > 0 && (!states || !out))) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  double *din = nullptr, *dout = nullptr;
+  hipError_t e = hipMalloc((void**)&din, sizeof(double) * 10 * (size_t)n);
+  if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpyAsync(din, states, sizeof(double) * 10 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_obs_distance(c->stream, c->dp, c->obs, din, n, dout);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(din);
+  hipFree(dout);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("obstacle_distance: ") + hipGetErrorString(e));
+  return CLRRT_OK;
+}
+
 int clrrt_selftest_units(clrrt_ctx* c, int32_t unit, const double* in, int32_t n, double* out) {
   static const int kin[5] = {11, 9, 9, 12, 2};
   static const int kout[5] = {1, 8, 1, 1 + 3 * CLRRT_UNIT_PROFILE_NMAX, 2};

@@ -237,6 +237,8 @@ hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const in
 hipError_t launch_bbox(hipStream_t st, const clrrt_node* recs, const int64_t* n_dev, int n_host, double* out4);
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn);
 hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out);
+hipError_t launch_obs_distance(hipStream_t st, const DevParams& p, const BakedObs* obs, const double* states, int n,
+                               double* out);
 hipError_t launch_selftest_units(hipStream_t st, int unit, const double* in, const BakedObs* obs, int n,
                                  const DevParams& p, double* out);
 // extractBestPath helpers: goal nodes (id, costS) appended in any order (count in *cnt), and the

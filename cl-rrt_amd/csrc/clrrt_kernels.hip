@@ -1775,6 +1775,24 @@ __global__ void k_selftest_units(int unit, const double* __restrict__ in, const 
   }
 }
 
+// checkObsDistance(x) (collision.h:41; stub collisioncheck.cpp:6-8 or the OBB form
+// old_collisioncheck.cpp:24-51 under CLRRT_COLLISION_OBB) for n states of 10 doubles: the documented
+// collision hook, evaluated by the rollout kernels' own collision code (every obstacle, gap value kept).
+__global__ void k_obs_distance(DevParams p, const BakedObs* __restrict__ obs, const double* __restrict__ st, int n,
+                               double* __restrict__ out) {
+  glibc::stage_tables();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ObsView ov{obs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                   p.coll_mode == CLRRT_COLLISION_OBB ? p.n_obs : 0, 0, 0, 0, 0.f, 0.f, 0.f};
+  const double* x = st + 10 * (int64_t)i;
+  Roll r;
+  r.x0 = x[0]; r.x1 = x[1]; r.x2 = x[2]; r.x6 = x[6];
+  glibc::sincos(r.x2, r.s2, r.c2);
+  uint32_t tests = 0;
+  out[i] = obs_distance<true>(r, p, ov, tests);
+}
+
 // ============================================================================================
 // launch wrappers (host)
 // ============================================================================================
@@ -2136,6 +2154,14 @@ hipError_t launch_selftest_units(hipStream_t st, int unit, const double* in, con
                                  const DevParams& p, double* out) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_selftest_units, dim3((n + 255) / 256), dim3(256), 0, st, unit, in, obs, n, p, out);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_obs_distance(hipStream_t st, const DevParams& p, const BakedObs* obs, const double* states, int n,
+                               double* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_obs_distance, dim3((n + 255) / 256), dim3(256), 0, st, p, obs, states, n, out);
   LAUNCH_CHECK();
   return hipSuccess;
 }

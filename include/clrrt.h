@@ -296,6 +296,14 @@ int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t
  * calls without it; any other tree change discards the prefetch. */
 int clrrt_round_prefetch(clrrt_ctx* ctx, const clrrt_sample* next_samples, int32_t n);
 
+/* checkObsDistance(const vector<double>& x) (rrt/include/rrt/collision.h:41, the documented collision
+ * hook README.md:40-47): out[i] = the distance the context's collision mode gives for states[i] (10
+ * doubles: x, y, theta, ..., t in column 6) — 100 under CLRRT_COLLISION_STUB
+ * (collisioncheck.cpp:6-8), the OBB form of old_collisioncheck.cpp:24-51 (0 on overlap, else the
+ * smallest first-separating-axis gap, 10000 without obstacles) under CLRRT_COLLISION_OBB.  Evaluated on
+ * the device by the rollout kernels' own collision code. */
+int clrrt_obstacle_distance(clrrt_ctx* ctx, const double* states, int32_t n, double* out);
+
 /* ---- kernel-level parity entries ---- */
 int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n,
                         clrrt_rollout_result* out, double* rows_out, int32_t rows_cap);

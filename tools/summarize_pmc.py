@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --pmc counter_collection.csv per kernel: dispatches, sum and mean per dispatch
-of each counter.  Usage: summarize_pmc.py run_counter_collection.csv [more.csv ...] > summary.json"""
+of each counter.  Usage: summarize_pmc.py [--build COMMIT] run_counter_collection.csv [more.csv ...] > summary.json
+(--build records the profiled build's commit under "_build", which bench.py quotes in traffic_note)."""
 import collections
 import csv
 import json
 import sys
 
+args = sys.argv[1:]
+build = None
+if args and args[0] == "--build":
+    build, args = args[1], args[2:]
 out = collections.defaultdict(lambda: {"dispatches": 0, "counters": collections.defaultdict(float)})
-for path in sys.argv[1:]:
+for path in args:
     seen = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"].split("(")[0]
@@ -21,4 +26,6 @@ for k, v in out.items():
     res[k] = {"dispatches": v["dispatches"],
               "per_dispatch": {c: x / n for c, x in v["counters"].items()},
               "total": dict(v["counters"])}
+if build:
+    res["_build"] = build
 json.dump(res, sys.stdout, indent=1, sort_keys=True)
