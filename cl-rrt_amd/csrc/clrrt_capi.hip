@@ -1720,7 +1720,7 @@ int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, 
 }
 
 int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double* b, int32_t n, double* out) {
-  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 17) return CLRRT_EINVAL;
+  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 19) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
   double *da = nullptr, *db = nullptr, *dout = nullptr;

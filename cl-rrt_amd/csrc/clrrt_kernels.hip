@@ -1134,6 +1134,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     }
     if (j < 0 || fin >= 0) continue;
     steps++;
+    // The abandon check's load of best[s] is issued BEFORE this step's row stores: vmcnt counts loads
+    // and stores in issue order, so a load issued after the stores would wait for all ten of them to
+    // complete (measured: ~60% of the kernel's wave time); issued here it only waits for the previous
+    // step's stores, long retired.
+    const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
+    const int best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
     if (pc) pc->mark(6);
     int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
 #ifdef CLRRT_ROLL_PROFILE
@@ -1159,7 +1165,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
       fin = o;
-    } else if ((steps & (CLRRT_ABANDON_EVERY - 1)) == 0 && __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+    } else if (best_s < k) {
       // an earlier candidate of this sample succeeded: this result will not be looked at
       if (pass == 0) a.res[j].outcome = -1;
       a.res_gb[j].outcome = -1;
@@ -1708,6 +1714,26 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 15: r = round(x); break;
     case 16: { double sx, cx; glibc::sincos(x, sx, cx); r = sx; } break;
     case 17: { double sx, cx; glibc::sincos(x, sx, cx); r = cx; } break;
+    case 18: {  // diagnostics: latency of a rollout step's trig (sincos, cos, sin, tan), y[0] iterations
+      double z = x;
+      for (int it = 0; it < (int)y; it++) {
+        double sx, cx;
+        glibc::sincos(z, sx, cx);
+        const double c2 = glibc::cos(z), s2 = glibc::sin(z), t3 = glibc::tan(0.5 * sx);
+        z = z + 1e-3 * (sx + cx + c2 + s2 + t3);
+      }
+      r = z;
+    } break;
+    case 19: {  // diagnostics: the same loop with FP64 multiply-adds only (no table, no branch)
+      double z = x;
+      for (int it = 0; it < (int)y; it++) {
+        double q = z;
+#pragma unroll 1
+        for (int k = 0; k < 100; k++) q = q * 0.999999 + 1e-9;
+        z = z + 1e-3 * q;
+      }
+      r = z;
+    } break;
     default: r = 0.0; break;
   }
   out[i] = r;
