@@ -15,6 +15,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <climits>
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -29,6 +30,8 @@
 #include "../../include/clrrt.h"
 #include "clrrt_dev.hpp"
 #include "clrrt_internal.hpp"
+
+static const int kWalkMaxOver = 512, kWalkMaxChunks = 64;  // walk overflow records, split waves per record
 
 using namespace clrrt;
 
@@ -95,6 +98,8 @@ struct clrrt_ctx {
   int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
   bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
+  // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64)
+  int nnw_bud_tiles = 2048, nnw_bud_ex = 12288, nnw_chunks = 32;
   WalkBufs nnw{};                      // allocated on first use
   CompactBufs cmp{};                   // round compaction scratch
   int nng_modes = 1;
@@ -392,7 +397,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
-                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->cmp.packed, c->cmp.scanned,
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->cmp.packed, c->cmp.scanned,
                   c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1117,6 +1122,9 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
   else if (k == "nn_walk_min" && value >= 0) c->nnw_min_nodes = value;
   else if (k == "nn_walk_stateless") c->nnw_stateless = value != 0;
+  else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) c->nnw_bud_tiles = (int)value;
+  else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
+  else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
@@ -1195,6 +1203,10 @@ static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
 
 // Walk-search buffers, sized for the context's capacity (first use).
 static int ensure_walk(clrrt_ctx* c) {
+  c->nnw.bud_tiles = c->nnw_bud_tiles;
+  c->nnw.bud_ex = c->nnw_bud_ex;
+  c->nnw.max_over = kWalkMaxOver;
+  c->nnw.nch = c->nnw_chunks;
   if (c->nnw.P) return CLRRT_OK;
   const int64_t M = std::max<int64_t>(c->cap.max_nodes, c->cap.max_batch);
   const int64_t Mp = c->cap.max_nodes + 1024;
@@ -1212,6 +1224,10 @@ static int ensure_walk(clrrt_ctx* c) {
   HIPC(c, dalloc(&c->nnw.TRIG, Mp));
   HIPC(c, dalloc(&c->nnw.tiles, Mp / 64 + 1));
   HIPC(c, dalloc(&c->nnw.supers, Mp / 1024 + 1));
+  HIPC(c, dalloc(&c->nnw.ovf_n, 1));
+  HIPC(c, dalloc(&c->nnw.ovf, kWalkMaxOver));
+  HIPC(c, dalloc(&c->nnw.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
+  HIPC(c, dalloc(&c->nnw.pi, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
   HIPC(c, dalloc(&c->nnw.P, Mp));  // last: marks the set complete
   return CLRRT_OK;
 }

@@ -175,6 +175,14 @@ struct WalkBufs {
   int* HEAD;               // first record of the run of records with equal Dubins-key inputs
   double2* TRIG;           // (cos, sin)(ang_par) in double
   WalkTile *tiles, *supers;
+  // overflow of the walk: a sample whose walk passes the budget (tiles visited / exact keys) hands
+  // its search to nch waves over interleaved super-tile subsets with the list's 11th entry as the
+  // bound, then a merge wave (k_walk_split / k_walk_merge); budget 0 = off
+  int bud_tiles, bud_ex, max_over, nch;
+  int* ovf_n;    // [1] overflow records claimed
+  int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
+  float* pk;     // [max_over * nch * 11] partial lists
+  int* pi;
 };
 size_t walk_sort_bytes(int n);
 // Candidate lists of samples S[0 .. B) (same output as the brute force: cand, ckey, ncand, ctie);

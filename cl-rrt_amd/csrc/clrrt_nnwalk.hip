@@ -250,6 +250,51 @@ __device__ __forceinline__ float acos_apx(float x) {
   return x < 0.f ? 3.14159265f - r : r;
 }
 
+// atan2 in float, |error| <= 1e-6 rad (Abramowitz & Stegun 4.4.49 on the reduced ratio, 2e-8, plus
+// float evaluation; tests/test_nnwalk_bounds.py).  (x, y) != (0, 0).
+__device__ __forceinline__ float atan2_apx(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float z = fminf(ax, ay) * frcp(fmaxf(ax, ay));
+  const float z2 = z * z;
+  float p = 0.0028662257f;
+  p = p * z2 - 0.0161657367f;
+  p = p * z2 + 0.0429096138f;
+  p = p * z2 - 0.0752896400f;
+  p = p * z2 + 0.1065626393f;
+  p = p * z2 - 0.1420889944f;
+  p = p * z2 + 0.1999355085f;
+  p = p * z2 - 0.3333314528f;
+  float a = z + z * z2 * p;
+  if (ay > ax) a = 1.57079633f - a;
+  if (x < 0.f) a = 3.14159265f - a;
+  return y < 0.f ? -a : a;
+}
+
+// Lower bound on the float Dubins key (dubins_key) of a node whose rotated offset to the sample,
+// (tx, ty >= 0) as dubins_key forms it, lies within pos_err of the given one; -inf unless the sample
+// is well outside the turning circle (tangent length t >= 0.1).  There the key is the length of the
+// turn-then-straight path, t + rho (thc - acos(rho / dc)) with acos(rho / dc) = atan2(t, rho): a
+// function of the offset with gradient norm 1 (continuous outside the circle: thc wraps only inside
+// it), so moving the offset by pos_err moves the key by at most pos_err; the margin also covers the
+// float evaluation here and in the reference (checked by tests/test_nnwalk_bounds.py).
+// The same margin bounds the key from above: lo <= key <= hi (lo = -inf, hi = +inf when undecided).
+__device__ __forceinline__ void walk_key_range(float tx, float ty, float pos_err, float& lo, float& hi) {
+  const float rho = 4.77f;
+  const float t2 = tx * tx + ty * (ty - 2.f * rho);  // dc^2 - rho^2
+  if (!(t2 >= 0.01f)) {
+    lo = -__builtin_inff();
+    hi = __builtin_inff();
+    return;
+  }
+  const float t = fsqrt(t2);
+  float th = atan2_apx(tx, rho - ty);
+  if (th < 0.f) th += 6.28318531f;
+  const float L = t + rho * (th - atan2_apx(t, rho));
+  const float m = 2.f * pos_err + 2e-4f + 2e-5f * L;
+  lo = L - m;
+  hi = L + m;
+}
+
 // Lower bound on the keys of a tile's nodes for the sample at (rsx, rsy) (frame coordinates);
 // +inf: no node of the tile can enter the list (empty, or feasibleNode fails for all of them);
 // -inf: no bound (non-finite records).  flen = feasibility length lower limit.  Angles come from
@@ -323,6 +368,26 @@ __device__ __forceinline__ void w_insert(float& lk, int& li, float k, int i, int
   }
 }
 
+// Writes a sample's list (lanes 0..10, ascending) in k_nn_merge's format: the first min(sortLimit,
+// valid entries) node ids, the keys, the count and whether a key tie crosses the selection boundary.
+__device__ __forceinline__ void walk_emit(float lk, int li, int lane, int s, int sort_limit, int* __restrict__ cand,
+                                          float* __restrict__ ckey, int* __restrict__ ncand, int* __restrict__ ctie) {
+  const bool valid = lane < NN_K && li != 0x7fffffff;
+  const int nvalid = __popcll(__ballot(valid));
+  const int sel = min(sort_limit, nvalid);
+  const float nk = __shfl_down(lk, 1, 64);
+  const bool tie = lane < CAND_K && lane < sel && lane + 1 < nvalid && lk == nk;
+  const bool anytie = __ballot(tie) != 0;
+  if (lane < CAND_K) {
+    cand[s * CAND_K + lane] = lane < sel ? li : -1;
+    ckey[s * CAND_K + lane] = lk;
+  }
+  if (lane == 0) {
+    ncand[s] = sel;
+    ctie[s] = anytie;
+  }
+}
+
 // One wave per sample.  LDS per super-tile: s_lb = a lower bound (fp16, rounded down) of the keys in
 // its tiles not yet visited.  Pass k visits the tiles whose bound lies in (T_{k-1}, min(T_k, kth)]
 // (T_k grows geometrically from the smallest bound; a tile's bound is max(tile bound, super-tile
@@ -336,7 +401,17 @@ __device__ __forceinline__ void w_insert(float& lk, int& li, float k, int i, int
 #endif
 // STATE = true (trees up to ~1.3 M nodes): per super-tile a float bound and a visited-tile mask
 // (8 bytes) instead of the stateless fp16 interval scheme, which spends an extra bound per visit.
-template <bool STATE>
+//
+// Overflow.  A round's search lasts as long as its slowest samples, and a few samples need 10-100x
+// the median work (optimize samples near the root, where the costE bound is weak: 1e5 exact keys).
+// A sample whose walk passes the budget (bud_tiles tiles or bud_ex exact keys; 0 = no budget) claims
+// an overflow record (sample, the list's 11th entry) and stops; SPLIT = true then runs nch waves per
+// record, wave ch searching the super-tiles ch, ch + nch, ch + 2 nch, ... (interleaved, so the dense
+// region near the sample spreads over all of them) with the 11th entry as the initial bound, and
+// k_walk_merge takes the 11 smallest (key, node) pairs of the nch partial lists.  Every pair of the
+// sample's true list precedes that 11th entry, each wave's list is exact over its super-tiles, so the
+// merged list equals the walk's (and the brute force's).  Records beyond max_over: the walk goes on.
+template <bool STATE, bool SPLIT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_WALK_WAVES))) k_walk_search(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                     const float4* __restrict__ Q, const float* __restrict__ CE,
@@ -347,19 +422,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
                                                     int* __restrict__ ncand, int* __restrict__ ctie,
                                                     const int* __restrict__ sorder,
                                                     const double2* __restrict__ TRIG,
-                                                    unsigned long long* __restrict__ stats) {
-  extern __shared__ __half s_lb[];  // [nsup] bounds of the super-tiles' remaining tiles (stateless)
-  float* s_lbf = (float*)s_lb;               // STATE: [nsup] float bounds ...
-  uint32_t* s_vis = (uint32_t*)(s_lbf + nsup);  // ... and [nsup] visited / discarded tile masks
+                                                    unsigned long long* __restrict__ stats, int bud_tiles,
+                                                    int bud_ex, int* __restrict__ ovf_n, int4* __restrict__ ovf,
+                                                    int max_over, int nch, float* __restrict__ pk,
+                                                    int* __restrict__ pi, int nloc_max) {
+  // LDS is indexed by the wave's local super-tile index l (super-tile gst(l))
+  extern __shared__ __half s_lb[];  // [nloc] bounds of the super-tiles' remaining tiles (stateless)
+  float* s_lbf = (float*)s_lb;               // STATE: [nloc] float bounds ...
+  uint32_t* s_vis = (uint32_t*)(s_lbf + nloc_max);  // ... and [nloc] visited / discarded tile masks
   auto lds_lb = [&](int t) -> float { return STATE ? s_lbf[t] : __half2float(s_lb[t]); };
-  __shared__ int s_q[64];
+  __shared__ int s_q2[64];  // records past stage 1 (stage 2: exact keys) ...
+  __shared__ float s_b2[64];  // ... and their key lower bounds
   const int lane = threadIdx.x;
-  // XCD-aware: consecutive blocks go to the 8 XCDs in turn; XCD x takes the x-th eighth of the
-  // place-ordered samples, so its L2 holds the tree region those samples search
-  const int per = (B + 7) >> 3;
-  const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (t >= B) return;
-  const int s = sorder[t];
+  int s, ch = 0, nloc = nsup;
+  float kb = __builtin_inff();  // SPLIT: the pairs sought precede (kb, ib)
+  int ib = 0x7fffffff;
+  if constexpr (SPLIT) {
+    const int o = (int)blockIdx.x / nch;
+    ch = (int)blockIdx.x % nch;
+    if (o >= min(*ovf_n, max_over)) return;
+    const int4 rec = ovf[o];
+    s = rec.x;
+    kb = __int_as_float(rec.y);
+    ib = rec.z;
+    nloc = ch < nsup ? (nsup - ch + nch - 1) / nch : 0;
+  } else {
+    // XCD-aware: consecutive blocks go to the 8 XCDs in turn; XCD x takes the x-th eighth of the
+    // place-ordered samples, so its L2 holds the tree region those samples search
+    const int per = (B + 7) >> 3;
+    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (t >= B) return;
+    s = sorder[t];
+  }
+  auto gst = [&](int l) -> int { return SPLIT ? ch + l * nch : l; };  // super-tile of local index l
   const double sx = S[s].x, sy = S[s].y;
   const bool ex = S[s].explore != 0;
   const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
@@ -375,11 +470,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   const float dsR = sqrtf((rsx - Rx) * (rsx - Rx) + (rsy - Ry) * (rsy - Ry)) * (1.f - 1e-5f) - 2.f * dl - 1e-4f;
   float lk = __builtin_inff();
   int li = 0x7fffffff;
+  // lanes 0..10: the 11 smallest key upper bounds (walk_key_range) of visited nodes that are surely
+  // feasible; 11 nodes have keys <= uk[10], so no pair with a larger key enters the list
+  float uk = __builtin_inff();
   float kth = __builtin_inff();
   int idk = 0x7fffffff;
   float lim = __builtin_inff();  // explore: (prune radius + delta)^2
   float cb0 = -2.f;             // explore: cos of the largest heading-to-sample angle a node may have
-  int nq = 0;
+  int n2 = 0;
 #ifdef CLRRT_WALK_PROFILE
   const bool prof = fr.debug == 2;  // diagnostics: per-phase shader clocks into stats[4..8]
 #else
@@ -388,11 +486,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   uint64_t cyc[4] = {0, 0, 0, 0};   // super bounds, visit_super (incl.), visit4 (incl.), drain
   int hc = -1;       // run head whose key is known ...
   float kc = 0.f;    // ... and that key
-  unsigned long long n_sup = 0, n_tile = 0, n_q = 0, n_ex = 0;
+  unsigned long long n_sup = 0, n_tile = 0, n_q = 0, n_ex = 0, n_und = 0, n_sure = 0, n_drop = 0;
 
   auto refresh = [&]() {
     kth = uni(__shfl(lk, NN_K - 1, 64));
     idk = uni(__shfl(li, NN_K - 1, 64));
+    if (SPLIT && w_less(kb, ib, kth, idk)) { kth = kb; idk = ib; }
+    const float u10 = uni(__shfl(uk, NN_K - 1, 64));
+    if (u10 < kth) { kth = u10; idk = 0x7fffffff; }
     if (kth < __builtin_inff()) {
       const float R = (kth + 2e-4f) * (1.0f / 0.9999f);
       lim = uni(R < 0.f ? -1.f : (R + dl) * (R + dl));
@@ -403,15 +504,34 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   // Exact keys of the queued records; feasibleNode decided in float where the float angle / length
   // is far (> 1e-4 rad, relative 1e-5) from the limit, else in double as the reference does.  The key
   // of the last record is remembered with its run head (records of one run share their key).
-  auto drain = [&]() {
-    if (nq == 0) return;
+  // Stage 2: the records past stage 1 whose bound still does not exceed the 11th entry; their exact
+  // keys are computed once fewer than `room` slots remain (room 64: always).
+  auto drain_exact = [&](int room) {
+    if (n2 == 0) return;
+    {
+      const int jj = lane < n2 ? s_q2[lane] : 0;
+      const float bb = lane < n2 ? s_b2[lane] : 0.f;
+      const bool k2 = lane < n2 && !(bb > kth);
+      const uint64_t m2 = __ballot(k2);
+      __builtin_amdgcn_wave_barrier();
+      if (k2) {
+        const int pos = __popcll(m2 & ((1ull << lane) - 1));
+        s_q2[pos] = jj;
+        s_b2[pos] = bb;
+      }
+      __builtin_amdgcn_wave_barrier();
+      n_drop += n2 - __popcll(m2);
+      n2 = __popcll(m2);
+      if (n2 == 0 || n2 + room <= 64) return;
+    }
+    const int nq = n2;
     const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     n_ex += nq;
     bool c = false;
     float key = 0.f;
     int id = 0, j = 0;
     if (lane < nq) {
-      j = s_q[lane];
+      j = s_q2[lane];
       id = ID[j];
       const NnRec& r = nodes[id];
       key = dubins_key(sx, sy, r.x, r.y, r.c, r.s);
@@ -463,9 +583,68 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         refresh();
       }
     }
-    nq = 0;
+    n2 = 0;
     if (prof) cyc[3] += __builtin_amdgcn_s_memtime() - c0;
   };
+  // Stage 1 (on the visited records that pass the prefilter): key bounds by walk_key_range.  The
+  // upper bounds of surely feasible records tighten the 11th entry; the records whose lower bound does
+  // not exceed it are queued for the exact keys (stage 2), which run on full waves of them.
+  const float f2_sure = fmaxf((float)(p.feas_len * p.feas_len) * 1.002f + 1e-3f, (1e4f * dl) * (1e4f * dl));
+  auto stage1 = [&](bool ok, float4 pp, float4 qq, float ce, float& lbt, float& ubt) {
+    lbt = __builtin_inff();
+    ubt = __builtin_inff();
+    if (!ok) return;
+    const float qx = rsx - pp.x, qy = rsy - pp.y;
+    const float tx = pp.z * qx - pp.w * qy, ty = fabsf(pp.w * qx + pp.z * qy);
+    float lo, hi;
+    walk_key_range(tx, ty, 4.f * dl + 1e-6f * (fabsf(tx) + ty), lo, hi);
+    const float cst = ex ? 0.f : ce;  // explore keys carry no cost
+    const float tlo = cst + lo, thi = cst + hi;
+    lbt = tlo - 1e-6f * fabsf(tlo);
+    // feasibleNode surely holds: the frame offset v errs by < 3 delta and |v| >= 1e4 delta, so its
+    // direction errs by < 3e-4 rad (the cos^2 margin 0.502 is 2e-3 rad inside pi/4); |v| errs by
+    // < 3 delta (the length margin is relative 1e-3 + 1e-3 absolute on |v|^2)
+    const float vx = rsx - qq.x, vy = rsy - qq.y;
+    const float dot = vx * qq.z + vy * qq.w, vv = vx * vx + vy * vy;
+    const bool sure = dot > 0.f && dot * dot >= 0.502f * vv && vv >= f2_sure;
+    ubt = sure ? thi + 1e-6f * fabsf(thi) : __builtin_inff();
+  };
+  // upper bounds below the 11th entry enter the bound list (lanes 0..10)
+  auto ub_insert = [&](float ubt) {
+    uint64_t mu = __ballot(ubt < kth);
+    if (!mu) return false;
+    while (mu) {
+      const int l = __ffsll((unsigned long long)mu) - 1;
+      mu &= mu - 1;
+      const float v = __shfl(ubt, l, 64);
+      const float u10 = uni(__shfl(uk, NN_K - 1, 64));
+      if (v < u10) {
+        const int pos = __popcll(__ballot(uk <= v && lane < NN_K));
+        const float up = __shfl_up(uk, 1, 64);
+        if (lane < NN_K) {
+          if (lane == pos) uk = v;
+          else if (lane > pos) uk = up;
+        }
+      }
+    }
+    return true;
+  };
+  auto enqueue = [&](bool ok, float lbt, int j) {
+    const bool keep = ok && !(lbt > kth);
+    const uint64_t m = __ballot(keep);
+    const int cnt = __popcll(m);
+    if (cnt == 0) return;
+    if (n2 + cnt > 64) drain_exact(cnt);
+    __builtin_amdgcn_wave_barrier();
+    if (keep) {
+      const int pos = n2 + __popcll(m & ((1ull << lane) - 1));
+      s_q2[pos] = j;
+      s_b2[pos] = lbt;
+    }
+    n2 += cnt;
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto drain = [&]() { drain_exact(64); };
   // Necessary conditions for record j to enter the list (the brute-force prefilter + turning bound).
   auto prefilter = [&](int id, int hd, float4 pp, float4 qq, float ce) -> bool {
     if (hd == hc && !w_less(kc, id, kth, idk)) return false;  // key known: kc
@@ -500,17 +679,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     }
     return !ang_bad && !in_bad && !turn_bad;
   };
-  auto enqueue = [&](bool ok, int j) {
-    const uint64_t m = __ballot(ok);
-    const int cnt = __popcll(m);
-    if (cnt == 0) return;
-    n_q += cnt;
-    if (nq + cnt > 64) drain();
-    if (ok) s_q[nq + __popcll(m & ((1ull << lane) - 1))] = j;
-    nq += cnt;
-    __builtin_amdgcn_wave_barrier();
-    if (nq == 64) drain();
-  };
   // nodes of up to four tiles: t0 / t1 on lanes 0-31 / 32-63 (first set), t2 / t3 (second set);
   // -1 = none.  Both sets' records are loaded before either is tested.
   auto visit4 = [&](int t0, int t1, int t2, int t3) {
@@ -526,8 +694,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     if (jb >= 0) { idb = ID[jb]; hb = HEAD[jb]; pb = P[jb]; qb = Q[jb]; cb = CE[jb]; }
     const bool oka = prefilter(ida, ha, pa, qa, ca);
     const bool okb = prefilter(idb, hb, pb, qb, cb);
-    enqueue(oka, ja);
-    enqueue(okb, jb);
+    n_q += __popcll(__ballot(oka)) + __popcll(__ballot(okb));
+    float la, ua, lb, ub;
+    stage1(oka, pa, qa, ca, la, ua);
+    stage1(okb, pb, qb, cb, lb, ub);
+    n_und += __popcll(__ballot(la == -__builtin_inff())) + __popcll(__ballot(lb == -__builtin_inff()));
+    n_sure += __popcll(__ballot(ua < __builtin_inff())) + __popcll(__ballot(ub < __builtin_inff()));
+    const bool ia = ub_insert(ua);
+    const bool ib2 = ub_insert(ub);
+    if (ia || ib2) refresh();
+    enqueue(oka, la, ja);
+    enqueue(okb, lb, jb);
     if (prof) cyc[2] += __builtin_amdgcn_s_memtime() - c0;
   };
   // visit the tiles of super-tile st whose bounds lie in (Tp, min(T, kth)] (pass 0: <= min(T, kth));
@@ -541,15 +718,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   // visit the tiles of super-tiles sa (lanes 0-31) and sb (lanes 32-63, -1: none) whose bounds lie in
   // (Tp, min(T, kth)] (STATE: not visited yet and <= min(T, kth)); the super-tiles' LDS bounds become
   // those of their tiles beyond T
-  auto visit_supers = [&](int sa, int sb, float Tp, float T, bool first) {
+  auto visit_supers = [&](int la, int lb2, float Tp, float T, bool first) {
     const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    n_sup += 1 + (sb >= 0);
+    n_sup += 1 + (lb2 >= 0);
+    const int sa = gst(la), sb = lb2 >= 0 ? gst(lb2) : -1;
+    const int lo = lane < 32 ? la : lb2;  // local index (LDS)
     const int st = lane < 32 ? sa : sb;
     const int tl = st * WALK_SUPER + (lane & 31);
     float lb = __builtin_inff();
     uint64_t tm;
     if constexpr (STATE) {
-      const uint32_t vis = st >= 0 ? s_vis[st] : 0xffffffffu;
+      const uint32_t vis = st >= 0 ? s_vis[lo] : 0xffffffffu;
       if (st >= 0 && tl < ntiles && !((vis >> (lane & 31)) & 1u)) {
 #if WALK_CHEAP_FIRST
         // the distance-only part of the bound first: a tile it already places beyond min(T, kth) skips the
@@ -569,8 +748,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       const float rest = hmin(take || drop || st < 0 ? __builtin_inff() : lb);
       if ((lane & 31) == 0 && st >= 0) {
         const int sh = lane;  // 0 or 32
-        s_vis[st] = vis | (uint32_t)(tm >> sh) | (uint32_t)(dm >> sh);
-        s_lbf[st] = rest;
+        s_vis[lo] = vis | (uint32_t)(tm >> sh) | (uint32_t)(dm >> sh);
+        s_lbf[lo] = rest;
       }
     } else {
       float sl = __builtin_inff();
@@ -580,7 +759,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       const bool take = st >= 0 && (first || lb > Tp) && lb <= T && !(lb > kth);
       tm = __ballot(take);
       const float rest = hmin(st >= 0 && lb > T ? lb : __builtin_inff());
-      if ((lane & 31) == 0 && st >= 0) s_lb[st] = __float2half_rd(rest);
+      if ((lane & 31) == 0 && st >= 0) s_lb[lo] = __float2half_rd(rest);
     }
     // tiles that the list has pruned since they were selected are skipped
     auto next_tile = [&]() -> int {
@@ -604,11 +783,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
 
   // 1. super-tile bounds
   const uint64_t ct0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  auto flush_stats = [&]() {
+    if (stats && lane == 0) {
+      atomicAdd(&stats[0], n_sup);
+      atomicAdd(&stats[1], n_tile);
+      atomicAdd(&stats[2], n_q);
+      atomicAdd(&stats[3], n_ex);
+      atomicAdd(&stats[10], n_und);   // stage 1: undecided bounds (near the turning circle)
+      atomicAdd(&stats[11], n_sure);  // stage 1: surely feasible (upper bounds)
+      atomicAdd(&stats[12], n_drop);  // stage 2: dropped by the refilter
+      if (prof) {
+        atomicAdd(&stats[4], (unsigned long long)cyc[0]);
+        atomicAdd(&stats[5], (unsigned long long)cyc[1]);
+        atomicAdd(&stats[6], (unsigned long long)cyc[2]);
+        atomicAdd(&stats[7], (unsigned long long)cyc[3]);
+        atomicAdd(&stats[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0));
+      }
+    }
+  };
+  if (SPLIT) refresh();  // the initial bound
   float mlb = __builtin_inff();
-  for (int t0 = 0; t0 < nsup; t0 += 64) {
+  for (int t0 = 0; t0 < nloc; t0 += 64) {
     const int t = t0 + lane;
-    if (t < nsup) {
-      const float lb = walk_lb(sup[t], rsx, rsy, ex, flen_t, dsR);
+    if (t < nloc) {
+      const float lb = walk_lb(sup[gst(t)], rsx, rsy, ex, flen_t, dsR);
       if constexpr (STATE) {
         s_lbf[t] = lb;
         s_vis[t] = 0u;
@@ -630,11 +828,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
 #define WALK_GROW 2.f
 #endif
   float T = base + WALK_T0, Tp = -__builtin_inff();
+  bool budget = !SPLIT && (bud_tiles > 0 || bud_ex > 0);
   for (int pass = 0;; pass++) {
     const float lim_t = fminf(T, kth);
-    for (int t0 = 0; t0 < nsup; t0 += 64) {
+    for (int t0 = 0; t0 < nloc; t0 += 64) {
       const int t = t0 + lane;
-      const float lb = t < nsup ? lds_lb(t) : __builtin_inff();
+      const float lb = t < nloc ? lds_lb(t) : __builtin_inff();
       uint64_t m = __ballot(lb < __builtin_inff() && lb <= lim_t);
       while (m) {
         // two super-tiles per visit (one per half wave)
@@ -646,6 +845,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
           if (sa < 0) sa = st; else sb = st;
         }
         if (sa >= 0) visit_supers(sa, sb, Tp, T, pass == 0);
+        if (budget && ((bud_tiles > 0 && n_tile > (unsigned long long)bud_tiles) ||
+                       (bud_ex > 0 && n_ex > (unsigned long long)bud_ex))) {
+          int slot = 0;
+          if (lane == 0) slot = atomicAdd(ovf_n, 1);
+          slot = uni(__shfl(slot, 0, 64));
+          if (slot < max_over) {  // hand over: the split waves and the merge write this sample's list
+            if (lane == 0) ovf[slot] = make_int4(s, __float_as_int(kth), idk == 0x7fffffff ? idk : idk + 1, 0);
+            if (stats && lane == 0) atomicAdd(&stats[14], 1ull);  // overflow records (work_ctr[32])
+            flush_stats();
+            return;
+          }
+          budget = false;  // no record left: finish here
+        }
       }
     }
     drain();
@@ -654,34 +866,55 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     T = base + (T - base) * WALK_GROW;
     if (T > 1e7f) T = __builtin_inff();
   }
-  // 3. output (k_nn_merge's format)
-  const bool valid = lane < NN_K && li != 0x7fffffff;
-  const int nvalid = __popcll(__ballot(valid));
-  const int sel = min(p.sort_limit, nvalid);
-  const float nk = __shfl_down(lk, 1, 64);
-  const bool tie = lane < CAND_K && lane < sel && lane + 1 < nvalid && lk == nk;
-  const bool anytie = __ballot(tie) != 0;
-  if (lane < CAND_K) {
-    cand[s * CAND_K + lane] = lane < sel ? li : -1;
-    ckey[s * CAND_K + lane] = lk;
-  }
-  if (lane == 0) {
-    ncand[s] = sel;
-    ctie[s] = anytie;
-  }
-  if (stats && lane == 0) {
-    atomicAdd(&stats[0], n_sup);
-    atomicAdd(&stats[1], n_tile);
-    atomicAdd(&stats[2], n_q);
-    atomicAdd(&stats[3], n_ex);
-    if (prof) {
-      atomicAdd(&stats[4], (unsigned long long)cyc[0]);
-      atomicAdd(&stats[5], (unsigned long long)cyc[1]);
-      atomicAdd(&stats[6], (unsigned long long)cyc[2]);
-      atomicAdd(&stats[7], (unsigned long long)cyc[3]);
-      atomicAdd(&stats[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0));
+  // 3. output (k_nn_merge's format); SPLIT: the wave's partial list
+  if constexpr (SPLIT) {
+    const int o = (int)blockIdx.x / nch;
+    if (lane < NN_K) {
+      pk[((size_t)o * nch + ch) * NN_K + lane] = lk;
+      pi[((size_t)o * nch + ch) * NN_K + lane] = li;
     }
+  } else {
+    walk_emit(lk, li, lane, s, p.sort_limit, cand, ckey, ncand, ctie);
   }
+  flush_stats();
+}
+
+// The 11 smallest (key, node) pairs of an overflow sample's nch partial lists (one wave per record);
+// pairs of different waves differ in the node, padding entries (inf, INT_MAX) sort last.
+__global__ void __launch_bounds__(64) k_walk_merge(const int* __restrict__ ovf_n, const int4* __restrict__ ovf,
+                                                   int max_over, int nch, const float* __restrict__ pk,
+                                                   const int* __restrict__ pi, int sort_limit, int* __restrict__ cand,
+                                                   float* __restrict__ ckey, int* __restrict__ ncand,
+                                                   int* __restrict__ ctie) {
+  const int o = blockIdx.x;
+  if (o >= min(*ovf_n, max_over)) return;
+  const int lane = threadIdx.x;
+  const int s = ovf[o].x;
+  const int n = nch * NN_K;
+  const float* k = pk + (size_t)o * n;
+  const int* id = pi + (size_t)o * n;
+  float lk = __builtin_inff(), pkey = -__builtin_inff();
+  int li = 0x7fffffff, pid = INT_MIN;
+  for (int r = 0; r < NN_K; r++) {
+    // the smallest pair after (pkey, pid)
+    float bk = __builtin_inff();
+    int bi = 0x7fffffff;
+    for (int j = lane; j < n; j += 64) {
+      const float kj = k[j];
+      const int ij = id[j];
+      if (w_less(pkey, pid, kj, ij) && w_less(kj, ij, bk, bi)) { bk = kj; bi = ij; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ok = __shfl_xor(bk, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (w_less(ok, oi, bk, bi)) { bk = ok; bi = oi; }
+    }
+    if (lane == r) { lk = bk; li = bi; }
+    pkey = bk;
+    pid = bi;
+  }
+  walk_emit(lk, li, lane, s, sort_limit, cand, ckey, ncand, ctie);
 }
 
 size_t walk_sort_bytes(int n) {
@@ -823,8 +1056,13 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   const bool state = nsup <= 1280 && !stateless;
   const size_t lds = (state ? 2 * sizeof(float) : sizeof(__half)) * (size_t)nsup;
   if (lds > 64 * 1024) {
-    e = hipFuncSetAttribute(state ? (const void*)&k_walk_search<true> : (const void*)&k_walk_search<false>,
+    e = hipFuncSetAttribute(state ? (const void*)&k_walk_search<true, false> : (const void*)&k_walk_search<false, false>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  const bool split = (w.bud_tiles > 0 || w.bud_ex > 0) && w.max_over > 0 && w.nch > 0 && w.ovf_n;
+  if (split) {
+    e = hipMemsetAsync(w.ovf_n, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
   }
   // samples in place order (radix sort of their Morton keys; the node sort's buffers are free again)
@@ -833,15 +1071,29 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   bytes = w.tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
   if (e != hipSuccess) return e;
+  const int bt = split ? w.bud_tiles : 0, be = split ? w.bud_ex : 0;
   if (state)
-    hipLaunchKernelGGL(k_walk_search<true>, dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q, w.CE,
-                       w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, w.TRIG,
-                       stats);
+    hipLaunchKernelGGL((k_walk_search<true, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q,
+                       w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder,
+                       w.TRIG, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   else
-    hipLaunchKernelGGL(k_walk_search<false>, dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q, w.CE,
-                       w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, w.TRIG,
-                       stats);
+    hipLaunchKernelGGL((k_walk_search<false, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P,
+                       w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,
+                       w.sorder, w.TRIG, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   LAUNCH_CHECK3();
+  if (split) {
+    // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
+    // claimed records exit at once) and the merge
+    const int nl = (nsup + w.nch - 1) / w.nch;
+    hipLaunchKernelGGL((k_walk_search<true, true>), dim3(w.max_over * w.nch), dim3(64), 2 * sizeof(float) * (size_t)nl,
+                       st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
+                       ckey, ncand, ctie, w.sorder, w.TRIG, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
+                       nl);
+    LAUNCH_CHECK3();
+    hipLaunchKernelGGL(k_walk_merge, dim3(w.max_over), dim3(64), 0, st, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
+                       p.sort_limit, cand, ckey, ncand, ctie);
+    LAUNCH_CHECK3();
+  }
   return hipSuccess;
 }
 

@@ -38,11 +38,17 @@ def _scene(kind):
 def _nn_strategy(pl, name):
     """Select the nearest-node search: 'brute' (node order), 'ordered' (place-ordered brute force with
     tile skipping), 'grid' (wave-uniform grid search + brute-force fallback) or 'walk' (one wave per
-    sample over place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes)."""
+    sample over place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes).  'walk_split*':
+    the walk with a budget of one tile, so every sample hands its search to the split waves and the
+    merge (the overflow path of large trees), 7 waves per sample (odd interleave)."""
     pl.set_nn_grid(0 if name == "grid" else 1 << 40, 3, 0)
     pl.set_option("nn_ordered_min", 0 if name == "ordered" else 1 << 40)
-    pl.set_option("nn_walk_min", 0 if name in ("walk", "walk_stateless") else 1 << 40)
-    pl.set_option("nn_walk_stateless", name == "walk_stateless")
+    pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
+    pl.set_option("nn_walk_stateless", name.endswith("stateless"))
+    split = name.startswith("walk_split")
+    pl.set_option("nn_walk_budget_tiles", 1 if split else 2048)
+    pl.set_option("nn_walk_budget_keys", 1 if split else 12288)
+    pl.set_option("nn_walk_chunks", 7 if split else 32)
 
 
 def _pair(kind, seed=1, iters=40):
@@ -95,7 +101,8 @@ def test_rollout_parity(kind):
 @pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "grid"),
                                            ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered"),
                                            ("empty", "walk"), ("obb200", "walk"), ("moving", "walk"),
-                                           ("obb200", "walk_stateless")])
+                                           ("obb200", "walk_stateless"), ("obb200", "walk_split"),
+                                           ("moving", "walk_split"), ("obb200", "walk_split_stateless")])
 def test_nearest_node_parity(kind, strategy):
     o, pl = _pair(kind, seed=4, iters=150)
     _nn_strategy(pl, strategy)
@@ -136,7 +143,8 @@ def _compare_trees(o, pl, label):
                                                       ("moving", 4, 250, "grid"), ("obb200", 5, 300, "ordered"),
                                                       ("moving", 4, 250, "ordered"), ("empty", 1, 200, "walk"),
                                                       ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk"),
-                                                      ("obb200", 5, 300, "walk_stateless")])
+                                                      ("obb200", 5, 300, "walk_stateless"),
+                                                      ("obb200", 3, 300, "walk_split")])
 def test_exact_mode_tree_parity(kind, seed, iters, strategy):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)
@@ -359,3 +367,22 @@ def test_round_prefetch_identical():
     print(f"round prefetch: {trees[1][2]} nodes")
     assert trees[0][2] > 20000
     assert trees[0][0] == trees[1][0] and trees[0][1] == trees[1][1]
+
+
+@pytest.mark.parametrize("chunks", [1, 32, 64])
+def test_walk_overflow_matches_brute(chunks):
+    """More overflowing samples than overflow records (512): the first 512 go through the split waves
+    and the merge, the rest finish their own walk; every list equals the brute force's bit for bit."""
+    o, pl = _pair("obb200", seed=6, iters=300)
+    smp = list(clrrt.Rng(23).draw_samples(pl.params, 2000))
+    _nn_strategy(pl, "brute")
+    ib, kb = pl.sort_nodes_batch(smp)
+    _nn_strategy(pl, "walk_split")
+    pl.set_option("nn_walk_chunks", chunks)
+    pl.reset_counters()
+    iw, kw = pl.sort_nodes_batch(smp)
+    records = pl.debug_counters()[32]
+    print(f"{o.size()} nodes, {len(smp)} samples, overflow records {records}")
+    assert records == 512
+    assert np.array_equal(ib, iw)
+    assert np.array_equal(np.asarray(kb, np.float32).view(np.uint32), np.asarray(kw, np.float32).view(np.uint32))

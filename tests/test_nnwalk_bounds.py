@@ -6,7 +6,9 @@ restate the key in float32 numpy on many random node-frame points and check the 
 relies on, with the margins it uses:
   * key >= rho * beta - 5e-3  (beta = angle between the node heading and the sample direction);
   * key >= |q| - 1e-4 - 1e-5 |q|;
-  * acos_apx (Abramowitz & Stegun 4.4.45) within 1e-4 rad of acos on [-1, 1].
+  * acos_apx (Abramowitz & Stegun 4.4.45) within 1e-4 rad of acos on [-1, 1];
+  * atan2_apx (A&S 4.4.49) within 1e-6 rad of atan2, and walk_key_range (the stage-1 key bounds of
+    the walk's drains) below / above the key of every offset within pos_err of its own.
 """
 import numpy as np
 
@@ -63,3 +65,67 @@ def test_acos_approximation():
     r = np.sqrt(np.float32(1) - ax) * p
     r = np.where(x < 0, np.float32(np.pi) - r, r)
     assert np.abs(r.astype(np.float64) - np.arccos(x.astype(np.float64))).max() < 1e-4
+
+
+F = np.float32
+
+
+def atan2_apx(y, x):
+    """atan2_apx of clrrt_nnwalk.hip in float32."""
+    y, x = y.astype(F), x.astype(F)
+    ax, ay = np.abs(x), np.abs(y)
+    z = (np.minimum(ax, ay) / np.maximum(ax, ay)).astype(F)
+    z2 = z * z
+    p = F(0.0028662257)
+    for c in (-0.0161657367, 0.0429096138, -0.0752896400, 0.1065626393, -0.1420889944, 0.1999355085,
+              -0.3333314528):
+        p = p * z2 + F(c)
+    a = z + z * z2 * p
+    a = np.where(ay > ax, F(1.57079633) - a, a)
+    a = np.where(x < 0, F(3.14159265) - a, a)
+    return np.where(y < 0, -a, a).astype(F)
+
+
+def walk_key_range(tx, ty, pos_err):
+    tx, ty = tx.astype(F), ty.astype(F)
+    rho = RHO
+    t2 = tx * tx + ty * (ty - F(2) * rho)
+    ok = t2 >= F(0.01)
+    t = np.sqrt(np.where(ok, t2, F(1)))
+    th = atan2_apx(tx, rho - ty)
+    th = np.where(th < 0, th + F(6.28318531), th)
+    L = t + rho * (th - atan2_apx(t, rho))
+    m = F(2) * pos_err + F(2e-4) + F(2e-5) * L
+    return (np.where(ok, L - m, -np.inf).astype(np.float64), np.where(ok, L + m, np.inf).astype(np.float64))
+
+
+def test_atan2_approximation():
+    rng = np.random.default_rng(11)
+    for scale in (1e-3, 1.0, 50.0, 1e4):
+        y = (rng.uniform(-1, 1, 1_000_000) * scale).astype(F)
+        x = (rng.uniform(-1, 1, 1_000_000) * scale).astype(F)
+        err = np.abs(atan2_apx(y, x).astype(np.float64) - np.arctan2(y.astype(np.float64), x.astype(np.float64)))
+        err = np.minimum(err, 2 * np.pi - err)  # +-pi
+        assert err.max() < 1e-6, (scale, err.max())
+
+
+def test_stage1_key_bound():
+    """walk_key_range at an offset jittered by up to pos_err brackets the float key at the true one."""
+    rng = np.random.default_rng(12)
+    pos = 4 * 2e-5  # 4 * delta of a 300 m frame (delta = 2^-24 * coordinate bound) -- generous
+    tight = []
+    for scale in (2.0, 6.0, 12.0, 40.0, 150.0):
+        tx, ty = _points(rng, 400_000, scale)
+        tx, ty = tx.astype(F), ty.astype(F)
+        key = dubins_key_f32(tx, ty)
+        ang = rng.uniform(0, 2 * np.pi, tx.size)
+        r = pos * np.sqrt(rng.uniform(0, 1, tx.size))
+        jx = (tx + r * np.cos(ang)).astype(F)
+        jy = np.abs(ty + r * np.sin(ang)).astype(F)
+        pe = F(pos) + F(1e-6) * (np.abs(jx) + jy)
+        lb, ub = walk_key_range(jx, jy, pe)
+        ok = np.isfinite(key) & np.isfinite(lb)
+        assert (key[ok] - lb[ok]).min() >= 0, (scale, (key[ok] - lb[ok]).min())
+        assert (ub[ok] - key[ok]).min() >= 0, (scale, (ub[ok] - key[ok]).min())
+        tight.append(np.median(key[ok] - lb[ok]))
+    assert max(tight) < 0.02, tight  # and it is tight: the stage-1 filter rejects what the key would

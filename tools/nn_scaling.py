@@ -38,17 +38,22 @@ for lab, pick in (("explore", 1), ("optimize", 0)):
 # per-sample cost spread: exact keys and tiles of 400 single samples (optimize and explore)
 for lab, pick in (("explore", 1), ("optimize", 0)):
     sub = [s for s in smp if s.explore == pick][:300]
-    ex, ti, tm = [], [], []
+    ex, ti, tm, qd = [], [], [], []
     for s in sub:
         pl.reset_counters()
         t0 = time.perf_counter()
         pl.sort_nodes_batch([s], exact=False)
         tm.append((time.perf_counter() - t0) * 1e3)
         st = pl.nn_stats()
+        dc = pl.debug_counters()
         ex.append(st["walk_exact"]); ti.append(st["walk_tiles"])
+        qd.append((st["walk_queued"], dc[28], dc[29], dc[30]))
     ex, ti, tm = np.array(ex), np.array(ti), np.array(tm)
     q = lambda a: [round(float(np.percentile(a, p)), 1) for p in (50, 90, 99, 100)]
     print(f"{lab}: single-sample exact keys p50/90/99/max {q(ex)}, tiles {q(ti)}, ms {q(tm)}")
+    qd = np.array(qd)
+    print(f"   per sample: queued {qd[:, 0].mean():.0f}, stage-1 undecided {qd[:, 1].mean():.0f}, surely feasible "
+          f"{qd[:, 2].mean():.0f}, stage-2 dropped {qd[:, 3].mean():.0f}, exact {ex.mean():.0f}")
     far = np.argsort(-ex)[:3]
     for i in far:
         print(f"   costly sample ({sub[i].x:.2f}, {sub[i].y:.2f}): exact {ex[i]}, tiles {ti[i]}, {tm[i]:.2f} ms")

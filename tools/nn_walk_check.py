@@ -40,6 +40,23 @@ bad = np.nonzero(~np.all(ib == iw, axis=1))[0]
 print(f"brute {tb:.2f} ms, walk {tw:.2f} ms; lists equal: {len(bad) == 0} ({len(bad)} differ); keys equal "
       f"{np.array_equal(kb.view(np.uint32), kw.view(np.uint32))}")
 print("walk stats", {k: v for k, v in sw.items() if k.startswith("walk")})
+# overflow budget sweep (tiles, exact keys; 0 = off): time and identity with the brute force
+for bt, be in ((0, 0), (8192, 49152), (4096, 24576), (2048, 12288), (1024, 8192)):
+    for nch in ((32,) if bt in (0, 8192) else (16, 32)):
+        pl.set_option("nn_walk_budget_tiles", bt)
+        pl.set_option("nn_walk_budget_keys", be)
+        pl.set_option("nn_walk_chunks", nch)
+        best = 1e9
+        for _ in range(3):
+            tx, (ix, kx), _ = timed(True)
+            best = min(best, tx)
+        nov = pl.debug_counters()[32]
+        same = bool(np.all(ib == ix)) and np.array_equal(kb.view(np.uint32), kx.view(np.uint32))
+        print(f"budget tiles {bt} keys {be} chunks {nch}: walk {best:.2f} ms, overflow records {nov}, "
+              f"equal to brute {same}", flush=True)
+pl.set_option("nn_walk_budget_tiles", 2048)
+pl.set_option("nn_walk_budget_keys", 12288)
+pl.set_option("nn_walk_chunks", 32)
 for i in bad[:5]:
     print("sample", i, smp[i].x, smp[i].y, smp[i].explore, "\n  brute", ib[i], kb[i], "\n  walk ", iw[i], kw[i])
 ex = np.array([s.explore for s in smp])
