@@ -31,7 +31,7 @@
 #include "clrrt_dev.hpp"
 #include "clrrt_internal.hpp"
 
-static const int kWalkMaxOver = 512, kWalkMaxChunks = 64;  // walk overflow records, split waves per record
+static const int kWalkMaxOver = 2048, kWalkMaxChunks = 64;  // walk overflow records, split waves per record
 
 using namespace clrrt;
 
@@ -98,8 +98,9 @@ struct clrrt_ctx {
   int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
   bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
-  // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64)
-  int nnw_bud_tiles = 2048, nnw_bud_ex = 12288, nnw_chunks = 32;
+  // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64;
+  // "nn_walk_max_over" records <= 2048); defaults from the cfg3 bench sweep
+  int nnw_bud_tiles = 4096, nnw_bud_ex = 4096, nnw_chunks = 32, nnw_max_over = 1024;
   WalkBufs nnw{};                      // allocated on first use
   CompactBufs cmp{};                   // round compaction scratch
   int nng_modes = 1;
@@ -112,6 +113,9 @@ struct clrrt_ctx {
   void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
+  int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
+  int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
+  int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
   int roll_handoff = 0;       // option "roll_handoff": donor waves hand their last rollouts to absorbers
   void* roll_cont = nullptr;  // [roll_cont_cap] RollCont
   int* roll_ready = nullptr;  // [roll_cont_cap]
@@ -393,7 +397,7 @@ static void free_all(clrrt_ctx* c) {
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
                   c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
-                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->nng.scount, c->nng.sfill, c->nng.sstart,
+                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag, c->nng.scount, c->nng.sfill, c->nng.sstart,
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
@@ -500,6 +504,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(hipMalloc(&c->roll_prep, rollout_prep_bytes() * (size_t)B * CAND_K));
   chk(dalloc(&c->roll_q, 1));
   chk(dalloc(&c->roll_best, B));
+  chk(dalloc(&c->roll_perm, (int64_t)B * CAND_K));
+  chk(dalloc(&c->roll_pflag, 2 * (int64_t)B * CAND_K + (int64_t)(roll_order_scratch_bytes(B * CAND_K) / 4 + 64)));
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
@@ -1125,10 +1131,12 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) c->nnw_bud_tiles = (int)value;
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
+  else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_handoff") c->roll_handoff = value != 0;
+  else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
     HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1204,8 +1212,11 @@ static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
 // Walk-search buffers, sized for the context's capacity (first use).
 static int ensure_walk(clrrt_ctx* c) {
   c->nnw.bud_tiles = c->nnw_bud_tiles;
-  c->nnw.bud_ex = c->nnw_bud_ex;
-  c->nnw.max_over = kWalkMaxOver;
+  // the exact-key budget grows with the tree (denser trees: more near-tied keys per sample; the cfg3
+  // sweeps: 4096 best at <= 1.6 M nodes, 8192 at 4.7 M, where 4096 overflows more samples than there
+  // are records)
+  c->nnw.bud_ex = c->nnw_bud_ex > 0 ? (int)std::max<int64_t>(c->nnw_bud_ex, c->n_nodes >> 9) : 0;
+  c->nnw.max_over = c->nnw_max_over;
   c->nnw.nch = c->nnw_chunks;
   if (c->nnw.P) return CLRRT_OK;
   const int64_t M = std::max<int64_t>(c->cap.max_nodes, c->cap.max_batch);
@@ -1412,6 +1423,10 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.cont_ready = c->roll_ready;
       a.cont_ctl = c->roll_ctl;
       a.cont_epoch = ++c->roll_epoch;
+    }
+    if (c->roll_priority) {
+      a.perm = c->roll_perm;
+      a.pflag = c->roll_pflag;
     }
     if (c->roll_persistent && c->dp.n_steps_max > 0)
       HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));

@@ -90,6 +90,12 @@ struct RollArgs {
   int* cont_ready;  // per slot: == cont_epoch once the slot is written
   int* cont_ctl;
   int cont_epoch, cont_donors;
+  // persistent rollouts: queue order (nullable).  k_roll_prep flags the jobs likely to run long
+  // (pflag[q], q = k B + s), the queue serves them first (perm[position] = q); results do not depend
+  // on the order
+  int* perm;
+  int* pflag;
+  int B;
 };
 
 struct SelArgs {
@@ -222,6 +228,7 @@ hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
 // njobs * rollout_prep_bytes(), best B ints, qnext one int.
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
                                      int blocks);
+size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t rollout_prep_bytes();
 size_t rollout_cont_bytes();
 hipError_t launch_select(hipStream_t st, const SelArgs& a);

@@ -779,8 +779,11 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
                  a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
 }
 
+#ifndef CLRRT_ROLLOUT_WAVES
+#define CLRRT_ROLLOUT_WAVES 1
+#endif
 template <int SRC, bool NEED_GAP>
-__global__ void __launch_bounds__(256) k_rollout(RollArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLLOUT_WAVES))) k_rollout(RollArgs a) {
   extern __shared__ float4 lds[];
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
@@ -878,6 +881,31 @@ struct RollInit {
   int32_t valid, pad;
 };
 
+// Scheduling only: a rollout toward a sample 8-20 m away (1.7-4.2 turning radii) at 30-90 degrees off
+// the heading is the kind that ends in the iteration limit after the full horizon (the vehicle
+// circles without reaching the reference: tools/orbit_predict.py, cfg3 round 40: this class is 3% of
+// the jobs and holds 472 of the 501 jobs of >= 300 steps).  Served first, these chains no longer
+// start late and set the kernel's makespan.
+__device__ __forceinline__ int roll_likely_long(const double* st, double sx, double sy) {
+  const float dx = (float)(sx - st[0]), dy = (float)(sy - st[1]);
+  const float d2 = dx * dx + dy * dy;
+  if (!(d2 >= 64.f && d2 < 400.f)) return 0;
+  const float c = cosf((float)st[2]), s = sinf((float)st[2]);
+  const float along = dx * c + dy * s, across = fabsf(dy * c - dx * s);
+  // 30 <= angle < 90 degrees: along > 0 and across >= tan(30 deg) along
+  return (along > 0.f && across >= 0.57735f * along) ? 1 : 0;
+}
+
+// Queue order: flagged positions first (in q order), then the rest (in q order).
+__global__ void __launch_bounds__(256) k_roll_order(const int* __restrict__ pflag, const int* __restrict__ ppos,
+                                                    int n, int* __restrict__ perm) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const int nf = ppos[n - 1] + pflag[n - 1];
+  const int pos = pflag[q] ? ppos[q] : nf + (q - ppos[q]);
+  perm[pos] = q;
+}
+
 template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
   glibc::stage_tables();
@@ -889,14 +917,17 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
   }
   if (j >= a.njobs) return;
   const int id = a.cand[j];
+  int* pflag = a.pflag ? a.pflag + (j % CAND_K) * a.B + j / CAND_K : nullptr;  // queue position q = k B + s
   if (id < 0) {
     prep[j].valid = 0;
+    if (pflag) *pflag = 0;
     return;
   }
   const clrrt_node& n = a.tree[id];
   St10 ps;
 #pragma unroll
   for (int k = 0; k < 10; k++) ps.v[k] = n.state[k];
+  if (pflag) *pflag = roll_likely_long(ps.v, a.samples[j / CAND_K].x, a.samples[j / CAND_K].y);
   const RefD R = make_ref(n.ref_back[0], n.ref_back[1], a.samples[j / CAND_K].x, a.samples[j / CAND_K].y, a.p);
   RollInit ini;
   roll_init(ini.r, ps.v, R, n.ref_vback, false, a.p);
@@ -1045,10 +1076,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         if (lane == leader) base = atomicAdd(qnext, __popcll(m));
         base = __shfl(base, leader, 64);
         if (idle) {
-          const int q = base + __popcll(m & ((1ull << lane) - 1));
-          if (q >= a.njobs) {
+          const int q0 = base + __popcll(m & ((1ull << lane) - 1));
+          if (q0 >= a.njobs) {
             exhausted = true;
           } else {
+            const int q = a.perm ? a.perm[q0] : q0;
             k = q / B;
             s = q - k * B;
             j = s * CAND_K + k;
@@ -2060,6 +2092,24 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   return hipSuccess;
 }
 
+// The queue order from k_roll_prep's flags: perm = flagged positions, then the others (both ascending).
+// a.pflag's buffer holds [njobs flags][njobs exclusive-scan positions][scan scratch].
+size_t roll_order_scratch_bytes(int n) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int*)nullptr, (int*)nullptr, n);
+  return bytes;
+}
+static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
+  if (!a.perm || !a.pflag) return hipSuccess;
+  int* ppos = a.pflag + a.njobs;
+  void* tmp = (void*)(((uintptr_t)(a.pflag + 2 * (size_t)a.njobs) + 255) & ~(uintptr_t)255);  // 256 B spare
+  size_t bytes = roll_order_scratch_bytes(a.njobs);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, a.pflag, ppos, a.njobs, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_roll_order, dim3((a.njobs + 255) / 256), dim3(256), 0, st, a.pflag, ppos, a.njobs, a.perm);
+  return hipGetLastError();
+}
+
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, void* prep, int* qnext, int* best,
                                      int blocks) {
   if (a0.njobs <= 0) return hipSuccess;
@@ -2084,14 +2134,17 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   }
   RollArgs a = a0;
   a.cont_donors = nb * 3;  // waves 1..3 of each block (launch_bounds 256)
+  a.B = B;
   if (a.p.need_gap) {
     hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
+    if ((e = roll_order(st, a)) != hipSuccess) return e;
     if (a.cont) hipLaunchKernelGGL((k_roll_run<true, true>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
     else hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
+    if ((e = roll_order(st, a)) != hipSuccess) return e;
     const void* fn = a.cont ? (const void*)&k_roll_run<false, true> : (const void*)&k_roll_run<false, false>;
     if (lds > 64 * 1024) {
       hipError_t e2 = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -46,9 +46,10 @@ def _nn_strategy(pl, name):
     pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
     pl.set_option("nn_walk_stateless", name.endswith("stateless"))
     split = name.startswith("walk_split")
-    pl.set_option("nn_walk_budget_tiles", 1 if split else 2048)
-    pl.set_option("nn_walk_budget_keys", 1 if split else 12288)
+    pl.set_option("nn_walk_budget_tiles", 1 if split else 4096)
+    pl.set_option("nn_walk_budget_keys", 1 if split else 4096)
     pl.set_option("nn_walk_chunks", 7 if split else 32)
+    pl.set_option("nn_walk_max_over", 1024)
 
 
 def _pair(kind, seed=1, iters=40):
@@ -379,6 +380,7 @@ def test_walk_overflow_matches_brute(chunks):
     ib, kb = pl.sort_nodes_batch(smp)
     _nn_strategy(pl, "walk_split")
     pl.set_option("nn_walk_chunks", chunks)
+    pl.set_option("nn_walk_max_over", 512)
     pl.reset_counters()
     iw, kw = pl.sort_nodes_batch(smp)
     records = pl.debug_counters()[32]

@@ -41,8 +41,8 @@ print(f"brute {tb:.2f} ms, walk {tw:.2f} ms; lists equal: {len(bad) == 0} ({len(
       f"{np.array_equal(kb.view(np.uint32), kw.view(np.uint32))}")
 print("walk stats", {k: v for k, v in sw.items() if k.startswith("walk")})
 # overflow budget sweep (tiles, exact keys; 0 = off): time and identity with the brute force
-for bt, be in ((0, 0), (8192, 49152), (4096, 24576), (2048, 12288), (1024, 8192)):
-    for nch in ((32,) if bt in (0, 8192) else (16, 32)):
+for bt, be in ((0, 0), (4096, 24576), (4096, 8192), (4096, 4096), (4096, 2048)):
+    for nch in ((32,) if bt == 0 else (16, 32)):
         pl.set_option("nn_walk_budget_tiles", bt)
         pl.set_option("nn_walk_budget_keys", be)
         pl.set_option("nn_walk_chunks", nch)
@@ -54,8 +54,8 @@ for bt, be in ((0, 0), (8192, 49152), (4096, 24576), (2048, 12288), (1024, 8192)
         same = bool(np.all(ib == ix)) and np.array_equal(kb.view(np.uint32), kx.view(np.uint32))
         print(f"budget tiles {bt} keys {be} chunks {nch}: walk {best:.2f} ms, overflow records {nov}, "
               f"equal to brute {same}", flush=True)
-pl.set_option("nn_walk_budget_tiles", 2048)
-pl.set_option("nn_walk_budget_keys", 12288)
+pl.set_option("nn_walk_budget_tiles", 4096)
+pl.set_option("nn_walk_budget_keys", 4096)
 pl.set_option("nn_walk_chunks", 32)
 for i in bad[:5]:
     print("sample", i, smp[i].x, smp[i].y, smp[i].explore, "\n  brute", ib[i], kb[i], "\n  walk ", iw[i], kw[i])

@@ -9,7 +9,7 @@ import clrrt
 from clrrt import abi, scenes
 
 pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=4 << 20,
-                   max_rows=1 << 27, max_batch=16384)
+                   max_rows=1 << 27, max_batch=16384)  # jobs <= 10 x max_batch
 pl.set_obstacles(scenes.urban_scene(200))
 pl.tree_init()
 pl.expand(clrrt.Rng(5), n_iters=40 * 16384, budget_ms=1e9, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
@@ -22,7 +22,8 @@ longest = [jobs[i] for i in np.argsort(-nr)[:8]]
 print("longest rollouts (steps):", sorted(nr)[-8:])
 pl.enable_timing(True)
 for label, jl in (("1 lane", longest[:1]), ("8 lanes, 8 jobs", longest[:8]), ("64 copies", longest[:1] * 64),
-                  ("4096 copies", longest[:1] * 4096), ("16384 copies", longest[:1] * 16384)):
+                  ("4096 copies", longest[:1] * 4096), ("16384 copies", longest[:1] * 16384),
+                  ("65536 copies", longest[:1] * 65536), ("131072 copies", longest[:1] * 131072)):
     for rep in range(3):
         pl.reset_counters()
         r = pl.simulate_batch(jl)
