@@ -271,8 +271,8 @@ __device__ __forceinline__ float atan2_apx(float y, float x) {
 }
 
 // Lower bound on the float Dubins key (dubins_key) of a node whose rotated offset to the sample,
-// (tx, ty >= 0) as dubins_key forms it, lies within pos_err of the given one; -inf unless the sample
-// is well outside the turning circle (tangent length t >= 0.1).  There the key is the length of the
+// (tx, ty >= 0) as dubins_key forms it, lies within pos_err of the given one.  Well outside the turning
+// circle (tangent length t >= 0.1) the key is the length of the
 // turn-then-straight path, t + rho (thc - acos(rho / dc)) with acos(rho / dc) = atan2(t, rho): a
 // function of the offset with gradient norm 1 (continuous outside the circle: thc wraps only inside
 // it), so moving the offset by pos_err moves the key by at most pos_err; the margin also covers the
@@ -281,18 +281,30 @@ __device__ __forceinline__ float atan2_apx(float y, float x) {
 __device__ __forceinline__ void walk_key_range(float tx, float ty, float pos_err, float& lo, float& hi) {
   const float rho = 4.77f;
   const float t2 = tx * tx + ty * (ty - 2.f * rho);  // dc^2 - rho^2
-  if (!(t2 >= 0.01f)) {
+  if (t2 <= -0.01f) {  // surely inside the circle: dubins_key's inside branch, >= rho pi = 14.98
+    lo = 14.9f;
+    hi = __builtin_inff();
+    return;
+  }
+  if (!(t2 > -0.01f)) {  // NaN
     lo = -__builtin_inff();
     hi = __builtin_inff();
     return;
   }
-  const float t = fsqrt(t2);
+  const float t = fsqrt(fmaxf(t2, 0.f));
   float th = atan2_apx(tx, rho - ty);
   if (th < 0.f) th += 6.28318531f;
   const float L = t + rho * (th - atan2_apx(t, rho));
   const float m = 2.f * pos_err + 2e-4f + 2e-5f * L;
-  lo = L - m;
-  hi = L + m;
+  if (t2 >= 0.01f) {  // surely outside (the reference's float inside test errs by ~1e-5)
+    lo = L - m;
+    hi = L + m;
+  } else {
+    // near the circle: the outside key (near t = 0 it depends on t only through t^3 / (3 rho^2), so the
+    // cancellation in t costs nothing) or, if the reference's point falls inside, the inside key
+    lo = fminf(L - m - 1e-4f, 14.9f);
+    hi = __builtin_inff();
+  }
 }
 
 // Lower bound on the keys of a tile's nodes for the sample at (rsx, rsy) (frame coordinates);

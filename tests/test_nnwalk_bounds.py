@@ -90,13 +90,16 @@ def walk_key_range(tx, ty, pos_err):
     tx, ty = tx.astype(F), ty.astype(F)
     rho = RHO
     t2 = tx * tx + ty * (ty - F(2) * rho)
-    ok = t2 >= F(0.01)
-    t = np.sqrt(np.where(ok, t2, F(1)))
+    out = t2 >= F(0.01)
+    near = (t2 > F(-0.01)) & ~out
+    t = np.sqrt(np.maximum(t2, F(0)))
     th = atan2_apx(tx, rho - ty)
     th = np.where(th < 0, th + F(6.28318531), th)
     L = t + rho * (th - atan2_apx(t, rho))
     m = F(2) * pos_err + F(2e-4) + F(2e-5) * L
-    return (np.where(ok, L - m, -np.inf).astype(np.float64), np.where(ok, L + m, np.inf).astype(np.float64))
+    lo = np.where(out, L - m, np.where(near, np.minimum(L - m - F(1e-4), F(14.9)), F(14.9)))
+    hi = np.where(out, L + m, np.inf)
+    return lo.astype(np.float64), hi.astype(np.float64)
 
 
 def test_atan2_approximation():
@@ -124,8 +127,33 @@ def test_stage1_key_bound():
         jy = np.abs(ty + r * np.sin(ang)).astype(F)
         pe = F(pos) + F(1e-6) * (np.abs(jx) + jy)
         lb, ub = walk_key_range(jx, jy, pe)
-        ok = np.isfinite(key) & np.isfinite(lb)
+        ok = np.isfinite(key)
         assert (key[ok] - lb[ok]).min() >= 0, (scale, (key[ok] - lb[ok]).min())
-        assert (ub[ok] - key[ok]).min() >= 0, (scale, (ub[ok] - key[ok]).min())
-        tight.append(np.median(key[ok] - lb[ok]))
+        okh = ok & np.isfinite(ub)
+        assert (ub[okh] - key[okh]).min() >= 0, (scale, (ub[okh] - key[okh]).min())
+        tight.append(np.median(key[okh] - lb[okh]))
     assert max(tight) < 0.02, tight  # and it is tight: the stage-1 filter rejects what the key would
+
+
+def test_stage1_bound_near_turning_circle():
+    """Offsets within 0.3 of the turning circle (both sides), jittered: the near-circle branch (the
+    outside key or rho pi) and the inside branch stay below the float key."""
+    rng = np.random.default_rng(13)
+    rho = float(RHO)
+    for band in (0.02, 0.1, 0.3):
+        n = 1_000_000
+        r = rho + rng.uniform(-band, band, n)
+        a = rng.uniform(0, 2 * np.pi, n)
+        tx = (r * np.cos(a)).astype(F)
+        ty = np.abs(rho + r * np.sin(a)).astype(F)
+        key = dubins_key_f32(tx, ty)
+        pos = 8e-5
+        ang = rng.uniform(0, 2 * np.pi, n)
+        rr = pos * np.sqrt(rng.uniform(0, 1, n))
+        jx = (tx + rr * np.cos(ang)).astype(F)
+        jy = np.abs(ty + rr * np.sin(ang)).astype(F)
+        lb, ub = walk_key_range(jx, jy, F(pos) + F(1e-6) * (np.abs(jx) + jy))
+        ok = np.isfinite(key)
+        assert (key[ok] - lb[ok]).min() >= 0, (band, (key[ok] - lb[ok]).min())
+        okh = ok & np.isfinite(ub)
+        assert (ub[okh] - key[okh]).min() >= 0, band

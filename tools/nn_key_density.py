@@ -28,31 +28,45 @@ ce = nd["costE"].astype(np.float32)
 feas_len = 2.1 * pl.params.ref_res  # DevParams.feas_len (clrrt_capi.hip)
 print(f"nodes {N}, distinct positions {len(np.unique(np.stack([x, y], 1), axis=0))}", flush=True)
 smp = list(clrrt.Rng(77).draw_samples(pl.params, 16384))
-ids_gpu, keys_gpu = pl.sort_nodes_batch(smp, exact=False)
+# argv[2:]: extra samples "x,y,explore" (e.g. the costly ones nn_scaling.py reports), analysed first
+extra = []
+for a in sys.argv[2:]:
+    x_, y_, e_ = a.split(",")
+    q = clrrt.abi.Sample() if hasattr(clrrt.abi, "Sample") else type(smp[0])()
+    q.x, q.y, q.explore = float(x_), float(y_), int(e_)
+    extra.append(q)
+smp = extra + smp
 deltas = (0.0, 1e-4, 1e-3, 1e-2, 0.1, 1.0)
+
+
+def analyse(j):
+    sx, sy, ex = smp[j].x, smp[j].y, smp[j].explore
+    qx = (sx - x).astype(np.float32)
+    qy = (sy - y).astype(np.float32)
+    tx = c * qx - s * qy
+    ty = np.abs(s * qx + c * qy)
+    key = dubins_key_f32(tx, ty).astype(np.float32)
+    if not ex:
+        key = (ce + key).astype(np.float32)
+    ang = np.arctan2(sy - by, sx - bx)
+    d = np.mod(ang - ap + np.pi, 2 * np.pi) - np.pi
+    feas = (np.abs(d) <= np.pi / 4) & (np.hypot(bx - sx, by - sy) >= feas_len)
+    kf = key[feas].astype(np.float64)
+    order = np.lexsort((np.nonzero(feas)[0], kf))
+    k11 = kf[order[10]] if len(order) > 10 else np.inf
+    cnt = [int(np.sum(kf <= k11 + dd)) for dd in deltas]
+    near = feas & (key <= k11 + 1e-3)
+    dist = len(np.unique(np.stack([x[near], y[near], th[near]], 1), axis=0))
+    distc = len(np.unique(np.stack([x[near], y[near], th[near], ce[near].astype(np.float64)], 1), axis=0))
+    rad = np.hypot(x[near], y[near])
+    print(f"{'explore' if ex else 'optimize'} sample ({sx:.2f}, {sy:.2f}): k11 {k11:.4f}; feasible nodes with key "
+          f"<= k11 + {deltas}: {cnt}; distinct (x, y, th) within 1e-3: {dist}, with costE {distc}; their |p| "
+          f"p50 {np.median(rad) if len(rad) else -1:.2f}", flush=True)
+    return cnt + [dist]
+
+
+for j in range(len(extra)):
+    analyse(j)
 for lab, pick in (("explore", 1), ("optimize", 0)):
-    rows = []
-    for j in [k for k, q in enumerate(smp) if q.explore == pick][:12]:
-        sx, sy = smp[j].x, smp[j].y
-        qx = (sx - x).astype(np.float32)
-        qy = (sy - y).astype(np.float32)
-        tx = c * qx - s * qy
-        ty = np.abs(s * qx + c * qy)
-        key = dubins_key_f32(tx, ty).astype(np.float32)
-        if not pick:
-            key = (ce + key).astype(np.float32)
-        ang = np.arctan2(sy - by, sx - bx)
-        d = np.mod(ang - ap + np.pi, 2 * np.pi) - np.pi
-        feas = (np.abs(d) <= np.pi / 4) & (np.hypot(bx - sx, by - sy) >= feas_len)
-        kf = key[feas].astype(np.float64)
-        order = np.lexsort((np.nonzero(feas)[0], kf))
-        k11 = kf[order[10]] if len(order) > 10 else np.inf
-        cnt = [int(np.sum(kf <= k11 + dd)) for dd in deltas]
-        near = feas & (key <= k11 + 1e-3)
-        dist = len(np.unique(np.stack([x[near], y[near], th[near]], 1), axis=0))
-        gk = keys_gpu[j][min(9, int(np.sum(ids_gpu[j] >= 0)) - 1)] if np.any(ids_gpu[j] >= 0) else np.nan
-        rows.append(cnt + [dist])
-        print(f"{lab} sample ({sx:.2f}, {sy:.2f}): k11 {k11:.4f} (gpu k10 {gk:.4f}); feasible nodes with key <= "
-              f"k11 + {deltas}: {cnt}; distinct inputs within 1e-3: {dist}", flush=True)
-    r = np.array(rows)
-    print(f"{lab} median counts {np.median(r, 0).tolist()}", flush=True)
+    rows = [analyse(j) for j in [k for k in range(len(extra), len(smp)) if smp[k].explore == pick][:8]]
+    print(f"{lab} median counts {np.median(np.array(rows), 0).tolist()}", flush=True)
