@@ -100,8 +100,14 @@ struct clrrt_ctx {
   bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
   // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64;
   // "nn_walk_max_over" records <= 2048); defaults from the cfg3 bench sweep
-  int nnw_bud_tiles = 4096, nnw_bud_ex = 4096, nnw_chunks = 32, nnw_max_over = 1024;
+  int nnw_bud_tiles = 2048, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
+  int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
+  // pipelined rounds: a second index set, so the next round's index is built while the side stream's
+  // search still reads this one (swapped in after each commit); nnw_built: the tree size and frame the
+  // current set's index was built for (n = -1: none)
+  WalkBufs nnw_alt{};
+  struct { int64_t n = -1; double ox, oy, x0, y0, x1, y1; float delta; } nnw_built;
   CompactBufs cmp{};                   // round compaction scratch
   int nng_modes = 1;
   int nng_budget = 0;
@@ -401,7 +407,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
-                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->cmp.packed, c->cmp.scanned,
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.TRIG, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->cmp.packed, c->cmp.scanned,
                   c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1132,6 +1138,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
+  else if (k == "nn_walk_double") c->nnw_double = value != 0;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
@@ -1209,7 +1216,34 @@ static int ensure_sort_scratch(clrrt_ctx* c, int64_t entries) {
   return CLRRT_OK;
 }
 
-// Walk-search buffers, sized for the context's capacity (first use).
+// One walk-search buffer set, sized for the context's capacity.
+static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
+  if (w.P) return CLRRT_OK;
+  const int64_t M = std::max<int64_t>(c->cap.max_nodes, c->cap.max_batch);
+  const int64_t Mp = c->cap.max_nodes + 1024;
+  HIPC(c, dalloc(&w.sorder, c->cap.max_batch));
+  HIPC(c, dalloc(&w.keys, 2 * M));
+  HIPC(c, dalloc(&w.keys2, 2 * M));
+  HIPC(c, dalloc(&w.vals, std::max<int64_t>(M, Mp)));  // also the run markers of the padded records
+  HIPC(c, dalloc(&w.vals2, M));
+  w.tmp_bytes = walk_sort_bytes((int)M);
+  HIPC(c, hipMalloc(&w.tmp, std::max<size_t>(w.tmp_bytes, 256)));
+  HIPC(c, dalloc(&w.Q, Mp));
+  HIPC(c, dalloc(&w.CE, Mp));
+  HIPC(c, dalloc(&w.ID, Mp));
+  HIPC(c, dalloc(&w.HEAD, Mp));
+  HIPC(c, dalloc(&w.TRIG, Mp));
+  HIPC(c, dalloc(&w.tiles, Mp / 64 + 1));
+  HIPC(c, dalloc(&w.supers, Mp / 1024 + 1));
+  HIPC(c, dalloc(&w.ovf_n, 1));
+  HIPC(c, dalloc(&w.ovf, kWalkMaxOver));
+  HIPC(c, dalloc(&w.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
+  HIPC(c, dalloc(&w.pi, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
+  HIPC(c, dalloc(&w.P, Mp));  // last: marks the set complete
+  return CLRRT_OK;
+}
+
+// Walk-search configuration of the current set (+ its buffers on first use).
 static int ensure_walk(clrrt_ctx* c) {
   c->nnw.bud_tiles = c->nnw_bud_tiles;
   // the exact-key budget grows with the tree (denser trees: more near-tied keys per sample; the cfg3
@@ -1218,29 +1252,7 @@ static int ensure_walk(clrrt_ctx* c) {
   c->nnw.bud_ex = c->nnw_bud_ex > 0 ? (int)std::max<int64_t>(c->nnw_bud_ex, c->n_nodes >> 9) : 0;
   c->nnw.max_over = c->nnw_max_over;
   c->nnw.nch = c->nnw_chunks;
-  if (c->nnw.P) return CLRRT_OK;
-  const int64_t M = std::max<int64_t>(c->cap.max_nodes, c->cap.max_batch);
-  const int64_t Mp = c->cap.max_nodes + 1024;
-  HIPC(c, dalloc(&c->nnw.sorder, c->cap.max_batch));
-  HIPC(c, dalloc(&c->nnw.keys, 2 * M));
-  HIPC(c, dalloc(&c->nnw.keys2, 2 * M));
-  HIPC(c, dalloc(&c->nnw.vals, std::max<int64_t>(M, Mp)));  // also the run markers of the padded records
-  HIPC(c, dalloc(&c->nnw.vals2, M));
-  c->nnw.tmp_bytes = walk_sort_bytes((int)M);
-  HIPC(c, hipMalloc(&c->nnw.tmp, std::max<size_t>(c->nnw.tmp_bytes, 256)));
-  HIPC(c, dalloc(&c->nnw.Q, Mp));
-  HIPC(c, dalloc(&c->nnw.CE, Mp));
-  HIPC(c, dalloc(&c->nnw.ID, Mp));
-  HIPC(c, dalloc(&c->nnw.HEAD, Mp));
-  HIPC(c, dalloc(&c->nnw.TRIG, Mp));
-  HIPC(c, dalloc(&c->nnw.tiles, Mp / 64 + 1));
-  HIPC(c, dalloc(&c->nnw.supers, Mp / 1024 + 1));
-  HIPC(c, dalloc(&c->nnw.ovf_n, 1));
-  HIPC(c, dalloc(&c->nnw.ovf, kWalkMaxOver));
-  HIPC(c, dalloc(&c->nnw.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
-  HIPC(c, dalloc(&c->nnw.pi, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
-  HIPC(c, dalloc(&c->nnw.P, Mp));  // last: marks the set complete
-  return CLRRT_OK;
+  return alloc_walk(c, c->nnw);
 }
 
 // Search region (the sampling region and the tree's box) and the float frame of the searches.
@@ -1287,18 +1299,40 @@ static void pf_reset(clrrt_ctx* c) {
   if (c->pf_state != 0 && c->side) hipStreamSynchronize(c->side);
   c->pf_state = 0;
   c->pf_next.clear();
+  c->nnw_built.n = -1;
 }
 
 // Launches the walk search of samples h2[0..n2) (host, pinned) over the current tree on the side
 // stream into the *2 buffers; eval_samples records ev_tree before its rollouts.
 // The index is built on the main stream before the rollouts (its radix sort's look-back passes starve
 // beside the rollout kernel on large trees: 3+ ms instead of 0.2), the search runs on the side stream.
+static bool walk_built_for(const clrrt_ctx* c, const NnSetup& su) {
+  const auto& b = c->nnw_built;
+  return b.n == c->n_nodes && b.ox == su.fr.ox && b.oy == su.fr.oy && b.delta == su.fr.delta && b.x0 == su.x0 &&
+         b.y0 == su.y0 && b.x1 == su.x1 && b.y1 == su.y1;
+}
 static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
   KTimer kt(c, 0);
   const int rw = ensure_walk(c);
   if (rw != CLRRT_OK) return rw;
+  if (walk_built_for(c, su)) return CLRRT_OK;  // built ahead (next_round_build)
   HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw));
+  auto& b = c->nnw_built;
+  b.n = c->n_nodes;
+  b.ox = su.fr.ox; b.oy = su.fr.oy; b.delta = su.fr.delta;
+  b.x0 = su.x0; b.y0 = su.y0; b.x1 = su.x1; b.y1 = su.y1;
   return CLRRT_OK;
+}
+
+// Pipelined rounds, right after a commit: the next round's index over the committed tree goes into
+// the other buffer set on the main stream while the side stream's search still reads this one (it
+// waits for nothing but the commit; the wait for the side search comes after it).
+static int next_round_build(clrrt_ctx* c) {
+  const NnSetup su = nn_setup(c);
+  if (!walk_serves(c, su)) return CLRRT_OK;
+  std::swap(c->nnw, c->nnw_alt);
+  c->nnw_built.n = -1;
+  return pre_roll_build(c, su);
 }
 
 static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
@@ -1355,6 +1389,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   if (!use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && region_ok) {
     int rc = ensure_walk(c);
     if (rc != CLRRT_OK) return rc;
+    c->nnw_built.n = -1;
     HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, fr, x0, y0, x1, y1, c->nnw, c->cand,
                            c->ckey, c->ncand, c->ctie, c->work_ctr + 18, c->nnw_stateless));
     if (scratch) HIPC(c, launch_nn_exact_only(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->ctie, scratch,
@@ -1673,6 +1708,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     have_next = false;
     if (nb2 > 0) {
+      if (c->nnw_double && (rc = next_round_build(c)) != CLRRT_OK) break;
       if ((rc = merge_side_lists(c, nb2, first_new, nn)) != CLRRT_OK) break;
       have_next = true;
     }

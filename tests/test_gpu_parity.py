@@ -46,9 +46,9 @@ def _nn_strategy(pl, name):
     pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
     pl.set_option("nn_walk_stateless", name.endswith("stateless"))
     split = name.startswith("walk_split")
-    pl.set_option("nn_walk_budget_tiles", 1 if split else 4096)
+    pl.set_option("nn_walk_budget_tiles", 1 if split else 2048)
     pl.set_option("nn_walk_budget_keys", 1 if split else 4096)
-    pl.set_option("nn_walk_chunks", 7 if split else 32)
+    pl.set_option("nn_walk_chunks", 7 if split else 16)
     pl.set_option("nn_walk_max_over", 1024)
 
 
