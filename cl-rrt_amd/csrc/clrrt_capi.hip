@@ -148,7 +148,7 @@ struct clrrt_ctx {
   // then merges in the nodes it appended (launch_nn_delta) and the buffers swap
   int nn_pipeline = 1;  // option "nn_pipeline"
   hipStream_t side = nullptr;
-  hipEvent_t ev_tree = nullptr, ev_walk = nullptr;
+  hipEvent_t ev_tree = nullptr, ev_walk = nullptr, ev_commit = nullptr;
   clrrt_sample* d_samples2 = nullptr;
   clrrt_sample* h_samples2 = nullptr;
   int* cand2 = nullptr;
@@ -416,6 +416,7 @@ static void free_all(clrrt_ctx* c) {
   if (c->side) hipStreamSynchronize(c->side);
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
+  if (c->ev_commit) hipEventDestroy(c->ev_commit);
   if (c->side) hipStreamDestroy(c->side);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
@@ -473,6 +474,7 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
   chk(hipEventCreateWithFlags(&c->ev_tree, hipEventDisableTiming));
   chk(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&c->ev_commit, hipEventDisableTiming));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->res_gb, B * CAND_K));
@@ -1350,18 +1352,28 @@ static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
   return CLRRT_OK;
 }
 
-// After the appended nodes [first_new, first_new + nn) are in the tree: merge them into the side
-// walk's lists and swap the *2 buffers in.
-static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
-  if (nn > 0) {
-    KTimer kt(c, 0);
+// After the appended nodes [first_new, first_new + nn) are in the tree (queued on the main stream):
+// their search for the next round's samples, merged into the side walk's lists, runs on the side
+// stream behind the walk, so the main stream can build the next round's index meanwhile.
+static int side_delta_launch(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
+  if (nn <= 0) return CLRRT_OK;
+  HIPC(c, hipEventRecord(c->ev_commit, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->side, c->ev_commit, 0));
+  {
+    KTimer kt(c, 0, c->side);
     c->nn_bf_keys += (int64_t)n2 * nn;
     const NnSetup su2 = nn_setup(c);  // the box includes the appended nodes
     const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n2 * NN_K));
-    HIPC(c, launch_nn_delta(c->stream, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
+    HIPC(c, launch_nn_delta(c->side, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
                             max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed));
   }
+  HIPC(c, hipEventRecord(c->ev_walk, c->side));
+  return CLRRT_OK;
+}
+
+// The main stream waits for the side stream's lists and swaps the *2 buffers in.
+static int side_lists_join(clrrt_ctx* c) {
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
   std::swap(c->d_samples, c->d_samples2);
   std::swap(c->h_samples, c->h_samples2);
   std::swap(c->cand, c->cand2);
@@ -1369,6 +1381,11 @@ static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
   std::swap(c->ncand, c->ncand2);
   std::swap(c->ctie, c->ctie2);
   return CLRRT_OK;
+}
+
+static int merge_side_lists(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
+  const int rc = side_delta_launch(c, n2, first_new, nn);
+  return rc != CLRRT_OK ? rc : side_lists_join(c);
 }
 
 // Stage 1: candidate lists of samples c->d_samples[0..n) (spatial index for large trees).
@@ -1708,8 +1725,9 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     have_next = false;
     if (nb2 > 0) {
+      if ((rc = side_delta_launch(c, nb2, first_new, nn)) != CLRRT_OK) break;
       if (c->nnw_double && (rc = next_round_build(c)) != CLRRT_OK) break;
-      if ((rc = merge_side_lists(c, nb2, first_new, nn)) != CLRRT_OK) break;
+      if ((rc = side_lists_join(c)) != CLRRT_OK) break;
       have_next = true;
     }
     for (int j = 0; j < L; j++) {
