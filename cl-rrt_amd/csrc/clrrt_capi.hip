@@ -114,7 +114,7 @@ struct clrrt_ctx {
   // persistent rollouts (k_roll_prep + k_roll_run)
   int roll_persistent = 1;
   int nn_debug = 0;
-  int roll_blocks = 0;       // persistent blocks (0: 2 per CU)
+  int roll_blocks = 0;       // persistent blocks (0: 5/8 of the CUs)
   int n_cu = 256;
   void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
   int* roll_q = nullptr;      // [1] queue head
@@ -1469,7 +1469,13 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     a.slots = c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
-    const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu) : c->roll_handoff ? c->n_cu : 2 * c->n_cu;
+    // persistent blocks (1 resident per CU: the step loop fills the register file): 5/8 of the CUs, so
+    // the side stream's search of the next round has 3/8 from the start (cfg3 sweep of 128..512 blocks:
+    // 160 best, 0.914 -> 0.949 M nodes/s; the rollout kernel's makespan is its longest chains, not its
+    // width)
+    const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu)
+                       : c->roll_handoff  ? c->n_cu
+                                          : std::max(1, (5 * c->n_cu) / 8);
     if (c->roll_persistent && c->roll_handoff) {
       a.cont = c->roll_cont;
       a.cont_ready = c->roll_ready;
