@@ -496,6 +496,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   constexpr bool prof = false;
 #endif
   uint64_t cyc[4] = {0, 0, 0, 0};   // super bounds, visit_super (incl.), visit4 (incl.), drain
+#ifdef CLRRT_WALK_PROFILE
+  unsigned long long hist[6] = {0, 0, 0, 0, 0, 0};  // exact keys: gap to the 11th key <= 0, 1e-3, 1e-2, 0.1, more; kth inf
+#endif
   int hc = -1;       // run head whose key is known ...
   float kc = 0.f;    // ... and that key
   unsigned long long n_sup = 0, n_tile = 0, n_q = 0, n_ex = 0, n_und = 0, n_sure = 0, n_drop = 0;
@@ -584,6 +587,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         hc = uni(__shfl(hd, l, 64));
       }
     }
+#ifdef CLRRT_WALK_PROFILE
+    if (prof) {  // diagnostics: exact keys by their distance above the 11th key at the drain
+      const float gap = key - kth;
+      const bool v = lane < nq;
+      hist[0] += __popcll(__ballot(v && !(gap > 0.f)));
+      hist[1] += __popcll(__ballot(v && gap > 0.f && gap <= 1e-3f));
+      hist[2] += __popcll(__ballot(v && gap > 1e-3f && gap <= 1e-2f));
+      hist[3] += __popcll(__ballot(v && gap > 1e-2f && gap <= 0.1f));
+      hist[4] += __popcll(__ballot(v && gap > 0.1f));
+      hist[5] += __popcll(__ballot(v && kth == __builtin_inff()));
+    }
+#endif
     uint64_t m = __ballot(c);
     while (m) {
       const int l = __ffsll((unsigned long long)m) - 1;
@@ -810,6 +825,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         atomicAdd(&stats[6], (unsigned long long)cyc[2]);
         atomicAdd(&stats[7], (unsigned long long)cyc[3]);
         atomicAdd(&stats[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0));
+#ifdef CLRRT_WALK_PROFILE
+        atomicAdd(&stats[13], hist[0]);  // work_ctr[31]
+        for (int q = 1; q < 6; q++) atomicAdd(&stats[14 + q], hist[q]);  // work_ctr[33..37]
+#endif
       }
     }
   };

@@ -69,3 +69,9 @@ for lab, m in (("explore", ex == 1), ("optimize", ex == 0)):
     s = pl.nn_stats()
     print(f"walk {lab} only ({len(sub)}): {(time.perf_counter() - t0) * 1e3:.2f} ms "
           f"{ {k: round(v / len(sub), 1) for k, v in s.items() if k.startswith('walk')} } per sample")
+    dc = pl.debug_counters()
+    h = [dc[31], dc[33], dc[34], dc[35], dc[36], dc[37]]
+    if sum(h[:5]):  # diagnostics build (CLRRT_WALK_PROFILE): exact keys by their gap above the 11th key
+        print(f"   exact keys per sample by key - kth at the drain: <=0 {h[0] / len(sub):.1f}, <=1e-3 "
+              f"{h[1] / len(sub):.1f}, <=1e-2 {h[2] / len(sub):.1f}, <=0.1 {h[3] / len(sub):.1f}, >0.1 "
+              f"{h[4] / len(sub):.1f} (list not full: {h[5] / len(sub):.1f})")
