@@ -50,7 +50,15 @@ namespace clrrt {
 #define NN_K (CAND_K + 1)
 #define WALK_TILE 32
 #define WALK_SUPER 32  // tiles per super-tile
+#ifndef WALK_APBINS
 #define WALK_APBINS 8  // ang_par sectors (top key bits)
+#endif
+#ifndef WALK_THBINS
+#define WALK_THBINS 1  // heading sectors within an ang_par sector (1: none)
+#endif
+#ifndef WALK_SECTOR_BITS
+#define WALK_SECTOR_BITS 3
+#endif
 
 #define LAUNCH_CHECK3()                          \
   do {                                           \
@@ -86,7 +94,17 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   const float a = (float)nodes[i].ang_par;
   int bin = (int)floorf((a + 3.14159265f) * (WALK_APBINS / 6.2831853f));
   bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
+#if WALK_THBINS > 1
+  // then the heading octant: tiles of similar headings sharpen the turning bound
+  const float th = atan2f(-nodes[i].s, nodes[i].c);  // (c, s) = (cos, sin)(-heading)
+  int tb = (int)floorf((th + 3.14159265f) * (WALK_THBINS / 6.2831853f));
+  tb = tb < 0 ? 0 : (tb >= WALK_THBINS ? WALK_THBINS - 1 : tb);
+  bin = bin * WALK_THBINS + tb;
+  keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | ((uint64_t)k << (32 - WALK_SECTOR_BITS)) |
+            (__float_as_uint(nodes[i].costE) >> (WALK_SECTOR_BITS + 0));
+#else
   keys[i] = ((uint64_t)bin << 61) | ((uint64_t)k << 29) | (__float_as_uint(nodes[i].costE) >> 3);
+#endif
   vals[i] = i;
 }
 
