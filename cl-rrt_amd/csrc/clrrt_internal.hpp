@@ -96,6 +96,10 @@ struct RollArgs {
   int* perm;
   int* pflag;
   int B;
+  // k_roll_run's per-lane reference-point cache in LDS (launch_rollout_persistent sizes it)
+  int pcache_enable;  // option "roll_point_cache"
+  int pcache_n;       // points per lane (0: off)
+  int pcache_off;     // byte offset in the dynamic LDS
 };
 
 struct SelArgs {

@@ -573,11 +573,12 @@ struct PhaseClk {
 // 7..9 and returns CLRRT_ROLL_* or -1 to continue.
 template <bool NEED_GAP>
 __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
-                                         double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr) {
+                                         double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr,
+                                         PtCache pts = {nullptr, 0}) {
   double Px, Py;
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
   w.scan += (uint32_t)(r.R.N - r.wp);
-  double dla = update_waypoint(r, p, Px, Py, false);
+  double dla = update_waypoint(r, p, Px, Py, false, pts);
 #ifdef CLRRT_DUP_WP
   {
     double z = 0.0;
@@ -588,7 +589,7 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   }
 #endif
   if (pc) pc->mark(1);
-  double ym = lateral_error(r, Px, Py);
+  double ym = lateral_error(r, Px, Py, pts);
 #ifdef CLRRT_DUP_LAT
   {
     double z = 0.0;
@@ -970,12 +971,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int lane = threadIdx.x & 63;
+  // this lane's reference-point cache: after the obstacle tables, a.pcache_n points x 256 lanes
+  double2* const pts_base = (double2*)((char*)lds + a.pcache_off) + threadIdx.x;
+  int pts_n = 0;  // points of the current rollout's reference in the cache
+  auto pts = [&]() -> PtCache { return PtCache{pts_base, pts_n}; };
   const int64_t slot = (int64_t)a.slot_rows * 10;
   const int64_t pass_stride = slot * a.slot_jobs;
   WorkCtr w{0, 0, 0};
   Roll r;
   double c7 = 0, c8 = 0, c9 = 0;
   int j = -1, k = 0, s = 0, pass = 0, steps = 0;
+  auto refill_pts = [&]() { pts_n = a.pcache_n > 0 ? fill_points(r.R, pts_base, a.pcache_n) : 0; };
   bool exhausted = false;
   PhaseClk pclk{};
 #ifdef CLRRT_ROLL_PROFILE
@@ -1021,6 +1027,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           // goal-biased rollout from the node this rollout would append (expandTree :163-173)
           const RefD R = make_goal_ref(out.bx, out.by, a.p);
           roll_init(r, out.st, R, out.vback, true, a.p);
+          refill_pts();
           c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
           pass = 1;
           steps = 0;
@@ -1090,6 +1097,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               j = -1;
             } else {
               r = prep[j].r;
+              refill_pts();
               c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
               pass = 0;
               steps = 0;
@@ -1136,6 +1144,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
             } else {
               const RollCont& cc = cont[q];
               r = cc.r;
+              refill_pts();
               c7 = cc.c7; c8 = cc.c8; c9 = cc.c9;
               j = cc.j; k = cc.k; s = cc.s; pass = cc.pass; steps = cc.steps;
               fin = -1;
@@ -1173,7 +1182,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
     const int best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
     if (pc) pc->mark(6);
-    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
+    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc, pts());
 #ifdef CLRRT_ROLL_PROFILE
     {
       unsigned it = r.scan_it, mx_ = it;
@@ -2117,39 +2126,43 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
   RollInit* pr = (RollInit*)prep;
-  const size_t lds = roll_lds_bytes(a0);
+  RollArgs a = a0;
+  a.B = B;
+  // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then the reference-point cache:
+  // whatever the tables leave of the 160 KB a workgroup may use (the glibc tables take ~10 KB of static
+  // LDS), up to 32 points x 256 lanes
+  const size_t obs_lds = a.p.need_gap ? 0 : (roll_lds_bytes(a0) + 15) / 16 * 16;
+  {
+    const size_t budget = 160 * 1024 - 12 * 1024;
+    const int n = obs_lds < budget ? (int)std::min<size_t>(32, (budget - obs_lds) / (256 * sizeof(double2))) : 0;
+    a.pcache_n = a.pcache_enable && n >= 4 ? n : 0;
+    a.pcache_off = (int)obs_lds;
+  }
+  const size_t lds = obs_lds + (size_t)a.pcache_n * 256 * sizeof(double2);
+  const void* fn = a.p.need_gap ? (a.cont ? (const void*)&k_roll_run<true, true> : (const void*)&k_roll_run<true, false>)
+                                : (a.cont ? (const void*)&k_roll_run<false, true> : (const void*)&k_roll_run<false, false>);
+  if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+    return e;
   int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
-  if (a0.cont) {
+  if (a.cont) {
     // hand-off absorbers wait for every donor wave of the grid: the grid must be resident at once
-    const void* fn = a0.p.need_gap ? (const void*)&k_roll_run<true, true> : (const void*)&k_roll_run<false, true>;
     int occ = 0, dev = 0, ncu = 0;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-    if (!a0.p.need_gap && lds > 64 * 1024 &&
-        (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
-      return e;
-    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, a0.p.need_gap ? 0 : lds)) != hipSuccess)
-      return e;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, lds)) != hipSuccess) return e;
     nb = std::max(1, std::min(nb, std::max(1, occ) * ncu));
   }
-  RollArgs a = a0;
   a.cont_donors = nb * 3;  // waves 1..3 of each block (launch_bounds 256)
-  a.B = B;
   if (a.p.need_gap) {
     hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    if (a.cont) hipLaunchKernelGGL((k_roll_run<true, true>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
-    else hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), 0, st, a, pr, qnext, best, B);
+    if (a.cont) hipLaunchKernelGGL((k_roll_run<true, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    else hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    const void* fn = a.cont ? (const void*)&k_roll_run<false, true> : (const void*)&k_roll_run<false, false>;
-    if (lds > 64 * 1024) {
-      hipError_t e2 = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e2 != hipSuccess) return e2;
-    }
     if (a.cont) hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
     else hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   }
