@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="samples per round per GPU (default: config)")
     ap.add_argument("--horizon-ms", type=float, default=0.0, help="per-query budget (default: config)")
-    ap.add_argument("--max-nodes", type=int, default=6 << 20)
+    ap.add_argument("--max-nodes", type=int, default=0,
+                    help="tree capacity per rank (0: max(6 Mi, 2 Mi x N) -- the replicated tree grows N x faster)")
     ap.add_argument("--rows-per-node", type=int, default=64)
     ap.add_argument("--cpu-queries", type=int, default=5, help="oracle queries timed for cpu_baseline")
     ap.add_argument("--no-cpu", action="store_true")
@@ -242,7 +243,9 @@ def main():
     obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
     params = clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
     GOAL_WORLD = (40.0, 0.0, 0.0, 0.0)
-    max_nodes = args.max_nodes
+    # the tree is replicated and grows N x faster with N ranks: size it so a 2 s query runs its whole
+    # horizon instead of stopping at capacity (rows: 80 B x rows_per_node per node, 82 GB at 16 Mi nodes)
+    max_nodes = args.max_nodes if args.max_nodes > 0 else max(6 << 20, (2 << 20) * world)
     max_rows = max_nodes * args.rows_per_node
     pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
                        max_obstacles=max(1, len(obs)))

@@ -1628,7 +1628,11 @@ int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t l
   HIPC(c, hipStreamSynchronize(c->stream));
   if (n > 0) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   if (c->pf_state == 1) {  // the next round's search ran beside this round's rollouts
-    if ((rc = merge_side_lists(c, (int)c->pf_samples.size(), first_new, n)) != CLRRT_OK) return rc;
+    // as in clrrt_expand: the appended nodes' search behind it on the side stream, the next round's
+    // index into the other buffer set meanwhile
+    if ((rc = side_delta_launch(c, (int)c->pf_samples.size(), first_new, n)) != CLRRT_OK) return rc;
+    if (c->nnw_double && (rc = next_round_build(c)) != CLRRT_OK) return rc;
+    if ((rc = side_lists_join(c)) != CLRRT_OK) return rc;
     c->pf_state = 2;
   }
   return CLRRT_OK;
