@@ -609,7 +609,8 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
 #endif
   double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
   double dc = satd(-p.dmax, p.dmax, cmd);
-  double E = prof_v(r.P, r.wp + 2) - r.x4;
+  const double vref = prof_v(r.P, r.wp + 2);  // ref.v[IDwp + 2]: the PI error and the logged column 8
+  double E = vref - r.x4;
   r.iE = r.iE + E * p.dt;
   double ac = satd(p.amin, p.amax, p.Kp * E + p.Ki * r.iE);
   // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
@@ -631,7 +632,7 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
 #endif
   if (pc) pc->mark(3);
   col7 = (double)r.wp;
-  col8 = prof_v(r.P, r.wp + 2);
+  col8 = vref;
   col9 = dc;
   // collision (simulation.cpp:83-86)
   double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);

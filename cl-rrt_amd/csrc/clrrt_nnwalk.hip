@@ -800,7 +800,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       float sl = __builtin_inff();
       if ((lane & 31) == 0 && st >= 0) sl = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
       const float slb = __shfl(sl, lane & 32, 64);
+#ifdef WALK_CHEAP_STATELESS
+      // the distance-only bound first; the full one only for tiles it does not place beyond min(T, kth)
+      // (the weaker value still bounds the super-tile's rest)
+      if (st >= 0 && tl < ntiles) {
+        const WalkTile tt = tiles[tl];
+        lb = fmaxf(walk_lb_dist(tt, rsx, rsy, ex, dsR), slb);
+        if (!(lb > fminf(T, kth))) lb = fmaxf(walk_lb(tt, rsx, rsy, ex, flen_t, dsR), slb);
+      }
+#else
       if (st >= 0 && tl < ntiles) lb = fmaxf(walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR), slb);  // both bound
+#endif
       const bool take = st >= 0 && (first || lb > Tp) && lb <= T && !(lb > kth);
       tm = __ballot(take);
       const float rest = hmin(st >= 0 && lb > T ? lb : __builtin_inff());
