@@ -660,11 +660,13 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   if (ay + p.ay_road_max > 3) return CLRRT_ROLL_ACCLIMIT;
   // end / goal (simulation.cpp:110-133)
   double ex = r.x0 - p.g0, ey = r.x1 - p.g1;
-  double dg = sqrt(ex * ex + ey * ey);
   double Ve = (r.x4 - r.vback);
   if (r.endr && (Ve < 0.1)) return CLRRT_ROLL_END;
-  // the heading error (an fmod) only matters within 1 m of the goal; both are side-effect free
-  if ((dg <= 1) && (fabs(angle_diff(r.x2, p.g2)) < 0.05)) return CLRRT_ROLL_GOAL;
+  // dg = sqrt(ex^2 + ey^2) <= 1 needs ex^2 + ey^2 <= 1 + 2^-52 (sqrt is correctly rounded and monotonic),
+  // so the square root is taken only near the goal; the heading error (an fmod) only matters within
+  // 1 m of the goal; all of these are side-effect free
+  const double dg2 = ex * ex + ey * ey;
+  if (dg2 <= 1.0000000000000004 && sqrt(dg2) <= 1 && (fabs(angle_diff(r.x2, p.g2)) < 0.05)) return CLRRT_ROLL_GOAL;
   return -1;
 }
 
