@@ -299,9 +299,29 @@ __device__ __forceinline__ float atan2_apx(float y, float x) {
 __device__ __forceinline__ void walk_key_range(float tx, float ty, float pos_err, float& lo, float& hi) {
   const float rho = 4.77f;
   const float t2 = tx * tx + ty * (ty - 2.f * rho);  // dc^2 - rho^2
-  if (t2 <= -0.01f) {  // surely inside the circle: dubins_key's inside branch, >= rho pi = 14.98
+  if (t2 <= -0.01f) {
+    // surely inside the circle: dubins_key's inside branch, rho (alpha + asin(qx / df) - asin(rho sin(alpha)
+    // / df)) with alpha = 2 pi - acos((5 rho^2 - df^2) / (4 rho^2)) (>= rho pi = 14.98 anywhere), restated
+    // with atan2: asin(qx / df) = atan2(qx, qy + rho), sin(alpha) = -sqrt(1 - c^2).  Its gradient grows
+    // like 1 / sqrt(1 - c^2) and df / sqrt(df^2 - (rho sin alpha)^2): the margin carries those factors,
+    // and near their poles the plain rho pi bound stays (tests/test_nnwalk_bounds.py, jittered offsets)
     lo = 14.9f;
     hi = __builtin_inff();
+#ifdef WALK_INSIDE_BRACKET  // off: it cuts exact keys 3x but costs more in the visits (cfg3 0.94 -> 0.89 M nodes/s)
+    const float df2 = tx * tx + (ty + rho) * (ty + rho);
+    const float cA = fminf(fmaxf((5.f * rho * rho - df2) * (1.f / (4.f * rho * rho)), -1.f), 1.f);
+    const float sA = fsqrt(fmaxf((1.f - cA) * (1.f + cA), 0.f));
+    const float u = rho * sA;
+    const float w = fsqrt(fmaxf(df2 - u * u, 0.f));
+    const float cw = w * frcp(fsqrt(df2));
+    if (sA >= 0.05f && cw >= 0.05f) {
+      const float alpha = 6.28318531f - atan2_apx(sA, cA);
+      const float L = rho * (alpha + atan2_apx(tx, ty + rho) + atan2_apx(u, w));
+      const float m = 2e-3f + 1e-4f * L + pos_err * (8.f + 8.f * frcp(sA) + 8.f * frcp(cw));
+      lo = fmaxf(L - m, 14.9f);
+      hi = L + m;
+    }
+#endif
     return;
   }
   if (!(t2 > -0.01f)) {  // NaN
