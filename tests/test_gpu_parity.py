@@ -319,14 +319,22 @@ def test_pipelined_batch_rounds_identical():
     """Full-size property: BATCH rounds with the next round's walk search overlapped with the current
     round's rollouts (+ the merge of the appended nodes, launch_nn_delta), and rounds whose last
     rollouts move between waves (roll_handoff), grow exactly the tree of plain rounds (every node
-    record and trajectory row)."""
+    record and trajectory row).  So do the scheduling and search options: the rollout queue order
+    (roll_priority), the persistent grid width (roll_blocks), the reference-point cache
+    (roll_point_cache), the single-buffered walk index (nn_walk_double) and the walk without overflow
+    split (budget 0) or with every sample split (budget 1)."""
     mode, obs = _scene("obb200")
     trees = []
-    for pipe, handoff in ((0, 0), (1, 0), (1, 1)):
+    variants = [dict(nn_pipeline=0, roll_handoff=0), dict(nn_pipeline=1, roll_handoff=0),
+                dict(nn_pipeline=1, roll_handoff=1), dict(roll_priority=0, roll_blocks=512),
+                dict(roll_point_cache=1, nn_walk_double=0),
+                dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
+                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
+    for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
-        pl.set_option("nn_pipeline", pipe)
-        pl.set_option("roll_handoff", handoff)
+        for k, v in opts.items():
+            pl.set_option(k, v)
         pl.set_obstacles(obs)
         pl.tree_init()
         st = pl.expand(clrrt.Rng(12), n_iters=16384 * 6, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
