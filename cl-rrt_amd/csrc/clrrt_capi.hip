@@ -408,7 +408,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
-                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.TRIG, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->cmp.packed, c->cmp.scanned,
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.TRIG, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
                   c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1243,6 +1243,9 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.ovf, kWalkMaxOver));
   HIPC(c, dalloc(&w.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
   HIPC(c, dalloc(&w.pi, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
+  HIPC(c, dalloc(&w.skeys, Mp));
+  HIPC(c, dalloc(&w.sids, Mp));
+  w.sorted_n = -1;
   HIPC(c, dalloc(&w.P, Mp));  // last: marks the set complete
   return CLRRT_OK;
 }
@@ -1304,6 +1307,8 @@ static void pf_reset(clrrt_ctx* c) {
   c->pf_state = 0;
   c->pf_next.clear();
   c->nnw_built.n = -1;
+  c->nnw.sorted_n = -1;  // the kept sort results describe the old tree
+  c->nnw_alt.sorted_n = -1;
 }
 
 // Launches the walk search of samples h2[0..n2) (host, pinned) over the current tree on the side
@@ -1320,7 +1325,8 @@ static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
   const int rw = ensure_walk(c);
   if (rw != CLRRT_OK) return rw;
   if (walk_built_for(c, su)) return CLRRT_OK;  // built ahead (next_round_build)
-  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw));
+  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw,
+                               c->nnw_alt.P ? &c->nnw_alt : nullptr));
   auto& b = c->nnw_built;
   b.n = c->n_nodes;
   b.ox = su.fr.ox; b.oy = su.fr.oy; b.delta = su.fr.delta;

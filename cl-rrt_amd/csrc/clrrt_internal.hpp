@@ -193,6 +193,12 @@ struct WalkBufs {
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists
   int* pi;
+  // the index's sort result, kept for the next build: skeys/sids = the sorted (key, node) pairs of nodes
+  // [0, sorted_n) in the frame (sorted_x0, sorted_y0, sorted_scale); sorted_n = -1: none
+  uint64_t* skeys;
+  int* sids;
+  int64_t sorted_n;
+  double sorted_x0, sorted_y0, sorted_scale;
 };
 size_t walk_sort_bytes(int n);
 // Candidate lists of samples S[0 .. B) (same output as the brute force: cand, ckey, ncand, ctie);
@@ -202,7 +208,7 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
                           float* ckey, int* ncand, int* ctie, unsigned long long* stats, bool stateless);
 // launch_nn_walk's two halves: the index of nodes [0, N), then the search of samples over it
 hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const NnFrame& fr, double x0, double y0,
-                                double x1, double y1, WalkBufs& w);
+                                double x1, double y1, WalkBufs& w, const WalkBufs* prev = nullptr);
 hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                  const DevParams& p, const NnFrame& fr, double x0, double y0, double x1, double y1,
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,

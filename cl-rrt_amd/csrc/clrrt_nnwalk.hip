@@ -39,6 +39,8 @@
 #include <climits>
 #include <hip/hip_fp16.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_merge.hpp>
+#include <algorithm>
 #include <stdint.h>
 
 #include "clrrt_dev.hpp"
@@ -79,9 +81,12 @@ __device__ __forceinline__ uint32_t w_spread(uint32_t v) {
 // (non-finite positions last within the sector), then the costE bits (top 29), so records with equal
 // key inputs (e.g. the root's zero-length children of one sector) end up next to each other.
 __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
-                            uint64_t* __restrict__ keys, int* __restrict__ vals) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+                            uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0) {
+  const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k0 >= N - first) return;
+  const int i = first + k0;
+  keys += -first;  // entries are written at [k0] (keys[i] below)
+  vals += -first;
   const double x = nodes[i].x, y = nodes[i].y;
   uint32_t k = 0xffffffffu;
   if (isfinite(x) && isfinite(y)) {
@@ -1002,7 +1007,10 @@ size_t walk_sort_bytes(int n) {
                                      (const int*)nullptr, (int*)nullptr, n, 0, 64);
   size_t b2 = 0;
   hipcub::DeviceScan::InclusiveScan(nullptr, b2, (const int*)nullptr, (int*)nullptr, hipcub::Max(), n + 1024);
-  return bytes > b2 ? bytes : b2;
+  size_t b3 = 0;
+  rocprim::merge(nullptr, b3, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                 (const int*)nullptr, (const int*)nullptr, (int*)nullptr, (size_t)n, (size_t)n);
+  return std::max(bytes, std::max(b2, b3));
 }
 
 // Inclusive max-scan of the run markers in three plain passes (tile scans, one-block scan of the tile
@@ -1082,21 +1090,55 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
 }
 
 // The place-ordered index of nodes [0, N) (Morton sort, gathered records, run heads, tile bounds).
+// prev: another buffer set whose sort result covers nodes [0, prev->sorted_n) in the same frame (the
+// previous round's index): only the appended nodes are keyed and sorted, then merged with it (nodes
+// never change once appended; ties take the older, lower-id entries first, so the order equals a full
+// stable sort's).
 hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const NnFrame& fr, double x0, double y0,
-                                double x1, double y1, WalkBufs& w) {
+                                double x1, double y1, WalkBufs& w, const WalkBufs* prev) {
   if (N <= 0) return hipSuccess;
   const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   const double span = fmax(x1 - x0, y1 - y0);
   const double scale = span > 0 ? 65535.0 / span : 1.0;
-  hipLaunchKernelGGL(k_walk_keys, dim3((N + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale, (uint64_t*)w.keys,
-                     w.vals);
-  LAUNCH_CHECK3();
-  size_t bytes = w.tmp_bytes;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, (uint64_t*)w.keys2, w.vals,
-                                                    w.vals2, N, 0, 64, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 255) / 256), dim3(256), 0, st, nodes, N, Npad, w.vals2, fr.ox, fr.oy,
+  hipError_t e;
+  const bool incremental = prev && prev != &w && prev->sorted_n > 0 && prev->sorted_n <= N &&
+                           prev->sorted_x0 == x0 && prev->sorted_y0 == y0 && prev->sorted_scale == scale;
+  if (incremental) {
+    const int n0 = (int)prev->sorted_n, nn = N - n0;
+    if (nn > 0) {
+      hipLaunchKernelGGL(k_walk_keys, dim3((nn + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale,
+                         (uint64_t*)w.keys, w.vals, n0);
+      LAUNCH_CHECK3();
+      size_t bytes = w.tmp_bytes;
+      e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, (uint64_t*)w.keys2, w.vals,
+                                             w.vals2, nn, 0, 64, st);
+      if (e != hipSuccess) return e;
+      bytes = w.tmp_bytes;
+      e = rocprim::merge(w.tmp, bytes, (const uint64_t*)prev->skeys, (const uint64_t*)w.keys2, w.skeys,
+                         (const int*)prev->sids, (const int*)w.vals2, w.sids, (size_t)n0, (size_t)nn,
+                         rocprim::less<uint64_t>(), st);
+      if (e != hipSuccess) return e;
+    } else {
+      if ((e = hipMemcpyAsync(w.skeys, prev->skeys, sizeof(uint64_t) * N, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+        return e;
+      if ((e = hipMemcpyAsync(w.sids, prev->sids, sizeof(int) * N, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+        return e;
+    }
+  } else {
+    hipLaunchKernelGGL(k_walk_keys, dim3((N + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale,
+                       (uint64_t*)w.keys, w.vals, 0);
+    LAUNCH_CHECK3();
+    size_t bytes = w.tmp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, w.skeys, w.vals, w.sids, N, 0, 64,
+                                           st);
+    if (e != hipSuccess) return e;
+  }
+  w.sorted_n = N;
+  w.sorted_x0 = x0;
+  w.sorted_y0 = y0;
+  w.sorted_scale = scale;
+  hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 255) / 256), dim3(256), 0, st, nodes, N, Npad, w.sids, fr.ox, fr.oy,
                      w.P, w.Q, w.CE, w.ID, w.vals, w.TRIG);
   LAUNCH_CHECK3();
   // HEAD[j] = first record of j's run of equal key inputs (inclusive max-scan of dup markers)
