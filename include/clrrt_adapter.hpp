@@ -21,6 +21,7 @@
  * by the same three draws per iteration, keeping both streams equal.
  */
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -222,6 +223,188 @@ class Engine {
 
   clrrt_ctx* ctx_ = nullptr;
   int64_t synced_ = 0;
+};
+
+/* ---------------------------------------------------------------------------------------------
+ * MotionPlanner::planMotion (motionplanner.cpp:8-77) without ROS.  The reference's callback reads
+ * its state (updateState :89-94), detections (updateObstacles :81-86) and request
+ * (car_msgs::MotionRequest) from topics/services and publishes the MPC message and rviz markers;
+ * here they are plain arguments and return values, and the whole query runs on the device:
+ *
+ *   transformStateToLocal(worldState)            transformations.cpp:143-147 (x, y, heading -> 0)
+ *   updateReferenceResolution(carPose[4]), vmax  :16-17 (clrrt_params.ref_res / vmax)
+ *   transformNodesWorldToCar(bestNodes, world)   :22  clrrt_path_transform(WORLD_TO_CAR)
+ *   bestNodes.clear() unless commit_path         :28-30
+ *   initializeTree(RRT, veh, bestNodes, carPose) :32  clrrt_tree_init_from_path
+ *   Timer(200) loop of expandTree                :39-43 clrrt_expand (budget_ms, or n_iters for tests)
+ *   bestNodes = extractBestPath(RRT.tree)        :51  clrrt_extract_best_path + clrrt_path_commit
+ *   transformNodesCarToworld(bestNodes, world)   :54  clrrt_path_transform(CAR_TO_WORLD)
+ *   generateMPCmessage + filterMPCmessage        :66-70 clrrt_path_mpc_message(filtered = 1)
+ *   publish when msg.x.size() >= 3               :71-74 (MPCTrajectory::published)
+ *
+ * draw_tree (rrtplanner.cpp:322-341, rrt_node.cpp draw flag): the reference builds one rviz marker
+ * per node (trajectory + goal flag) inside extractBestPath when the flag is set.  The engine keeps the
+ * tree on the device, so the markers' data (every node's rows) is downloaded only when draw_tree is
+ * on and a marker sink is passed; with the flag off nothing leaves the device (the default, and what
+ * the benchmark runs). */
+struct MotionRequest {          /* car_msgs::MotionRequest fields planMotion reads */
+  double goal[4] = {0, 0, 0, 0};  /* x, y, heading, velocity (the planner's car frame, used as given) */
+  double vmax = 5.0;
+  std::vector<double> laneShifts, Cxy;
+  bool bend = false;
+};
+
+struct MPCTrajectory {          /* car_msgs::Trajectory after filterMPCmessage (no delta: not copied) */
+  std::vector<double> x, y, theta, v, a, a_cmd, d_cmd;
+  bool published = false;       /* msg.x.size() >= 3 (motionplanner.cpp:71) */
+};
+
+struct TreeMarker {             /* createStateMsg(nodeid, tree[nodeid].tra, goalReached) input */
+  int32_t id;
+  bool goal;
+  std::vector<double> rows;     /* nrows x 10 */
+};
+
+struct PlanReport {
+  int32_t reinit_outcome = -1;  /* CLRRT_REINIT_* of initializeTree */
+  int64_t iterations = 0;       /* expandTree iterations of the Timer loop */
+  int64_t tree_size = 0;
+  std::vector<int32_t> path;    /* bestNodes as tree ids, root -> goal */
+  float best_cost = 0;
+  int64_t counters[4] = {0, 0, 0, 0};  /* sim_count, fail_collision, fail_acclimit, fail_iterlimit (:9, :45) */
+};
+
+class MotionPlanner {
+ public:
+  struct Config {
+    clrrt_params base;          /* vehicle, gains, weights, collision mode (goal/vmax/ref_res set per query) */
+    clrrt_capacity cap;
+    bool commit_path = true;    /* motionplanner/commit_path */
+    int32_t mode = CLRRT_MODE_BATCH;
+    int32_t batch = 4096;
+    double budget_ms = 200;     /* Timer(200) */
+    int64_t n_iters = 0;        /* > 0: a fixed iteration count instead of the budget (reproducible runs) */
+    bool draw_tree = false;
+  };
+
+  MotionPlanner(const Config& c, uint32_t seed, int device = 0) : cfg_(c) {
+    check(nullptr, clrrt_create(&cfg_.base, &cfg_.cap, device, &ctx_), "clrrt_create");
+    clrrt_rng_seed(&rng_, seed);
+  }
+  ~MotionPlanner() { clrrt_destroy(ctx_); }
+  MotionPlanner(const MotionPlanner&) = delete;
+  MotionPlanner& operator=(const MotionPlanner&) = delete;
+
+  clrrt_ctx* ctx() { return ctx_; }
+  clrrt_rng& rng() { return rng_; }
+
+  /* updateState (motionplanner.cpp:89-94): state = [x, y, theta, delta, v, a] in the world frame */
+  void updateState(const std::vector<double>& s) {
+    if (s.size() != 6) throw Error("updateState: the state has 6 entries (motionplanner.cpp:93)");
+    state_ = s;
+  }
+  /* updateObstacles (motionplanner.cpp:81-86): the detections as the obstacle service returns them */
+  void updateObstacles(const std::vector<clrrt_obstacle>& det) { det_ = det; }
+  template <class ObsVec>
+  void updateObstaclesFrom(const ObsVec& det) {
+    det_.clear();
+    for (const auto& d : det) det_.push_back(obstacle_to_c(d));
+  }
+
+  /* One query.  Returns false when no path was found ("No solution found", :56-58): the committed path
+   * is then empty and the next query restarts from the car state. */
+  bool planMotion(const MotionRequest& req, MPCTrajectory* msg = nullptr, PlanReport* rep = nullptr,
+                  std::vector<TreeMarker>* markers = nullptr) {
+    if (state_.size() != 6) throw Error("planMotion before updateState");
+    check(ctx_, clrrt_reset_counters(ctx_), "clrrt_reset_counters");  // :9
+    const double world[3] = {state_[0], state_[1], state_[2]};
+    const double car[6] = {0.0, 0.0, 0.0, state_[3], state_[4], state_[5]};  // transformStateToLocal
+    clrrt_params p = cfg_.base;
+    p.ref_res = std::max(std::abs(car[4]) * p.ref_int, p.ref_mindist);  // updateReferenceResolution (:16)
+    p.vmax = req.vmax;                                                  // :17
+    for (int i = 0; i < 4; i++) p.goal[i] = req.goal[i];                // MyRRT RRT(req.goal, ...) (:23)
+    p.bend = req.bend ? 1 : 0;
+    p.lane_shift0 = req.laneShifts.empty() ? 0.0 : req.laneShifts[0];
+    for (int i = 0; i < 3; i++) p.Cxy[i] = i < (int)req.Cxy.size() ? req.Cxy[i] : 0.0;
+    check(ctx_, clrrt_set_params(ctx_, &p), "clrrt_set_params");
+    check(ctx_, clrrt_set_obstacles(ctx_, det_.data(), (int32_t)det_.size()), "clrrt_set_obstacles");  // RRT.det
+    check(ctx_, clrrt_path_transform(ctx_, CLRRT_WORLD_TO_CAR, world), "clrrt_path_transform");          // :22
+    if (!cfg_.commit_path) check(ctx_, clrrt_path_commit(ctx_, nullptr, 0, nullptr), "clrrt_path_commit");  // :28-30
+    int32_t oc = -1;
+    check(ctx_, clrrt_tree_init_from_path(ctx_, car, &oc), "clrrt_tree_init_from_path");                   // :32
+    clrrt_stats st;
+    check(ctx_, clrrt_expand(ctx_, &rng_, cfg_.n_iters, cfg_.n_iters > 0 ? 0.0 : cfg_.budget_ms, cfg_.mode,
+                             cfg_.batch, &st), "clrrt_expand");                                            // :39-43
+    int64_t n_nodes = 0, n_rows = 0;
+    check(ctx_, clrrt_tree_size(ctx_, &n_nodes, &n_rows), "clrrt_tree_size");
+    if (cfg_.draw_tree && markers) draw_tree(n_nodes, *markers);  // extractBestPath's MarkerArray (:322-341)
+    // bestNodes = extractBestPath(RRT.tree) (:51)
+    int32_t n_path = 0;
+    float best = 0;
+    std::vector<int32_t> ids(256);
+    check(ctx_, clrrt_extract_best_path(ctx_, ids.data(), (int32_t)ids.size(), &n_path, &best, nullptr),
+          "clrrt_extract_best_path");
+    if (n_path > (int32_t)ids.size()) {
+      ids.resize(n_path);
+      check(ctx_, clrrt_extract_best_path(ctx_, ids.data(), n_path, &n_path, &best, nullptr), "clrrt_extract_best_path");
+    }
+    ids.resize(n_path);
+    int32_t n_remote = 0;
+    check(ctx_, clrrt_path_commit(ctx_, ids.data(), n_path, &n_remote), "clrrt_path_commit");
+    check(ctx_, clrrt_path_transform(ctx_, CLRRT_CAR_TO_WORLD, world), "clrrt_path_transform");  // :54
+    if (rep) {
+      rep->reinit_outcome = oc;
+      rep->iterations = st.iterations;
+      rep->tree_size = n_nodes;
+      rep->path = ids;
+      rep->best_cost = best;
+      clrrt_counters c;
+      check(ctx_, clrrt_get_counters(ctx_, &c), "clrrt_get_counters");
+      rep->counters[0] = c.sim_count; rep->counters[1] = c.fail_collision;
+      rep->counters[2] = c.fail_acclimit; rep->counters[3] = c.fail_iterlimit;
+    }
+    if (n_path == 0) return false;  // :56-58
+    if (msg) {
+      int32_t np = 0;
+      check(ctx_, clrrt_path_mpc_message(ctx_, 1, nullptr, 0, &np), "clrrt_path_mpc_message");
+      std::vector<double> pts(8 * (size_t)np);
+      check(ctx_, clrrt_path_mpc_message(ctx_, 1, pts.data(), np, &np), "clrrt_path_mpc_message");
+      *msg = MPCTrajectory{};
+      for (int32_t i = 0; i < np; i++) {
+        const double* q = &pts[8 * (size_t)i];  // x, y, theta, delta (NaN), v, a, a_cmd, d_cmd
+        msg->x.push_back(q[0]); msg->y.push_back(q[1]); msg->theta.push_back(q[2]);
+        msg->v.push_back(q[4]); msg->a.push_back(q[5]); msg->a_cmd.push_back(q[6]); msg->d_cmd.push_back(q[7]);
+      }
+      msg->published = msg->x.size() >= 3;  // :71
+    }
+    return true;
+  }
+
+  /* resetPlanner (motionplanner.cpp:98-100) clears MotionPlanner::motionplan, a ROS-side store the
+   * engine does not hold; the committed path (bestNodes) is cleared by clearPath(). */
+  void clearPath() { check(ctx_, clrrt_path_commit(ctx_, nullptr, 0, nullptr), "clrrt_path_commit"); }
+
+ private:
+  void draw_tree(int64_t n_nodes, std::vector<TreeMarker>& out) {
+    std::vector<clrrt_node> h((size_t)n_nodes);
+    if (n_nodes) check(ctx_, clrrt_tree_download(ctx_, 0, n_nodes, h.data()), "clrrt_tree_download");
+    out.clear();
+    out.reserve(h.size());
+    for (int64_t i = 0; i < n_nodes; i++) {
+      TreeMarker m;
+      m.id = (int32_t)i;
+      m.goal = h[i].goal != 0;
+      m.rows.resize(10 * (size_t)h[i].nrows);
+      if (h[i].nrows) check(ctx_, clrrt_tree_rows(ctx_, h[i].row_offset, h[i].nrows, m.rows.data()), "clrrt_tree_rows");
+      out.push_back(std::move(m));
+    }
+  }
+
+  Config cfg_;
+  clrrt_ctx* ctx_ = nullptr;
+  clrrt_rng rng_;
+  std::vector<double> state_;
+  std::vector<clrrt_obstacle> det_;
 };
 
 }  // namespace clrrt_adapter
