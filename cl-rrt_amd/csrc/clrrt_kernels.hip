@@ -14,6 +14,7 @@
 //   k_append                  : RRT.addNode for a batch of records (rrtplanner.h:111-113)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "clrrt_dev.hpp"
@@ -1280,14 +1281,23 @@ __global__ void k_select(SelArgs a) {
   const int nc = a.ncand[s];
   SampleOut o = {};
   o.k = -1;
-  for (int k = 0; k < nc; k++) {
-    const RollRes& r = a.res[s * CAND_K + k];
+  // (outcome, nrows) of every candidate loaded up front: independent loads, one memory latency instead
+  // of one per candidate tried
+  static_assert(offsetof(RollRes, nrows) == offsetof(RollRes, outcome) + 4 && offsetof(RollRes, outcome) % 8 == 0,
+                "outcome and nrows load as one int2");
+  int2 on[CAND_K];
+#pragma unroll
+  for (int k = 0; k < CAND_K; k++)
+    on[k] = k < nc ? *(const int2*)&a.res[s * CAND_K + k].outcome : make_int2(-1, 1);
+#pragma unroll
+  for (int k = 0; k < CAND_K; k++) {
+    if (k >= nc || o.k >= 0) break;
     o.rollouts++;
-    o.steps += r.nrows - 1;
-    o.f_col += r.outcome == CLRRT_ROLL_COLLISION;
-    o.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
-    o.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
-    if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL) { o.k = k; break; }
+    o.steps += on[k].y - 1;
+    o.f_col += on[k].x == CLRRT_ROLL_COLLISION;
+    o.f_acc += on[k].x == CLRRT_ROLL_ACCLIMIT;
+    o.f_it += on[k].x == CLRRT_ROLL_ITERLIMIT;
+    if (on[k].x == CLRRT_ROLL_END || on[k].x == CLRRT_ROLL_GOAL) o.k = k;
   }
   // EXACT-mode conflict threshold: the key a new node must beat (<=) to be tried before the result.
   o.thr = o.k >= 0 ? a.ckey[s * CAND_K + o.k] : (nc == a.p.sort_limit ? a.ckey[s * CAND_K + nc - 1] : __builtin_inff());
