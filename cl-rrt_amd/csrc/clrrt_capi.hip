@@ -1477,13 +1477,17 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     a.slots = c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
-    // persistent blocks (1 resident per CU: the step loop fills the register file): 5/8 of the CUs, so
-    // the side stream's search of the next round has 3/8 from the start (cfg3 sweep of 128..512 blocks:
-    // 160 best, 0.914 -> 0.949 M nodes/s; the rollout kernel's makespan is its longest chains, not its
-    // width)
+    // persistent blocks (1 resident per CU: the step loop fills the register file).  The rollout kernel's
+    // makespan is its longest chains, not its width, while the side stream's search of the next round
+    // grows with the tree and takes the CUs the rollouts leave; so the grid narrows as the tree grows:
+    // 7/8 of the CUs below 300 k nodes, 5/8 to 700 k, 1/2 to 1.1 M, 3/8 beyond (cfg3 round time by tree
+    // size and width, tools/blocks_vs_size.py: each step the best or within 2% of it; a fixed 5/8 grid
+    // was the best single width).  Scheduling only: results do not depend on the width.
+    const int64_t nt = c->n_nodes;
+    const int eighths = nt < 300000 ? 7 : nt < 700000 ? 5 : nt < 1100000 ? 4 : 3;
     const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu)
                        : c->roll_handoff  ? c->n_cu
-                                          : std::max(1, (5 * c->n_cu) / 8);
+                                          : std::max(1, (eighths * c->n_cu) / 8);
     if (c->roll_persistent && c->roll_handoff) {
       a.cont = c->roll_cont;
       a.cont_ready = c->roll_ready;
