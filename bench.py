@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path (e.g. several ranks sharing one GPU)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="clrrt_set_option before the run (A/B of scheduling options; results do not change)")
     return ap.parse_args()
 
 
@@ -249,6 +251,9 @@ def main():
     max_rows = max_nodes * args.rows_per_node
     pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
                        max_obstacles=max(1, len(obs)))
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        pl.set_option(k, int(v))
     pl.set_obstacles(obs)
     pl.set_rank(rank)
     stream = torch.cuda.current_stream()

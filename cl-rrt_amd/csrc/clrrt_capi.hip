@@ -148,8 +148,19 @@ struct clrrt_ctx {
   // of the next round's samples over the same tree runs on `side` into the *2 buffers; the round
   // then merges in the nodes it appended (launch_nn_delta) and the buffers swap
   int nn_pipeline = 1;  // option "nn_pipeline"
+  // option "nn_delta_grid": appended-node search through a uniform grid instead of the chunked brute force
+  // (off: identical lists, but one lane per sample walks its cells' records with dependent loads, and on
+  // cfg3 the round time nearly doubles: 0.515 vs 0.955 M nodes/s)
+  int nn_delta_grid = 0;
+  DeltaGrid dg{};
   hipStream_t side = nullptr;
   hipEvent_t ev_tree = nullptr, ev_walk = nullptr, ev_commit = nullptr;
+  // option "nn_side_build": the next round's walk index is built on the side stream behind the
+  // appended-node search (only the side stream's next walk reads it), so the main stream goes on to the
+  // next round's rollouts; ev_built marks its end for any main-stream use of the index
+  int nn_side_build = 0;  // off: no measurable change on cfg3 (0.952 vs 0.958 M nodes/s)
+  hipEvent_t ev_built = nullptr;
+  bool nnw_side_pending = false;
   clrrt_sample* d_samples2 = nullptr;
   clrrt_sample* h_samples2 = nullptr;
   int* cand2 = nullptr;
@@ -409,7 +420,8 @@ static void free_all(clrrt_ctx* c) {
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
                   c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.TRIG, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
-                  c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
+                  c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2,
+                  c->dg.cnt, c->dg.fill, c->dg.cmin, c->dg.box, c->dg.gmin, c->dg.frame, c->dg.idx};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -418,6 +430,7 @@ static void free_all(clrrt_ctx* c) {
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
   if (c->ev_commit) hipEventDestroy(c->ev_commit);
+  if (c->ev_built) hipEventDestroy(c->ev_built);
   if (c->side) hipStreamDestroy(c->side);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
@@ -463,6 +476,16 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   c->partial_cap = std::max<int64_t>(B * 16, 4096) * NN_K;
   chk(dalloc(&c->pk, c->partial_cap));
   chk(dalloc(&c->pi, c->partial_cap));
+  // appended-node grid: a round appends <= 2 records per sample; the multi-rank commit appends every
+  // rank's (up to 8 ranks here, more fall back to the chunked search)
+  chk(dalloc(&c->dg.cnt, DG_NC + 2));
+  chk(dalloc(&c->dg.fill, DG_NC + 1));
+  chk(dalloc(&c->dg.cmin, DG_NC + 1));
+  chk(dalloc(&c->dg.box, 4 * (DG_NC + 1)));
+  chk(dalloc(&c->dg.gmin, 1));
+  chk(dalloc(&c->dg.frame, 1));
+  c->dg.cap = (int)std::min<int64_t>(16 * B, 1 << 30);
+  chk(dalloc(&c->dg.idx, c->dg.cap));
   chk(dalloc(&c->cand, B * CAND_K));
   chk(dalloc(&c->ckey, B * CAND_K));
   chk(dalloc(&c->ncand, B));
@@ -476,6 +499,7 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(hipEventCreateWithFlags(&c->ev_tree, hipEventDisableTiming));
   chk(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
   chk(hipEventCreateWithFlags(&c->ev_commit, hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->res_gb, B * CAND_K));
@@ -1145,6 +1169,8 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
+  else if (k == "nn_delta_grid") c->nn_delta_grid = value != 0;
+  else if (k == "nn_side_build") c->nn_side_build = value != 0;
   else if (k == "roll_handoff") c->roll_handoff = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_point_cache") c->roll_point_cache = value != 0;
@@ -1320,12 +1346,23 @@ static bool walk_built_for(const clrrt_ctx* c, const NnSetup& su) {
   return b.n == c->n_nodes && b.ox == su.fr.ox && b.oy == su.fr.oy && b.delta == su.fr.delta && b.x0 == su.x0 &&
          b.y0 == su.y0 && b.x1 == su.x1 && b.y1 == su.y1;
 }
-static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
-  KTimer kt(c, 0);
+// The main stream is about to use (or rebuild) the walk index: wait for a side-stream build of it.
+static int side_build_wait(clrrt_ctx* c) {
+  if (!c->nnw_side_pending) return CLRRT_OK;
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_built, 0));
+  c->nnw_side_pending = false;
+  return CLRRT_OK;
+}
+static int pre_roll_build(clrrt_ctx* c, const NnSetup& su, hipStream_t st = nullptr) {
+  KTimer kt(c, 0, st ? st : c->stream);
   const int rw = ensure_walk(c);
   if (rw != CLRRT_OK) return rw;
   if (walk_built_for(c, su)) return CLRRT_OK;  // built ahead (next_round_build)
-  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw,
+  if (!st) {
+    const int r2 = side_build_wait(c);
+    if (r2 != CLRRT_OK) return r2;
+  }
+  HIPC(c, launch_nn_walk_build(st ? st : c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw,
                                c->nnw_alt.P ? &c->nnw_alt : nullptr));
   auto& b = c->nnw_built;
   b.n = c->n_nodes;
@@ -1337,12 +1374,23 @@ static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
 // Pipelined rounds, right after a commit: the next round's index over the committed tree goes into
 // the other buffer set on the main stream while the side stream's search still reads this one (it
 // waits for nothing but the commit; the wait for the side search comes after it).
+// With nn_side_build, the build goes on the side stream behind the appended-node search (the side
+// stream's walk of the round after next is its only reader; it already waited for the commit); the
+// main stream then waits for the search alone.
 static int next_round_build(clrrt_ctx* c) {
   const NnSetup su = nn_setup(c);
   if (!walk_serves(c, su)) return CLRRT_OK;
+  int rc = side_build_wait(c);
+  if (rc != CLRRT_OK) return rc;
   std::swap(c->nnw, c->nnw_alt);
   c->nnw_built.n = -1;
-  return pre_roll_build(c, su);
+  if (!c->nn_side_build) return pre_roll_build(c, su);
+  HIPC(c, hipStreamWaitEvent(c->side, c->ev_commit, 0));
+  rc = pre_roll_build(c, su, c->side);
+  if (rc != CLRRT_OK) return rc;
+  HIPC(c, hipEventRecord(c->ev_built, c->side));
+  c->nnw_side_pending = true;
+  return CLRRT_OK;
 }
 
 static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
@@ -1373,7 +1421,8 @@ static int side_delta_launch(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
     const NnSetup su2 = nn_setup(c);  // the box includes the appended nodes
     const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n2 * NN_K));
     HIPC(c, launch_nn_delta(c->side, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
-                            max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed));
+                            max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed,
+                            c->nn_delta_grid ? &c->dg : nullptr));
   }
   HIPC(c, hipEventRecord(c->ev_walk, c->side));
   return CLRRT_OK;
@@ -1414,6 +1463,7 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   if (!use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && region_ok) {
     int rc = ensure_walk(c);
     if (rc != CLRRT_OK) return rc;
+    if ((rc = side_build_wait(c)) != CLRRT_OK) return rc;
     c->nnw_built.n = -1;
     HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, fr, x0, y0, x1, y1, c->nnw, c->cand,
                            c->ckey, c->ncand, c->ctie, c->work_ctr + 18, c->nnw_stateless));

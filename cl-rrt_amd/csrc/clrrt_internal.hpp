@@ -155,6 +155,21 @@ hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, c
 
 // Frame of the brute-force search's float prune: positions relative to (ox, oy) in float are within
 // delta of the exact differences for every node and sample of the round.
+// Uniform grid over a round's appended records for the pipelined rounds' appended-node search
+// (k_nn_delta_grid): DG_G x DG_G cells + one cell (index DG_NC) for non-finite positions.
+#define DG_G 64
+#define DG_NC (DG_G * DG_G)
+struct DeltaGrid {
+  int* cnt;            // [DG_NC + 2]: counts, then exclusive starts; [DG_NC + 1] = total
+  int* fill;           // [DG_NC + 1]
+  unsigned int* cmin;  // [DG_NC + 1] minimum costE per cell (order-preserving encoding)
+  unsigned int* box;   // [4 (DG_NC + 1)] x0, y0, -x1, -y1 of the cell's float positions (encoded minima)
+  unsigned int* gmin;  // [1] minimum costE of all records
+  float4* frame;       // [1] x0, y0, 1 / cell, cell (float frame coordinates)
+  int* idx;            // [capacity] record indices in cell order
+  int cap;
+};
+
 struct NnFrame {
   double ox, oy;
   float delta;
@@ -214,10 +229,11 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
                                  bool stateless);
 // Pipelined BATCH rounds: merges into (cand, ckey, ncand) -- the lists over nodes [0, first) -- the
-// nodes [first, first + count) appended since (k_nn_partial over them + k_nn_merge_delta).
+// nodes [first, first + count) appended since (k_nn_partial over them, or k_nn_delta_grid when `dg` is
+// given and can hold them, + k_nn_merge_delta).
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
-                           float* ckey, int* ncand, int* ctie, float* seed);
+                           float* ckey, int* ncand, int* ctie, float* seed, const DeltaGrid* dg = nullptr);
 // Brute-force candidate lists of the samples fb_list[0 .. *fb_count) (the walk search's hand-offs).
 hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,

@@ -386,6 +386,211 @@ __global__ void k_nn_merge_delta(int B, int nchunks, int limit, const float* __r
   ctie[s] = tie;
 }
 
+// Appended-node search through a uniform grid (pipelined BATCH rounds; replaces the chunked brute force
+// of launch_nn_delta when a DeltaGrid is given).  The round's appended records [first, first + n) are
+// bucketed by their float frame position into DG_G x DG_G cells over their bounding box (records with
+// non-finite positions into an extra cell every sample visits); per cell the bounding box of those float
+// positions and the minimum costE are kept.  One lane per sample then visits only the cells that can hold
+// a record able to enter its list: the cell range of the prune radius of the seed (the walk list's
+// `limit`-th key: a larger key cannot enter the merged list, an equal one sorts after it since every
+// appended id is larger), and per cell the tile bound of k_nn_partial's place-ordered path (cell box
+// distance against the prune radius of min(11th key, seed) minus the cell's minimum cost).  The records
+// visited go through k_nn_partial's tests unchanged (Euclidean prune, feasibleNode margins, turning
+// circle, the key's lower bound, exact key, feasibleNode), so the lane's list holds the 11 smallest
+// (key, id) pairs of every appended record that can enter, and k_nn_merge_delta's result is the one the
+// brute force gives.
+__global__ void k_dg_init(DeltaGrid g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= DG_NC) {
+    g.cnt[i] = 0;
+    g.fill[i] = 0;
+    g.cmin[i] = 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < 4; q++) g.box[4 * i + q] = 0xffffffffu;
+  }
+  if (i == 0) g.gmin[0] = 0xffffffffu;
+}
+
+// grid frame over the finite float positions: x0, y0, 1 / cell, cell (one block)
+__global__ void __launch_bounds__(256) k_dg_bounds(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
+  float x0 = __builtin_inff(), y0 = __builtin_inff(), x1 = -__builtin_inff(), y1 = -__builtin_inff();
+  float cm = __builtin_inff();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float fx = (float)(nodes[i].x - fr.ox), fy = (float)(nodes[i].y - fr.oy);
+    cm = fminf(cm, nodes[i].costE);
+    if (!(isfinite(fx) && isfinite(fy))) continue;
+    x0 = fminf(x0, fx); x1 = fmaxf(x1, fx);
+    y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
+  }
+  __shared__ float r[5][256];
+  r[0][threadIdx.x] = x0; r[1][threadIdx.x] = y0; r[2][threadIdx.x] = -x1; r[3][threadIdx.x] = -y1;
+  r[4][threadIdx.x] = cm;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int q = 0; q < 5; q++) r[q][threadIdx.x] = fminf(r[q][threadIdx.x], r[q][threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    x0 = r[0][0]; y0 = r[1][0]; x1 = -r[2][0]; y1 = -r[3][0];
+    float cs = fmaxf(x1 - x0, y1 - y0) * (1.0f / DG_G) * 1.0001f;
+    if (!(cs > 1e-3f)) cs = 1e-3f;  // also no finite position at all
+    if (!isfinite(x0)) { x0 = 0.f; y0 = 0.f; }
+    g.frame[0] = make_float4(x0, y0, 1.0f / cs, cs);
+    g.gmin[0] = ord_enc32(r[4][0]);
+  }
+}
+
+__device__ __forceinline__ int dg_cell(const float4& gf, float fx, float fy) {
+  if (!(isfinite(fx) && isfinite(fy))) return DG_NC;
+  const int gx = min(max((int)floorf((fx - gf.x) * gf.z), 0), DG_G - 1);
+  const int gy = min(max((int)floorf((fy - gf.y) * gf.z), 0), DG_G - 1);
+  return gy * DG_G + gx;
+}
+
+__global__ void __launch_bounds__(256) k_dg_count(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 gf = g.frame[0];
+  const float fx = (float)(nodes[i].x - fr.ox), fy = (float)(nodes[i].y - fr.oy);
+  const int c = dg_cell(gf, fx, fy);
+  atomicAdd(&g.cnt[c], 1);
+  atomicMin(&g.cmin[c], ord_enc32(nodes[i].costE));
+  atomicMin(&g.box[4 * c], ord_enc32(fx));
+  atomicMin(&g.box[4 * c + 1], ord_enc32(fy));
+  atomicMin(&g.box[4 * c + 2], ord_enc32(-fx));
+  atomicMin(&g.box[4 * c + 3], ord_enc32(-fy));
+}
+
+// exclusive scan of the DG_NC + 1 counts in place (one block of 1024); cnt[DG_NC + 1] = total
+__global__ void __launch_bounds__(1024) k_dg_scan(DeltaGrid g) {
+  constexpr int per = (DG_NC + 1 + 1023) / 1024;
+  __shared__ int s[1024];
+  const int b = threadIdx.x * per;
+  int v[per], sum = 0;
+#pragma unroll
+  for (int q = 0; q < per; q++) {
+    v[q] = b + q <= DG_NC ? g.cnt[b + q] : 0;
+    sum += v[q];
+  }
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int t = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int run = s[threadIdx.x] - sum;
+#pragma unroll
+  for (int q = 0; q < per; q++) {
+    if (b + q <= DG_NC) g.cnt[b + q] = run;
+    run += v[q];
+  }
+  if (threadIdx.x == 1023) g.cnt[DG_NC + 1] = s[1023];
+}
+
+__global__ void __launch_bounds__(256) k_dg_scatter(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 gf = g.frame[0];
+  const int c = dg_cell(gf, (float)(nodes[i].x - fr.ox), (float)(nodes[i].y - fr.oy));
+  g.idx[g.cnt[c] + atomicAdd(&g.fill[c], 1)] = i;
+}
+
+__global__ void __launch_bounds__(64) k_nn_delta_grid(const clrrt_sample* __restrict__ S, int B,
+                                                      const NnRec* __restrict__ nodes, DevParams p, NnFrame fr,
+                                                      DeltaGrid g, const float* __restrict__ seed,
+                                                      float* __restrict__ pk, int* __restrict__ pi) {
+  // explore samples in the first half of the grid, optimize samples in the second: a wave then holds one
+  // kind only (optimize radii, which subtract the costE, span most of the cells; explore radii a few)
+  const int half = (int)gridDim.x >> 1;
+  const bool want_ex = (int)blockIdx.x < half;
+  const int s = ((int)blockIdx.x - (want_ex ? 0 : half)) * (int)blockDim.x + (int)threadIdx.x;
+  if (s >= B || (S[s].explore != 0) != want_ex) return;
+  const double sx = S[s].x, sy = S[s].y;
+  const bool ex = want_ex;
+  const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
+  const float dl = fr.delta;
+  float keys[NN_K];
+  int ids[NN_K];
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
+  const float kcap = ord_dec32(((const unsigned int*)seed)[s]);
+  const float flen = (float)p.feas_len - 2.f * dl;
+  const float fl2 = flen > 0.f ? flen * flen : 0.f;
+  const float c45 = 0.69276f;
+  const float rho = 4.77f, rin = rho - 0.01f - 4.f * dl;
+  const float rin2 = rin > 0.f ? rin * rin : -1.f;
+  auto lim_of = [&](float slack) -> float {  // (prune radius + delta)^2; -1: nothing can enter
+    const float R = prune_r(slack);
+    return R < 0.f ? -1.f : (R + dl) * (R + dl);
+  };
+  auto test = [&](int i) {
+    const NnRec& rec = nodes[i];
+    const float kt = fminf(keys[NN_K - 1], kcap);
+    const float cst = rec.costE;
+    const float qx = (float)(rec.x - fr.ox), qy = (float)(rec.y - fr.oy);
+    const float dx = rsx - qx, dy = rsy - qy;
+    const float d2 = dx * dx + dy * dy;
+    const float lim = lim_of(ex ? kt : kt - cst);
+    if (!((d2 <= lim) || (lim != lim))) return;  // a NaN limit never prunes
+    const float vx = rsx - (float)(rec.bx - fr.ox), vy = rsy - (float)(rec.by - fr.oy);
+    const float dot = vx * rec.ca + vy * rec.sa, vv = vx * vx + vy * vy;
+    const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
+    const float tx = rec.c * dx - rec.s * dy, ty = fabsf(rec.s * dx + rec.c * dy);
+    const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
+    const bool in_bad = deep && !((ex ? 14.9f : cst + 14.9f) <= kt);
+    if (ang_bad || in_bad) return;
+    const float qx2 = (float)(sx - rec.x), qy2 = (float)(sy - rec.y);
+    const float tx2 = rec.c * qx2 - rec.s * qy2, ty2 = fabsf(rec.s * qx2 + rec.c * qy2);
+    float lb = dubins_lb(tx2, ty2);
+    if (!ex) lb = cst + lb;
+    if (lb > keys[NN_K - 1]) return;
+    float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+    if (!ex) key = cst + key;
+    // (key, i) must precede the lane's 11th entry; a key at or above the seed cannot enter the merge
+    if (!lex_less(key, i, keys[NN_K - 1], ids[NN_K - 1]) || !(key < kcap)) return;
+    if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) topk_insert(keys, ids, key, i);
+  };
+  const float4 gf = g.frame[0];
+  const float gmin = ord_dec32(g.gmin[0]);
+  // cell range from the initial radius (bounds only shrink)
+  const float lim0 = lim_of(ex ? kcap : kcap - gmin);
+  int gx0 = 0, gx1 = DG_G - 1, gy0 = 0, gy1 = DG_G - 1;
+  if (lim0 < 0.f) {
+    gx1 = gy1 = -1;  // nothing can enter
+  } else if (lim0 < __builtin_inff() && isfinite(rsx) && isfinite(rsy)) {
+    const float R = sqrtf(lim0) * 1.0001f + 1e-3f;
+    gx0 = max(0, (int)floorf((rsx - R - gf.x) * gf.z) - 1);
+    gx1 = min(DG_G - 1, (int)floorf((rsx + R - gf.x) * gf.z) + 1);
+    gy0 = max(0, (int)floorf((rsy - R - gf.y) * gf.z) - 1);
+    gy1 = min(DG_G - 1, (int)floorf((rsy + R - gf.y) * gf.z) + 1);
+  }
+  for (int gy = gy0; gy <= gy1; gy++)
+    for (int gx = gx0; gx <= gx1; gx++) {
+      const int c = gy * DG_G + gx;
+      const int a = g.cnt[c], e = g.cnt[c + 1];
+      if (a == e) continue;
+      // the cell's bound: distance from the sample to the box of its records' float positions
+      const float bx0 = ord_dec32(g.box[4 * c]), by0 = ord_dec32(g.box[4 * c + 1]);
+      const float bx1 = -ord_dec32(g.box[4 * c + 2]), by1 = -ord_dec32(g.box[4 * c + 3]);
+      const float ex0 = fmaxf(fmaxf(bx0 - rsx, rsx - bx1), 0.f);
+      const float ey0 = fmaxf(fmaxf(by0 - rsy, rsy - by1), 0.f);
+      const float bd2 = (ex0 * ex0 + ey0 * ey0) * (1.f - 1e-6f);
+      const float kt = fminf(keys[NN_K - 1], kcap);
+      const float lim = lim_of(ex ? kt : kt - ord_dec32(g.cmin[c]));
+      if (bd2 > lim) continue;  // NaN bounds never skip
+      for (int q = a; q < e; q++) test(g.idx[q]);
+    }
+  for (int q = g.cnt[DG_NC]; q < g.cnt[DG_NC + 1]; q++) test(g.idx[q]);  // non-finite positions
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) {
+    pk[(size_t)s * NN_K + j] = keys[j];
+    pi[(size_t)s * NN_K + j] = ids[j];
+  }
+}
+
 // EXACT mode, samples whose candidate selection involves equal keys: rebuild the full (id, key)
 // sequence in node order and replay libstdc++'s std::sort on it (one lane per sample), then walk it
 // exactly as sortNodesExplore/Optimize do (rrtplanner.cpp:237-243).
@@ -2031,8 +2236,30 @@ hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, co
 
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
-                           float* ckey, int* ncand, int* ctie, float* seed) {
+                           float* ckey, int* ncand, int* ctie, float* seed, const DeltaGrid* dg) {
   if (count <= 0 || B <= 0) return hipSuccess;
+  if (dg && count <= dg->cap) {
+    const NnRec* base = nodes + first;
+    hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 255) / 256), dim3(256), 0, st, B, p.sort_limit, ckey, ncand, seed);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dg_init, dim3((DG_NC + 1 + 255) / 256), dim3(256), 0, st, *dg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dg_bounds, dim3(1), dim3(256), 0, st, base, count, fr, *dg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dg_count, dim3((count + 255) / 256), dim3(256), 0, st, base, count, fr, *dg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dg_scan, dim3(1), dim3(1024), 0, st, *dg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dg_scatter, dim3((count + 255) / 256), dim3(256), 0, st, base, count, fr, *dg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_nn_delta_grid, dim3(2 * ((B + 63) / 64)), dim3(64), 0, st, S, B, base, p, fr, *dg, seed, pk,
+                       pi);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 255) / 256), dim3(256), 0, st, B, 1, p.sort_limit, pk, pi, first,
+                       cand, ckey, ncand, ctie);
+    LAUNCH_CHECK();
+    return hipSuccess;
+  }
   const int groups = (B + 255) / 256;
   int nchunks = (count + 255) / 256;
   const int want = max(1, 2048 / max(1, groups));

@@ -321,15 +321,18 @@ def test_pipelined_batch_rounds_identical():
     rollouts move between waves (roll_handoff), grow exactly the tree of plain rounds (every node
     record and trajectory row).  So do the scheduling and search options: the rollout queue order
     (roll_priority), the persistent grid width (roll_blocks), the reference-point cache
-    (roll_point_cache), the single-buffered walk index (nn_walk_double) and the walk without overflow
-    split (budget 0) or with every sample split (budget 1)."""
+    (roll_point_cache), the single-buffered walk index (nn_walk_double), the walk without overflow
+    split (budget 0) or with every sample split (budget 1), the appended-node search through the grid
+    instead of the chunked brute force (nn_delta_grid) and the next index built on the side stream
+    (nn_side_build)."""
     mode, obs = _scene("obb200")
     trees = []
     variants = [dict(nn_pipeline=0, roll_handoff=0), dict(nn_pipeline=1, roll_handoff=0),
                 dict(nn_pipeline=1, roll_handoff=1), dict(roll_priority=0, roll_blocks=512),
                 dict(roll_point_cache=1, nn_walk_double=0),
                 dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
-                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
+                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5),
+                dict(nn_delta_grid=1, nn_side_build=1)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
@@ -346,6 +349,29 @@ def test_pipelined_batch_rounds_identical():
     assert trees[0][2] > 20000
     for t in trees[1:]:
         assert trees[0][0] == t[0] and trees[0][1] == t[1]
+
+
+@pytest.mark.gpu
+def test_delta_grid_matches_chunked_large_tree():
+    """The appended-node search through the grid (k_nn_delta_grid) against the chunked brute force
+    (k_nn_partial) over 40 pipelined cfg3 rounds (trees past 250 k nodes, where the appended records are
+    a small fraction of the tree): identical trees, record for record and row for row."""
+    mode, obs = _scene("obb200")
+    trees = []
+    for grid in (1, 0):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 27,
+                           max_batch=16384)
+        pl.set_option("nn_delta_grid", grid)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(21), n_iters=16384 * 40, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+        assert st["rounds"] == 40
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n))
+        pl.close()
+    print(f"delta grid: {trees[0][2]} nodes")
+    assert trees[0][2] > 200000
+    assert trees[0][0] == trees[1][0] and trees[0][1] == trees[1][1]
 
 
 @pytest.mark.gpu
