@@ -145,11 +145,13 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       const float tx = f.x * qx - f.y * qy, ty = fabsf(f.y * qx + f.x * qy);
       float lb = dubins_lb(tx, ty);
       if (!ex) lb = cost + lb;
-      if (lb > keys[NN_K - 1]) continue;
+      // kcap bounds the sample's 11th key over all chunks (and, for the appended-node search, the
+      // `limit`-th key of the older nodes' list): a key above it cannot be in the merged list
+      if (lb > keys[NN_K - 1] || lb > kcap) continue;
       n_exact++;
       float key = dubins_key(sx, sy, np.x, np.y, f.x, f.y);
       if (!ex) key = cost + key;
-      if (!lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1])) continue;
+      if (!lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) || key > kcap) continue;
       const NnRec& rec = nodes[b + k];
       if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
         topk_insert(keys, ids, key, n);
