@@ -422,3 +422,41 @@ def test_walk_overflow_matches_brute(chunks):
     assert records == 512
     assert np.array_equal(ib, iw)
     assert np.array_equal(np.asarray(kb, np.float32).view(np.uint32), np.asarray(kw, np.float32).view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode_name", ["EXACT", "BATCH"])
+def test_budget_loop_termination_and_draws(mode_name):
+    """SURVEY §8(a) a13, the Timer(200) loop of planMotion (motionplanner.cpp:39-43) as clrrt_expand with a
+    wall-clock budget: it stops once 200 ms have elapsed (checked between rounds), consumes exactly three
+    rand() draws per counted iteration (the returned RNG state equals a fresh stream advanced 3 x
+    iterations), and its tree equals the fixed-count expansion of the same number of iterations."""
+    mode, obs = _scene("obb200")
+    m = clrrt.CLRRT_MODE_EXACT if mode_name == "EXACT" else clrrt.CLRRT_MODE_BATCH
+    batch = 256 if mode_name == "EXACT" else 4096
+    trees, its = [], None
+    for fixed in (False, True):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
+                           max_batch=batch)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        rng = clrrt.Rng(9)
+        if not fixed:
+            st = pl.expand(rng, n_iters=0, budget_ms=200.0, mode=m, batch=batch)
+            its = st["iterations"]
+            assert its > 0 and st["elapsed_ms"] >= 200.0, st
+            assert st["elapsed_ms"] < 200.0 + 5000.0, st
+            if m == clrrt.CLRRT_MODE_BATCH:
+                assert its % batch == 0, st
+            ref = clrrt.Rng(9)
+            for _ in range(3 * its):
+                ref.next()
+            assert bytes(rng.state) == bytes(ref.state)
+        else:
+            st = pl.expand(rng, n_iters=its, mode=m, batch=batch)
+            assert st["iterations"] == its
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes()))
+        pl.close()
+    print(mode_name, "budget 200 ms:", its, "iterations")
+    assert trees[0] == trees[1]
