@@ -376,8 +376,9 @@ class Planner:
         return out
 
     # in/out widths per CLRRT_UNIT_* (include/clrrt.h)
-    UNIT_IN = {0: 11, 1: 9, 2: 9, 3: 12, 4: 2}
-    UNIT_OUT = {0: 1, 1: 8, 2: 1, 3: 1 + 3 * abi.UNIT_PROFILE_NMAX, 4: 2}
+    UNIT_IN = {0: 11, 1: 9, 2: 9, 3: 12, 4: 2, 5: 6, 6: 7, 7: 8, 8: 8, 9: 12 + 6 * abi.UNIT_CTRL_K}
+    UNIT_OUT = {0: 1, 1: 8, 2: 1, 3: 1 + 3 * abi.UNIT_PROFILE_NMAX, 4: 2, 5: 2, 6: 3, 7: 1,
+                8: 1 + 3 * abi.UNIT_PROFILE_NMAX, 9: 4 + 8 * abi.UNIT_CTRL_K}
 
     def selftest_units(self, unit, cases):
         """Device evaluation of a hot-path unit (clrrt_selftest_units): cases [n, UNIT_IN] -> [n, UNIT_OUT]."""

@@ -7,7 +7,9 @@ import ctypes as C
 
 CLRRT_ABI_VERSION = 6  # include/clrrt.h
 UNIT_OBB, UNIT_ODE, UNIT_LATERAL, UNIT_PROFILE, UNIT_ANGLE = 0, 1, 2, 3, 4  # CLRRT_UNIT_*
+UNIT_DUBINS, UNIT_FEASIBLE, UNIT_GOALBIAS, UNIT_GOALREF, UNIT_CTRL = 5, 6, 7, 8, 9
 UNIT_PROFILE_NMAX = 1024
+UNIT_CTRL_K = 24
 CLRRT_MODE_EXACT = 0
 CLRRT_PARENT_PREV = -2  # goal-biased record: parent = the record before it (include/clrrt.h)
 CLRRT_MODE_BATCH = 1

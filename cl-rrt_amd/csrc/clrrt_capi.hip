@@ -419,7 +419,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
-                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.TRIG, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.TRIG, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
+                  c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
                   c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2,
                   c->dg.cnt, c->dg.fill, c->dg.cmin, c->dg.box, c->dg.gmin, c->dg.frame, c->dg.idx};
   for (void* p : ptrs)
@@ -1262,7 +1262,6 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.CE, Mp));
   HIPC(c, dalloc(&w.ID, Mp));
   HIPC(c, dalloc(&w.HEAD, Mp));
-  HIPC(c, dalloc(&w.TRIG, Mp));
   HIPC(c, dalloc(&w.tiles, Mp / 64 + 1));
   HIPC(c, dalloc(&w.supers, Mp / 1024 + 1));
   HIPC(c, dalloc(&w.ovf_n, 1));
@@ -1915,9 +1914,11 @@ int clrrt_obstacle_distance(clrrt_ctx* c, const double* states, int32_t n, doubl
 }
 
 int clrrt_selftest_units(clrrt_ctx* c, int32_t unit, const double* in, int32_t n, double* out) {
-  static const int kin[5] = {11, 9, 9, 12, 2};
-  static const int kout[5] = {1, 8, 1, 1 + 3 * CLRRT_UNIT_PROFILE_NMAX, 2};
-  if (!c || n < 0 || (n > 0 && (!in || !out)) || unit < 0 || unit > 4) return CLRRT_EINVAL;
+  const int K = CLRRT_UNIT_CTRL_K;
+  static const int kin[10] = {11, 9, 9, 12, 2, 6, 7, 8, 8, 12 + 6 * K};
+  static const int kout[10] = {1, 8, 1, 1 + 3 * CLRRT_UNIT_PROFILE_NMAX, 2, 2, 3, 1, 1 + 3 * CLRRT_UNIT_PROFILE_NMAX,
+                               4 + 8 * K};
+  if (!c || n < 0 || (n > 0 && (!in || !out)) || unit < 0 || unit > CLRRT_UNIT_CTRL) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
   const size_t nin = (size_t)kin[unit] * n, nout = (size_t)kout[unit] * n;
@@ -1930,21 +1931,41 @@ int clrrt_selftest_units(clrrt_ctx* c, int32_t unit, const double* in, int32_t n
       bake_obstacle(o, baked[i]);
     }
   }
+  // per-case parameters: the context's, with the case's goal / vmax / ref_res, derived as
+  // clrrt_set_params derives them
+  std::vector<DevParams> cps;
+  if (unit >= CLRRT_UNIT_FEASIBLE) {
+    cps.resize(n);
+    for (int i = 0; i < n; i++) {
+      const double* a = in + (size_t)kin[unit] * i;
+      clrrt_params q = c->params;
+      if (unit == CLRRT_UNIT_FEASIBLE) q.ref_res = a[6];
+      if (unit == CLRRT_UNIT_GOALBIAS) for (int k = 0; k < 4; k++) q.goal[k] = a[k];
+      if (unit == CLRRT_UNIT_GOALREF) { for (int k = 0; k < 4; k++) q.goal[k] = a[k]; q.ref_res = a[7]; }
+      if (unit == CLRRT_UNIT_CTRL) { for (int k = 0; k < 4; k++) q.goal[k] = a[5 + k]; q.vmax = a[10]; q.ref_res = a[11]; }
+      derive(q, cps[i], c->n_obs);
+    }
+  }
   double *din = nullptr, *dout = nullptr;
   BakedObs* dobs = nullptr;
+  DevParams* dcp = nullptr;
   hipError_t e = hipMalloc((void**)&din, sizeof(double) * nin);
   if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * nout);
   if (e == hipSuccess && !baked.empty()) e = hipMalloc((void**)&dobs, sizeof(BakedObs) * baked.size());
+  if (e == hipSuccess && !cps.empty()) e = hipMalloc((void**)&dcp, sizeof(DevParams) * cps.size());
   if (e == hipSuccess) e = hipMemcpyAsync(din, in, sizeof(double) * nin, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess && dobs)
     e = hipMemcpyAsync(dobs, baked.data(), sizeof(BakedObs) * baked.size(), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && dcp)
+    e = hipMemcpyAsync(dcp, cps.data(), sizeof(DevParams) * cps.size(), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(dout, 0, sizeof(double) * nout, c->stream);
-  if (e == hipSuccess) e = launch_selftest_units(c->stream, unit, din, dobs, n, c->dp, dout);
+  if (e == hipSuccess) e = launch_selftest_units(c->stream, unit, din, dobs, n, c->dp, dcp, dout);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(din);
   hipFree(dout);
   if (dobs) hipFree(dobs);
+  if (dcp) hipFree(dcp);
   if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("selftest_units: ") + hipGetErrorString(e));
   return CLRRT_OK;
 }

@@ -403,5 +403,145 @@ CLRRT_HD inline float sinf(float y) {
   return s;
 }
 
+// --------------------------------------------------------------------------------- double atan2
+// glibc 2.35 atan2 (sysdeps/ieee754/dbl-64/e_atan2.c, IBM Accurate Mathematical Library; the FMA variant
+// libm's ifunc selects on FMA+AVX2 hosts, whose build contracts the EMULV product error and the
+// polynomials into fused multiply-adds): special cases, de = exponent difference cut-offs, 2^+-500
+// scaling, then u = min/max of |x|, |y| with its division residual du, and atan(u) either from an odd
+// polynomial (u < 1/16) or from the cij table row of the 1/256 grid point nearest u (uatan2.tbl), in the
+// quadrant form (i) x > 0, |y| < |x|; (ii) x > 0, |x| <= |y|; (iii) x < 0, |x| < |y|; (iv) x < 0,
+// |y| <= |x|, with EADD / ESUB double-double corrections.  The reference's feasibleNode angles
+// (rrtplanner.cpp:273-274), feasibleGoalBias' angleRef (:305) and sampleAroundVehicle's goal heading
+// (:189) call it; restated so that every decision compares the reference's own angles.  Checked bit for
+// bit against the host libm (tests/native/atan2_check.cpp).  The default rounding mode is assumed (the
+// library's SET_RESTORE_ROUND is a no-op then).
+#if defined(__HIPCC__)
+static __device__ __constant__ double d_atan2_cij[ATAN2_CIJ_ROWS * 7] = CLRRT_GLIBC_ATAN2_CIJ;
+#endif
+static const double h_atan2_cij[ATAN2_CIJ_ROWS * 7] = CLRRT_GLIBC_ATAN2_CIJ;
+
+// the cij row of u in [1/16, 1]: i = (TWO52 + TWO8 * u) - TWO52 (one rounding), minus 16
+CLRRT_HD inline const double* atan2_row(double u) {
+  const int i = (int)(fma_(u, at_two8, at_two52) - at_two52) - 16;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return d_atan2_cij + 7 * i;
+#else
+  return h_atan2_cij + 7 * i;
+#endif
+}
+// d3 + v (d5 + v (d7 + v (d9 + v (d11 + v d13)))), contracted
+CLRRT_HD inline double atan2_poly(double v) {
+  double p = fma_(v, at_d13, at_d11);
+  p = fma_(v, p, at_d9);
+  p = fma_(v, p, at_d7);
+  p = fma_(v, p, at_d5);
+  return fma_(v, p, at_d3);
+}
+// cij[2] + v (cij[3] + v (cij[4] + v (cij[5] + v cij[6]))), contracted
+CLRRT_HD inline double atan2_tpoly(const double* c, double v) {
+  double p = fma_(v, c[6], c[5]);
+  p = fma_(v, p, c[4]);
+  p = fma_(v, p, c[3]);
+  return fma_(v, p, c[2]);
+}
+
+CLRRT_HD inline double atan2(double y, double x) {
+  const uint32_t ux = hi_word(x), dx = (uint32_t)lo_word(x);
+  const uint32_t uy = hi_word(y), dy = (uint32_t)lo_word(y);
+  if ((ux & 0x7ff00000u) == 0x7ff00000u && ((ux & 0xfffffu) | dx) != 0) return x + y;  // x NaN
+  if ((uy & 0x7ff00000u) == 0x7ff00000u && ((uy & 0xfffffu) | dy) != 0) return y + y;  // y NaN
+  const bool xneg = (int32_t)ux < 0, yneg = (int32_t)uy < 0;
+  if (uy == 0 && dy == 0) return xneg ? at_opi : 0.0;                   // y = +0
+  if (uy == 0x80000000u && dy == 0) return xneg ? at_mopi : -0.0;       // y = -0
+  if (x == 0) return yneg ? at_mhpi : at_hpi;
+  if (dx == 0 && ux == 0x7ff00000u) {                                    // x = +inf
+    if (dy == 0 && uy == 0x7ff00000u) return at_qpi;
+    if (dy == 0 && uy == 0xfff00000u) return at_mqpi;
+    return yneg ? -0.0 : 0.0;
+  }
+  if (dx == 0 && ux == 0xfff00000u) {                                    // x = -inf
+    if (dy == 0 && uy == 0x7ff00000u) return at_tqpi;
+    if (dy == 0 && uy == 0xfff00000u) return at_mtqpi;
+    return yneg ? at_mopi : at_opi;
+  }
+  if (dy == 0 && uy == 0x7ff00000u) return at_hpi;                       // y = +inf
+  if (dy == 0 && uy == 0xfff00000u) return at_mhpi;                      // y = -inf
+  double ax = x < 0 ? -x : x, ay = y < 0 ? -y : y;
+  const int32_t de = (int32_t)(uy & 0x7ff00000u) - (int32_t)(ux & 0x7ff00000u);
+  if (de >= 59768832) return (0 < y) ? at_hpi : at_mhpi;                 // 57 * 16^5
+  if (de <= -59768832) {
+    if (x > 0) return copysign_(ay / ax, y);
+    return (0 < y) ? at_opi : at_mopi;
+  }
+  if (ax < at_twom500 || ay < at_twom500) { ax *= at_two500; ay *= at_two500; }
+  if (ax > at_two500 || ay > at_two500) { ax *= at_twom500; ay *= at_twom500; }
+  double u, du;
+  if (ay < ax) {
+    u = ay / ax;
+    const double v = ax * u, vv = fma_(ax, u, -v);
+    du = ((ay - v) - vv) / ax;
+  } else {
+    u = ax / ay;
+    const double v = ay * u, vv = fma_(ay, u, -v);
+    du = ((ax - v) - vv) / ay;
+  }
+  double z;
+  if (x > 0) {
+    if (ay < ax) {  // (i) atan(ay / ax)
+      if (u < at_inv16) {
+        const double v = u * u;
+        z = u + fma_(u * v, atan2_poly(v), du);
+      } else {
+        const double* c = atan2_row(u);
+        const double t3 = u - c[0];
+        const double v = t3 + du;  // EADD (t3, du, v, dv)
+        const double dv = (fabs(t3) > fabs(du)) ? (t3 - v) + du : (du - v) + t3;
+        double p = fma_(v, c[6], c[5]);
+        p = fma_(v, p, c[4]);
+        p = fma_(v, p, c[3]);
+        double q = fma_(dv, c[2], (v * v) * p);
+        z = fma_(v, c[2], q) + c[1];
+      }
+    } else {  // (ii) pi/2 - atan(ax / ay)
+      if (u < at_inv16) {
+        const double v = u * u;
+        const double zz = (u * v) * atan2_poly(v);
+        const double t2 = at_hpi - u;  // ESUB (hpi, u, t2, cor)
+        const double cor = (at_hpi > fabs(u)) ? (at_hpi - t2) - u : at_hpi - (u + t2);
+        z = (((cor + at_hpi1) - du) - zz) + t2;
+      } else {
+        const double* c = atan2_row(u);
+        const double v = (u - c[0]) + du;
+        z = (at_hpi - c[1]) + fma_(-v, atan2_tpoly(c, v), at_hpi1);
+      }
+    }
+  } else if (ax < ay) {  // (iii) pi/2 + atan(ax / ay)
+    if (u < at_inv16) {
+      const double v = u * u;
+      const double zz = (v * u) * atan2_poly(v);
+      const double t2 = u + at_hpi;  // EADD (hpi, u, t2, cor)
+      const double cor = (at_hpi > fabs(u)) ? (at_hpi - t2) + u : (u - t2) + at_hpi;
+      z = (((cor + at_hpi1) + du) + zz) + t2;
+    } else {
+      const double* c = atan2_row(u);
+      const double v = (u - c[0]) + du;
+      z = (at_hpi + c[1]) + fma_(v, atan2_tpoly(c, v), at_hpi1);
+    }
+  } else {  // (iv) pi - atan(ay / ax)
+    if (u < at_inv16) {
+      const double v = u * u;
+      const double zz = (v * u) * atan2_poly(v);
+      const double t2 = at_opi - u;  // ESUB (opi, u, t2, cor)
+      const double cor = (at_opi > fabs(u)) ? (at_opi - t2) - u : at_opi - (t2 + u);
+      z = (((cor + at_opi1) - du) - zz) + t2;
+    } else {
+      const double* c = atan2_row(u);
+      const double v = (u - c[0]) + du;
+      z = (at_opi - c[1]) + fma_(-v, atan2_tpoly(c, v), at_opi1);
+    }
+  }
+  return copysign_(z, y);
+}
+
 }  // namespace glibc
 }  // namespace clrrt

@@ -198,7 +198,6 @@ struct WalkBufs {
   float* CE;               // costE
   int* ID;                 // node id (-1: padding)
   int* HEAD;               // first record of the run of records with equal Dubins-key inputs
-  double2* TRIG;           // (cos, sin)(ang_par) in double
   WalkTile *tiles, *supers;
   // overflow of the walk: a sample whose walk passes the budget (tiles visited / exact keys) hands
   // its search to nch waves over interleaved super-tile subsets with the list's 11th entry as the
@@ -280,8 +279,9 @@ hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t ba
 hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const double* b, int n, double* out);
 hipError_t launch_obs_distance(hipStream_t st, const DevParams& p, const BakedObs* obs, const double* states, int n,
                                double* out);
+// cp: per-case parameters (units CLRRT_UNIT_FEASIBLE .. CLRRT_UNIT_CTRL), else null
 hipError_t launch_selftest_units(hipStream_t st, int unit, const double* in, const BakedObs* obs, int n,
-                                 const DevParams& p, double* out);
+                                 const DevParams& p, const DevParams* cp, double* out);
 // extractBestPath helpers: goal nodes (id, costS) appended in any order (count in *cnt), and the
 // ancestor chain of `start` (start first) into path[0 .. cap) with its full length in *len.
 struct GoalRec { int32_t id; float cost; };

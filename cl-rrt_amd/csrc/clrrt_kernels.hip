@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   int ids[NN_K];
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
-  const float feas2 = (float)(p.feas_len * (1 - 1e-6) * p.feas_len * (1 - 1e-6));
+  const float feas2 = nn_feas2(p.feas_len);
   const float flen = (float)p.feas_len - 2.f * fr.delta;
   const float fl2 = flen > 0.f ? flen * flen : 0.f;
   const float c45 = 0.69276f;                    // cos(pi/4 + 0.02), rounded down
@@ -815,12 +815,9 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
     ym = fmin(ym, ym + (double)(r2.wp - r.wp) * z);
   }
 #endif
-  double cmd = 2 * ((p.L + p.Kus * r.x4 * r.x4) / (dla * dla)) * ym;
-  double dc = satd(-p.dmax, p.dmax, cmd);
+  const double dc = steer_cmd(r, p, dla, ym);
   const double vref = prof_v(r.P, r.wp + 2);  // ref.v[IDwp + 2]: the PI error and the logged column 8
-  double E = vref - r.x4;
-  r.iE = r.iE + E * p.dt;
-  double ac = satd(p.amin, p.amax, p.Kp * E + p.Ki * r.iE);
+  const double ac = accel_cmd(r, p, vref);
   // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
   const double d2 = ode_euler(r, p, dc, ac);
   if (pc) pc->mark(2);
@@ -935,7 +932,7 @@ __device__ __forceinline__ bool feasible_goal_bias(const DevParams& p, const dou
                                                    double by) {
   bool outL = sqrt((st[0] - p.gbLx) * (st[0] - p.gbLx) + (st[1] - p.gbLy) * (st[1] - p.gbLy)) > p.gbR2;
   bool outR = sqrt((st[0] - p.gbRx) * (st[0] - p.gbRx) + (st[1] - p.gbRy) * (st[1] - p.gbRy)) > p.gbR2;
-  double aRef = atan2(p.g1 - by, p.g0 - bx);
+  double aRef = glibc::atan2(p.g1 - by, p.g0 - bx);
   double h1 = fabs(wrap_pi(p.g2 - aRef));
   double h2 = fabs(wrap_pi(p.g2 + M_PI - aRef));
   double m = mn(h1, h2);
@@ -1470,7 +1467,7 @@ __device__ __forceinline__ void fill_node(clrrt_node& n, const RollRes& r, int p
   n.ref_front[0] = r.fx; n.ref_front[1] = r.fy;
   n.ref_back[0] = r.bx; n.ref_back[1] = r.by;
   n.ref_vback = r.vback;
-  n.ang_par = atan2(r.by - r.fy, r.bx - r.fx);
+  n.ang_par = node_ang_par(r.bx, r.by, r.fx, r.fy);
   n.parent = parent;
   n.costE = (float)(r.costE + (double)pcE);
   n.costS = (float)(r.costS + (double)pcS);
@@ -1728,7 +1725,7 @@ __device__ void init_root(const double* st, clrrt_node* tree, NnRec* nn, double*
   n.ref_front[0] = 0.0; n.ref_front[1] = 0.0;
   n.ref_back[0] = x; n.ref_back[1] = 0.0;
   n.ref_vback = st[4];
-  n.ang_par = atan2(0.0 - 0.0, x - 0.0);
+  n.ang_par = node_ang_par(x, 0.0, 0.0, 0.0);
   n.parent = -1;
   n.costE = 0.f; n.costS = 0.f;
   n.goal = 0;
@@ -1824,7 +1821,7 @@ __global__ void __launch_bounds__(256) k_path_transform(clrrt_node* __restrict__
       point_world_to_car(d.ref_front[0], d.ref_front[1], P0, P1, s, c);
       point_world_to_car(d.ref_back[0], d.ref_back[1], P0, P1, s, c);
     }
-    d.ang_par = atan2(d.ref_back[1] - d.ref_front[1], d.ref_back[0] - d.ref_front[0]);
+    d.ang_par = node_ang_par(d.ref_back[0], d.ref_back[1], d.ref_front[0], d.ref_front[1]);
   } else if (i - n < nrows) {
     double* r = rows + (i - n) * 10;
     if (to_world) point_car_to_world(r[0], r[1], P0, P1, s, c);
@@ -1962,7 +1959,7 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 2: r = glibc::tan(x); break;
     case 3: r = sqrt(x); break;
     case 4: r = fmod(x, y); break;
-    case 5: r = atan2(x, y); break;
+    case 5: r = glibc::atan2(x, y); break;
     case 6: r = exp(x); break;
     case 7: r = x / y; break;
     case 8: { float sf, cf; glibc::sincosf(xf, sf, cf); r = (double)cf; } break;
@@ -2003,11 +2000,94 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
 // Hot-path units exactly as the kernels evaluate them, one case per lane (test hook: bit-compared with
 // the reference's own code through tests/golden/ref_units.npz).  Formats: clrrt_selftest_units.
 __global__ void k_selftest_units(int unit, const double* __restrict__ in, const BakedObs* __restrict__ obs, int n,
-                                 DevParams p, double* __restrict__ out) {
+                                 DevParams p, const DevParams* __restrict__ cp, double* __restrict__ out) {
   glibc::stage_tables();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   switch (unit) {
+    case CLRRT_UNIT_DUBINS: {  // the nearest-node record's rotation (nn_record) + dubins_key
+      const double* a = in + 6 * (int64_t)i;
+      clrrt_node d;
+      d.state[0] = a[2]; d.state[1] = a[3]; d.state[2] = a[4];
+      d.ref_back[0] = 0.0; d.ref_back[1] = 0.0;
+      d.ang_par = 0.0;
+      d.costE = (float)a[5];
+      const NnRec r = nn_record(d, 0);
+      const float key = dubins_key(a[0], a[1], r.x, r.y, r.c, r.s);
+      out[2 * (int64_t)i] = (double)key;
+      out[2 * (int64_t)i + 1] = (double)(r.costE + key);
+    } break;
+    case CLRRT_UNIT_FEASIBLE: {  // angPar as the node records carry it, then the three deciders
+      const double* a = in + 7 * (int64_t)i;
+      const DevParams& q = cp[i];
+      clrrt_node d;
+      d.state[0] = 0.0; d.state[1] = 0.0; d.state[2] = 0.0;
+      d.ref_back[0] = a[4]; d.ref_back[1] = a[5];
+      d.ang_par = node_ang_par(a[4], a[5], a[2], a[3]);
+      d.costE = 0.f;
+      const NnRec r = nn_record(d, 0);
+      const bool brute = feasible_node(r.bx, r.by, r.ang_par, a[0], a[1], q.feas_len);
+      const bool walk = feasible_walk(a[0], a[1], r.bx, r.by, r.ca, r.sa, r.ang_par, q.feas_len);
+      const float qx = (float)(a[0] - r.x), qy = (float)(a[1] - r.y);
+      const float feas2 = nn_feas2(q.feas_len);
+      const bool pre = nn_prefilter(a[0], a[1], qx, qy, r.c, r.s, r.ca, r.sa, r.bx, r.by, 0.f, 1,
+                                    __builtin_inff(), feas2);
+      out[3 * (int64_t)i] = brute ? 1.0 : 0.0;
+      out[3 * (int64_t)i + 1] = walk ? 1.0 : 0.0;
+      out[3 * (int64_t)i + 2] = pre ? 1.0 : 0.0;
+    } break;
+    case CLRRT_UNIT_GOALBIAS: {
+      const double* a = in + 8 * (int64_t)i;
+      const double st[2] = {a[4], a[5]};
+      out[i] = feasible_goal_bias(cp[i], st, a[6], a[7]) ? 1.0 : 0.0;
+    } break;
+    case CLRRT_UNIT_GOALREF: {  // getGoalReference's two segments + the goal-biased profile
+      const double* a = in + 8 * (int64_t)i;
+      const DevParams& q = cp[i];
+      RefD R = make_goal_ref(a[4], a[5], q);
+      double* row = out + (int64_t)(1 + 3 * CLRRT_UNIT_PROFILE_NMAX) * i;
+      row[0] = (double)R.N;
+      double x = R.a1x, y = R.a1y;
+      for (int j = 0; j < R.N; j++) {
+        if (j < CLRRT_UNIT_PROFILE_NMAX) {
+          row[1 + CLRRT_UNIT_PROFILE_NMAX + j] = x;
+          row[1 + 2 * CLRRT_UNIT_PROFILE_NMAX + j] = y;
+        }
+        if (j == R.N - 1) { R.bx = x; R.by = y; }
+        ref_next(R, j, x, y);
+      }
+      const Prof P = make_profile(R, a[6], q, true);
+      for (int j = 0; j < R.N && j < CLRRT_UNIT_PROFILE_NMAX; j++) row[1 + j] = prof_v(P, j);
+    } break;
+    case CLRRT_UNIT_CTRL: {  // Simulation ctor's controller + profile, then getControls per state
+      const int K = CLRRT_UNIT_CTRL_K;
+      const double* a = in + (int64_t)(12 + 6 * K) * i;
+      double* o = out + (int64_t)(4 + 8 * K) * i;
+      const DevParams& q = cp[i];
+      const bool GB = a[0] != 0.0;
+      const RefD R = GB ? make_goal_ref(a[1], a[2], q) : make_ref(a[1], a[2], a[3], a[4], q);
+      const double* st = a + 12;
+      double s0[10];
+      for (int k = 0; k < 10; k++) s0[k] = k < 6 ? st[k] : 0.0;
+      Roll r;
+      double Px, Py;
+      roll_init(r, s0, R, a[9], GB, q, &Px, &Py);
+      o[0] = (double)r.wp; o[1] = (double)r.endr; o[2] = Px; o[3] = Py;
+      for (int j = 0; j < K; j++) {
+        const double* x = st + 6 * j;
+        r.x0 = x[0]; r.x1 = x[1]; r.x2 = x[2]; r.x3 = x[3]; r.x4 = x[4]; r.x5 = x[5];
+        glibc::sincos(r.x2, r.s2, r.c2);
+        r.cwp = glibc::cos(r.x2);
+        r.swp = glibc::sin(r.x2);
+        const double dla = update_waypoint(r, q, Px, Py, false);
+        const double ym = lateral_error(r, Px, Py);
+        const double dc = steer_cmd(r, q, dla, ym);
+        const double ac = accel_cmd(r, q, prof_v(r.P, r.wp + 2));
+        double* w = o + 4 + 8 * j;
+        w[0] = (double)r.wp; w[1] = (double)r.endr; w[2] = Px; w[3] = Py;
+        w[4] = ym; w[5] = dc; w[6] = ac; w[7] = r.iE;
+      }
+    } break;
     case CLRRT_UNIT_OBB: {  // checkObsDistance's vehicle box vs one obstacle (getOBBdist)
       const double* a = in + 11 * (int64_t)i;
       double s2, c2;
@@ -2153,7 +2233,7 @@ __global__ void __launch_bounds__(256) k_nn_seed(const clrrt_sample* __restrict_
   for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
   const int ht = home[t] >> 8;
   const int a = max(0, (ht - 2) << 8), b = min(N, (ht + 3) << 8);
-  const float feas2 = (float)(p.feas_len * (1 - 1e-6) * p.feas_len * (1 - 1e-6));
+  const float feas2 = nn_feas2(p.feas_len);
   for (int k = a; k < b; k++) {
     const NnRec& rec = recs[k];
     const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
@@ -2485,9 +2565,9 @@ hipError_t launch_selftest_math(hipStream_t st, int fn, const double* a, const d
 }
 
 hipError_t launch_selftest_units(hipStream_t st, int unit, const double* in, const BakedObs* obs, int n,
-                                 const DevParams& p, double* out) {
+                                 const DevParams& p, const DevParams* cp, double* out) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_selftest_units, dim3((n + 255) / 256), dim3(256), 0, st, unit, in, obs, n, p, out);
+  hipLaunchKernelGGL(k_selftest_units, dim3((n + 255) / 256), dim3(256), 0, st, unit, in, obs, n, p, cp, out);
   LAUNCH_CHECK();
   return hipSuccess;
 }

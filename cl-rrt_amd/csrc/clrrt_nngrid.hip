@@ -248,7 +248,7 @@ struct Lane {
 // Nodes recs[a .. b) (wave-uniform range) offered to the lanes with `take` set.
 __device__ __forceinline__ void scan_nodes(Lane& L, const NnRec* __restrict__ recs, uint32_t a, uint32_t b,
                                            bool take, double feas_len) {
-  const float feas2 = (float)(feas_len * (1 - 1e-6) * feas_len * (1 - 1e-6));
+  const float feas2 = nn_feas2(feas_len);
   for (uint32_t k = a; k < b; k++) {
     const NnRec rec = recs[k];
     if (!take) continue;

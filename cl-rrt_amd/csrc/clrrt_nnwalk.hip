@@ -132,8 +132,7 @@ __global__ void k_walk_skeys(const clrrt_sample* __restrict__ S, int B, double x
 // Place-ordered float records (relative to the frame origin); entries N .. Npad are padding (id -1).
 __global__ void k_walk_gather(const NnRec* __restrict__ nodes, int N, int Npad, const int* __restrict__ order,
                               double ox, double oy, float4* __restrict__ P, float4* __restrict__ Q,
-                              float* __restrict__ CE, int* __restrict__ ID, int* __restrict__ dup,
-                              double2* __restrict__ trig) {
+                              float* __restrict__ CE, int* __restrict__ ID, int* __restrict__ dup) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= Npad) return;
   if (j < N) {
@@ -143,9 +142,6 @@ __global__ void k_walk_gather(const NnRec* __restrict__ nodes, int N, int Npad, 
     Q[j] = make_float4((float)(r.bx - ox), (float)(r.by - oy), r.ca, r.sa);
     CE[j] = r.costE;
     ID[j] = i;
-    double sp, cp;
-    sincos(r.ang_par, &sp, &cp);
-    trig[j] = make_double2(cp, sp);
     // a record whose Dubins-key inputs equal its predecessor's has the same key for every sample
     bool same = false;
     if (j > 0) {
@@ -476,7 +472,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
                                                     NnFrame fr, int* __restrict__ cand, float* __restrict__ ckey,
                                                     int* __restrict__ ncand, int* __restrict__ ctie,
                                                     const int* __restrict__ sorder,
-                                                    const double2* __restrict__ TRIG,
                                                     unsigned long long* __restrict__ stats, int bud_tiles,
                                                     int bud_ex, int* __restrict__ ovf_n, int4* __restrict__ ovf,
                                                     int max_over, int nch, float* __restrict__ pk,
@@ -595,24 +590,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       key = dubins_key(sx, sy, r.x, r.y, r.c, r.s);
       if (!ex) key = r.costE + key;
       if (w_less(key, id, kth, idk)) {
-        const float vx = (float)(sx - r.bx), vy = (float)(sy - r.by);
-        const float dot = vx * r.ca + vy * r.sa, vv = vx * vx + vy * vy;
-        const float f2 = (float)(p.feas_len * p.feas_len);
-        // float errors: direction of v and (ca, sa) < 1e-6 rad, dot^2 / vv and vv relative < 1e-6
-        const bool yes = dot > 0.f && dot * dot >= (0.5f + 1e-5f) * vv && vv >= f2 * (1.f + 1e-5f);
-        const bool no = dot < 0.f || dot * dot < (0.5f - 1e-5f) * vv || vv < f2 * (1.f - 1e-5f);
-        c = yes;
-        if (!yes && !no) {
-          // within the float error of a limit: feasibleNode in double.  Lref exactly as the
-          // reference forms it (pow(d, 2) = d * d rounded once, IEEE sqrt); the angle test
-          // |angleDiff(atan2(v), angPar)| <= pi/4 as dot >= |cross| against (cos, sin)(angPar)
-          // (agrees with the reference's atan2 / fmod evaluation outside a ~1e-15 rad band)
-          const double dx = sx - r.bx, dy = sy - r.by;
-          const double Lref = sqrt((r.bx - sx) * (r.bx - sx) + (r.by - sy) * (r.by - sy));
-          const double2 tr = TRIG[j];
-          const double dd = dx * tr.x + dy * tr.y, cr = dy * tr.x - dx * tr.y;
-          c = (dd >= fabs(cr)) && !(Lref < p.feas_len);
-        }
+        // feasibleNode in float, exactly as the reference within the float error of a limit
+        c = feasible_walk(sx, sy, r.bx, r.by, r.ca, r.sa, r.ang_par, p.feas_len);
       }
     }
     // remember the key of the queued record deepest inside a run of equal records (the longest runs,
@@ -1139,7 +1118,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   w.sorted_y0 = y0;
   w.sorted_scale = scale;
   hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 255) / 256), dim3(256), 0, st, nodes, N, Npad, w.sids, fr.ox, fr.oy,
-                     w.P, w.Q, w.CE, w.ID, w.vals, w.TRIG);
+                     w.P, w.Q, w.CE, w.ID, w.vals);
   LAUNCH_CHECK3();
   // HEAD[j] = first record of j's run of equal key inputs (inclusive max-scan of dup markers)
   {
@@ -1196,11 +1175,11 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   if (state)
     hipLaunchKernelGGL((k_walk_search<true, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q,
                        w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder,
-                       w.TRIG, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
+                       stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   else
     hipLaunchKernelGGL((k_walk_search<false, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P,
                        w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,
-                       w.sorder, w.TRIG, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
+                       w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   LAUNCH_CHECK3();
   if (split) {
     // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
@@ -1208,7 +1187,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
     const int nl = (nsup + w.nch - 1) / w.nch;
     hipLaunchKernelGGL((k_walk_search<true, true>), dim3(w.max_over * w.nch), dim3(64), 2 * sizeof(float) * (size_t)nl,
                        st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
-                       ckey, ncand, ctie, w.sorder, w.TRIG, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
+                       ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
                        nl);
     LAUNCH_CHECK3();
     hipLaunchKernelGGL(k_walk_merge, dim3(w.max_over), dim3(64), 0, st, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,

@@ -331,13 +331,37 @@ int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const doubl
  *   CLRRT_UNIT_PROFILE  ax, ay, sx, sy, ref_res, v0, vmax, goal[4], GB -> N, v[NMAX], x[NMAX], y[NMAX] of
  *                       getReference's line (reference.cpp:13-18) and generateVelocityProfile
  *                       (reference.cpp:73-170)  [12 -> 1 + 3 * CLRRT_UNIT_PROFILE_NMAX]
- *   CLRRT_UNIT_ANGLE    a, b -> angleDiff(a, b), wrapToPi(a) (functions.h:43-57)  [2 -> 2] */
+ *   CLRRT_UNIT_ANGLE    a, b -> angleDiff(a, b), wrapToPi(a) (functions.h:43-57)  [2 -> 2]
+ * The units below take the goal / vmax / ref_res of each case (the rest of the context's params):
+ *   CLRRT_UNIT_DUBINS   sx, sy, node x, y, heading, costE -> the explore key dubinsDistance (float) and
+ *                       the optimize key costE + dubinsDistance (rrtplanner.cpp:231,254,371-406) as the
+ *                       nearest-node kernels evaluate them  [6 -> 2]
+ *   CLRRT_UNIT_FEASIBLE sx, sy, node ref front x, y, ref back x, y, ref_res -> feasibleNode
+ *                       (rrtplanner.cpp:271-289) as the brute-force search decides it, as the walk search
+ *                       decides it, and 1 when the search prefilter lets the node through  [7 -> 3]
+ *   CLRRT_UNIT_GOALBIAS goal[4], node x, y, ref back x, y -> feasibleGoalBias (rrtplanner.cpp:292-315)
+ *                       [8 -> 1]
+ *   CLRRT_UNIT_GOALREF  goal[4], parent ref back x, y, v0, ref_res -> N, v, x, y of getGoalReference
+ *                       (reference.cpp:25-70) + generateVelocityProfile(GB) (:72-170)
+ *                       [8 -> 1 + 3 * CLRRT_UNIT_PROFILE_NMAX]
+ *   CLRRT_UNIT_CTRL     kind (0: getReference from (a0, a1) to (a2, a3); 1: getGoalReference from ref back
+ *                       (a0, a1)), a0..a3, goal[4], Vstart, vmax, ref_res, then CLRRT_UNIT_CTRL_K states
+ *                       (x, y, heading, delta, v, a) -> the Controller of a Simulation (simulation.cpp:39-43,
+ *                       controller.cpp:23-113): IDwp, endreached, Ppreview x, y after the constructor, then per
+ *                       state getControls' IDwp, endreached, Ppreview x, y, ym, dc, ac, iE
+ *                       [12 + 6 K -> 4 + 8 K] */
 #define CLRRT_UNIT_OBB 0
 #define CLRRT_UNIT_ODE 1
 #define CLRRT_UNIT_LATERAL 2
 #define CLRRT_UNIT_PROFILE 3
 #define CLRRT_UNIT_ANGLE 4
+#define CLRRT_UNIT_DUBINS 5
+#define CLRRT_UNIT_FEASIBLE 6
+#define CLRRT_UNIT_GOALBIAS 7
+#define CLRRT_UNIT_GOALREF 8
+#define CLRRT_UNIT_CTRL 9
 #define CLRRT_UNIT_PROFILE_NMAX 1024
+#define CLRRT_UNIT_CTRL_K 24
 int clrrt_selftest_units(clrrt_ctx* ctx, int32_t unit, const double* in, int32_t n, double* out);
 
 int clrrt_get_counters(clrrt_ctx* ctx, clrrt_counters* out);

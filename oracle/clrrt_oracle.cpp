@@ -1006,6 +1006,110 @@ void orc_unit_angle(int n, const double* in, double* out) {
     out[2 * k + 1] = wrap_pi(in[2 * k]);
   }
 }
+// dubinsDistance (explore key) and costE + dubinsDistance (optimize key).
+// in: sx, sy, node x, y, heading, costE.
+void orc_unit_dubins(int n, const double* in, double* out) {
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 6 * k;
+    Pt s; s.x = a[0]; s.y = a[1];
+    Node nd;
+    nd.state.assign(10, 0.0);
+    nd.state[0] = a[2]; nd.state[1] = a[3]; nd.state[2] = a[4];
+    nd.costE = (float)a[5];
+    const float key = dubins(s, nd, 1);
+    out[2 * k] = key;
+    out[2 * k + 1] = (float)(nd.costE + key);
+  }
+}
+// feasibleNode.  in: sx, sy, ref front x, y, ref back x, y, ref_res.
+void orc_unit_feasible(void* h, int n, const double* in, double* out) {
+  Oracle o = *(Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 7 * k;
+    o.p.ref_res = a[6];
+    Pt s; s.x = a[0]; s.y = a[1];
+    Node nd;
+    nd.ref.x = {a[2], a[4]};
+    nd.ref.y = {a[3], a[5]};
+    out[k] = feasible_node(o, nd, s) ? 1.0 : 0.0;
+  }
+}
+// feasibleGoalBias of a new node.  in: goal[4], node x, y, ref back x, y.
+void orc_unit_goal_bias(void* h, int n, const double* in, double* out) {
+  Oracle o = *(Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 8 * k;
+    for (int i = 0; i < 4; i++) o.p.goal[i] = a[i];
+    Node nd;
+    nd.state.assign(10, 0.0);
+    nd.state[0] = a[4]; nd.state[1] = a[5];
+    nd.ref.x = {a[6]};
+    nd.ref.y = {a[7]};
+    out[k] = feasible_goal_bias(o, nd) ? 1.0 : 0.0;
+  }
+}
+// getGoalReference + the goal-biased velocity profile.  in: goal[4], parent ref back x, y, v0, ref_res;
+// out row (1 + 3 nmax): N, v, x, y.
+void orc_unit_goal_ref(void* h, int n, const double* in, int nmax, double* out) {
+  Oracle o = *(Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    const double* a = in + 8 * k;
+    vector<double> g(a, a + 4);
+    for (int i = 0; i < 4; i++) o.p.goal[i] = a[i];
+    o.p.ref_res = a[7];
+    Node par;
+    par.ref.x = {a[4]};
+    par.ref.y = {a[5]};
+    Ref r = get_goal_reference(o, par, g);
+    velocity_profile(o, r, a[6], o.p.vmax, g, true);
+    double* row = out + (size_t)(1 + 3 * nmax) * k;
+    row[0] = (double)r.x.size();
+    for (size_t i = 0; i < r.x.size() && (int)i < nmax; i++) {
+      row[1 + i] = at0(r.v, (long)i);
+      row[1 + nmax + i] = r.x[i];
+      row[1 + 2 * nmax + i] = r.y[i];
+    }
+  }
+}
+// The Controller of a Simulation over a state sequence (CLRRT_UNIT_CTRL layout, include/clrrt.h).
+void orc_unit_ctrl(void* h, int n, const double* in, int K, double* out) {
+  Oracle o = *(Oracle*)h;
+  for (int k = 0; k < n; k++) {
+    const double* a = in + (size_t)(12 + 6 * K) * k;
+    double* w = out + (size_t)(4 + 8 * K) * k;
+    for (int i = 0; i < 4; i++) o.p.goal[i] = a[5 + i];
+    o.p.vmax = a[10];
+    o.p.ref_res = a[11];
+    vector<double> g(a + 5, a + 9);
+    const bool GB = a[0] != 0;
+    Node par;
+    par.ref.x = {a[1]};
+    par.ref.y = {a[2]};
+    Ref r;
+    if (GB) {
+      r = get_goal_reference(o, par, g);
+    } else {
+      Pt s; s.x = a[3]; s.y = a[4];
+      r = get_reference(o, s, par, 1);
+    }
+    const double* st = a + 12;
+    Row x0(st, st + 6);
+    x0.resize(10, 0.0);
+    Ctrl c(o, r, x0);
+    w[0] = c.IDwp; w[1] = c.endreached; w[2] = c.P.x; w[3] = c.P.y;
+    velocity_profile(o, r, a[9], o.p.vmax, g, GB);
+    for (int j = 0; j < K; j++) {
+      Row x(st + 6 * j, st + 6 * j + 6);
+      x.resize(10, 0.0);
+      c.update_waypoint(o, r, x);
+      const double dc = c.steer(o, r, x);
+      const double ac = c.accel(o, r, x);
+      double* q = w + 4 + 8 * j;
+      q[0] = c.IDwp; q[1] = c.endreached; q[2] = c.P.x; q[3] = c.P.y;
+      q[4] = c.ym; q[5] = dc; q[6] = ac; q[7] = c.iE;
+    }
+  }
+}
 
 }  // extern "C"
 

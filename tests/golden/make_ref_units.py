@@ -21,8 +21,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
 import ref_units as R  # noqa: E402
 
-FIX_N = {"obb": 2048, "geom": 1024, "ode": 2048, "lateral": 2048, "profile": 160, "angle": 2048}
-LIVE_N = {"obb": 100000, "geom": 100000, "ode": 100000, "lateral": 100000, "profile": 20000, "angle": 100000}
+FIX_N = {"obb": 2048, "geom": 1024, "ode": 2048, "lateral": 2048, "profile": 160, "angle": 2048,
+         "dubins": 4096, "feasible": 4096, "goalbias": 4096, "goalref": 160, "ctrl": 384}
+LIVE_N = {"obb": 100000, "geom": 100000, "ode": 100000, "lateral": 100000, "profile": 20000, "angle": 100000,
+          "dubins": 100000, "feasible": 100000, "goalbias": 100000, "goalref": 20000, "ctrl": 10000}
 FIX_SEED, LIVE_SEED = 20261016, 7
 
 
@@ -65,12 +67,12 @@ def main():
         y = R.run_reference(ref, unit, x)
         if unit == "ode":
             y = y[0]
-        if unit == "profile":
+        if unit in ("profile", "goalref"):
             nmax = int(y[:, 0].max())
             assert nmax <= R.NMAX
             y = np.concatenate([y[:, :1 + nmax], y[:, 1 + R.NMAX:1 + R.NMAX + nmax],
                                 y[:, 1 + 2 * R.NMAX:1 + 2 * R.NMAX + nmax]], 1)
-            meta["profile_nmax"] = nmax
+            meta[f"{unit}_nmax"] = nmax
         arrays[f"{unit}_in"] = x
         arrays[f"{unit}_out"] = y
     arrays["prius"] = R.reference_prius(ref)

@@ -30,6 +30,7 @@ FUNCS = {
     "__sin_fma": (0x789B0, 0x791C0),
     "__cos_fma": (0x791C0, 0x799D0),
     "__tan_fma": (0x799D0, 0x7A250),
+    "__ieee754_atan2_fma": (0x78060, 0x789B0),
 }
 CONSTS = {
     # s_sin.c / usncs.h
@@ -42,6 +43,15 @@ CONSTS = {
     "d3": 0x96608, "d5": 0x9C068, "d7": 0x9C060, "d9": 0x9C058, "d11": 0x9C050,
     "e0": 0x9C088, "e1": 0x9C080, "two8": 0x96610, "mfftnhf": 0xC2D00,
 }
+# e_atan2.c / atnat2.h (IBM Accurate Mathematical Library) as its FMA variant loads them
+ATAN2_CONSTS = {
+    "at_hpi": 0x93048, "at_mhpi": 0x93040, "at_opi": 0x930C0, "at_mopi": 0x96598, "at_qpi": 0x965A0,
+    "at_mqpi": 0x965A8, "at_tqpi": 0x965B0, "at_mtqpi": 0x965B8, "at_hpi1": 0x930B8, "at_opi1": 0x96618,
+    "at_twom500": 0x965C0, "at_two500": 0x965C8, "at_inv16": 0x965D8, "at_twom1022": 0x93050,
+    "at_d3": 0xB8BA8, "at_d5": 0x96600, "at_d7": 0xB8BA0, "at_d9": 0x965F0, "at_d11": 0xB8B98, "at_d13": 0x965E0,
+    "at_two52": 0x8A2F0, "at_two8": 0x96610,
+}
+ATAN2_CIJ = (0xBE0E0, 241)  # cij[241][7] (uatan2.tbl)
 SINCOSTAB = (0xAEB80, 440)
 XFG = (0xC15C0, 186)
 # sysdeps/ieee754/flt-32 (sincosf.h, sincosf_data.c): __sincosf_table[2] (sign[4], hpi_inv, hpi, c0, c1,
@@ -162,10 +172,21 @@ def main():
     sctab = [dbl(b, SINCOSF_TABLE[0] + 8 * i) for i in range(SINCOSF_TABLE[1])]
     inv = list(struct.unpack_from(f"<{INV_PIO4[1]}I", b, INV_PIO4[0]))
     check_sincosf(sctab, inv)
+    at = {n: dbl(b, a) for n, a in ATAN2_CONSTS.items()}
+    if at["at_hpi"] != math.pi / 2 or at["at_opi"] != math.pi or at["at_qpi"] != math.pi / 4 or \
+            at["at_inv16"] != 1.0 / 16 or at["at_two52"] != 2.0 ** 52 or at["at_two8"] != 256.0:
+        sys.exit("atan2 constants")
+    cij = [dbl(b, ATAN2_CIJ[0] + 8 * i) for i in range(7 * ATAN2_CIJ[1])]
+    for i in range(ATAN2_CIJ[1]):
+        x, t1, t2 = cij[7 * i:7 * i + 3]
+        # x_i on the 1/256 grid (+- a little), atan(x_i) and 1/(1 + x_i^2) to double precision
+        if not (abs(x * 256 - (i + 16)) <= 0.5 and abs(t1 - math.atan(x)) <= 2 * abs(t1) * 2.0 ** -52
+                and abs(t2 - 1 / (1 + x * x)) <= 4 * t2 * 2.0 ** -52):
+            sys.exit(f"atan2 cij row {i}: {cij[7 * i:7 * i + 7]}")
     lines = [
         "// clrrt_glibc_data.hpp — GENERATED by tools/gen_glibc_libm.py; do not edit.",
-        "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c) and tan (s_tan.c) as loaded by",
-        "// its FMA variants, read from the libm image the CPU oracle links (hash-checked);",
+        "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c), tan (s_tan.c) and atan2 (e_atan2.c)",
+        "// as loaded by its FMA variants, read from the libm image the CPU oracle links (hash-checked);",
         "// __sincostab cross-checked against 60-digit sin/cos(k/128).",
         "#pragma once",
         "namespace clrrt { namespace glibc {",
@@ -187,6 +208,14 @@ def main():
     for i in range(0, len(sctab), 7):
         lines.append("  " + ", ".join(hexf(v) for v in sctab[i:i + 7]) + ", \\")
     lines.append("}")
+    lines.append("// double atan2 (dbl-64/e_atan2.c): constants and cij[241][7] (uatan2.tbl)")
+    for n, v in at.items():
+        lines.append(f"constexpr double {n} = {hexf(v)};")
+    lines.append(f"constexpr int ATAN2_CIJ_ROWS = {ATAN2_CIJ[1]};")
+    lines.append("#define CLRRT_GLIBC_ATAN2_CIJ { \\")
+    for i in range(0, len(cij), 7):
+        lines.append("  " + ", ".join(hexf(v) for v in cij[i:i + 7]) + ", \\")
+    lines.append("}")
     lines.append("#define CLRRT_GLIBC_INV_PIO4 { \\")
     for i in range(0, len(inv), 8):
         lines.append("  " + ", ".join(f"{v:#010x}u" for v in inv[i:i + 8]) + ", \\")
@@ -200,6 +229,7 @@ EXPECTED = {
     "__sin_fma": "aabda6ef77abfc7c2712b8c7f84622b16deb450fa5357c65d42ca1a31b5404f6",
     "__cos_fma": "e178beb9f63a803e0b2567f4d7dd94d3b850f8bf76d5076ad7f294f136bb5f4b",
     "__tan_fma": "c7575a60b74f0488aaa4875ed6aee7c04c2b8f6a1544ac6f6e8d4589d195145c",
+    "__ieee754_atan2_fma": "7ed0818283517f6aeaf62cc86d32503c62371b8404feefa6fd69f5e76fd92eb6",
 }
 
 if __name__ == "__main__":
