@@ -57,6 +57,8 @@ _SIGS = {
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "clrrt_round_prefetch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32]),
+    "clrrt_simulate": (C.c_int, [C.c_void_p, P(abi.SimCase), C.c_int32, P(abi.RolloutResult), P(C.c_double),
+                                 C.c_int32, P(C.c_double), C.c_int32]),
     "clrrt_rollout_batch": (C.c_int, [C.c_void_p, P(abi.RolloutJob), C.c_int32, P(abi.RolloutResult),
                                       P(C.c_double), C.c_int32]),
     "clrrt_nn_batch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_int32, P(C.c_int32), P(C.c_float)]),
@@ -347,6 +349,31 @@ class Planner:
             if rows:
                 d["rows"] = buf[i, :o.nrows].copy()
             res.append(d)
+        return res
+
+    def simulate(self, cases, ref_cap=1024):
+        """Simulation::Simulation for explicit cases (clrrt_simulate): cases = list of (state[10], ax, ay,
+        hx, hy, ref_n, goal_biased, vstart).  Returns result dicts with rows and the reference (x, y, v)."""
+        n = len(cases)
+        arr = (abi.SimCase * n)()
+        for i, (st, ax, ay, hx, hy, rn, gb, vs) in enumerate(cases):
+            for k in range(10):
+                arr[i].state[k] = st[k]
+            arr[i].ax, arr[i].ay, arr[i].hx, arr[i].hy, arr[i].vstart = ax, ay, hx, hy, vs
+            arr[i].ref_n, arr[i].goal_biased = rn, gb
+        out = (abi.RolloutResult * n)()
+        cap = 1100
+        rows = np.zeros((n, cap, 10))
+        ref = np.zeros((n, 3, ref_cap))
+        self._chk(self.L.clrrt_simulate(self.h, arr, n, out, rows.ctypes.data_as(P(C.c_double)), cap,
+                                        ref.ctypes.data_as(P(C.c_double)), ref_cap), "simulate")
+        res = []
+        for i in range(n):
+            o = out[i]
+            m = min(o.ref_n, ref_cap)
+            res.append({"outcome": o.outcome, "nrows": o.nrows, "costE": o.costE, "costS": o.costS,
+                        "final": np.array(o.final_state[:]), "ref_n": o.ref_n, "rows": rows[i, :o.nrows].copy(),
+                        "ref_x": ref[i, 0, :m].copy(), "ref_y": ref[i, 1, :m].copy(), "ref_v": ref[i, 2, :m].copy()})
         return res
 
     def sort_nodes_batch(self, samples, exact=True):

@@ -5,7 +5,7 @@ header documents so a drift between the two fails at import time.
 """
 import ctypes as C
 
-CLRRT_ABI_VERSION = 6  # include/clrrt.h
+CLRRT_ABI_VERSION = 7  # include/clrrt.h
 UNIT_OBB, UNIT_ODE, UNIT_LATERAL, UNIT_PROFILE, UNIT_ANGLE = 0, 1, 2, 3, 4  # CLRRT_UNIT_*
 UNIT_DUBINS, UNIT_FEASIBLE, UNIT_GOALBIAS, UNIT_GOALREF, UNIT_CTRL = 5, 6, 7, 8, 9
 UNIT_PROFILE_NMAX = 1024
@@ -76,6 +76,11 @@ class Stats(C.Structure):
 class Capacity(C.Structure):
     _fields_ = [("max_nodes", C.c_int64), ("max_rows", C.c_int64), ("max_batch", C.c_int32),
                 ("max_obstacles", C.c_int32)]
+
+
+class SimCase(C.Structure):
+    _fields_ = [("state", C.c_double * 10), ("ax", C.c_double), ("ay", C.c_double), ("hx", C.c_double),
+                ("hy", C.c_double), ("vstart", C.c_double), ("ref_n", C.c_int32), ("goal_biased", C.c_int32)]
 
 
 class RolloutJob(C.Structure):

@@ -1876,6 +1876,70 @@ int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, 
   return CLRRT_OK;
 }
 
+int clrrt_simulate(clrrt_ctx* c, const clrrt_sim_case* cases, int32_t n, clrrt_rollout_result* out, double* rows_out,
+                   int32_t rows_cap, double* ref_out, int32_t ref_cap) {
+  if (!c || n < 0 || (n > 0 && (!cases || !out)) || (ref_out && ref_cap <= 0)) return CLRRT_EINVAL;
+  pf_reset(c);
+  if (rows_out && rows_cap < c->dp.n_steps_max + 1) return fail(c, CLRRT_EINVAL, "rows_cap < max steps + 1");
+  for (int j = 0; j < n; j++)
+    if (!cases[j].goal_biased && cases[j].ref_n < 1) return fail(c, CLRRT_EINVAL, "ref_n < 1");
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  std::vector<SimJob> hj(n);
+  for (int j = 0; j < n; j++) {
+    const clrrt_sim_case& q = cases[j];
+    SimJob& s = hj[j];
+    for (int k = 0; k < 10; k++) s.st[k] = q.state[k];
+    s.ax = q.ax; s.ay = q.ay; s.hx = q.hx; s.hy = q.hy; s.vstart = q.vstart;
+    s.n = q.ref_n; s.gb = q.goal_biased ? 1 : 0;
+    s.row_off = rows_out ? (int64_t)j * rows_cap : -1;
+    s.ref_off = ref_out ? (int64_t)j * 3 * ref_cap : -1;
+  }
+  SimJob* dj = nullptr;
+  RollRes* dr = nullptr;
+  double *drows = nullptr, *dref = nullptr;
+  hipError_t e = hipMalloc((void**)&dj, sizeof(SimJob) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&dr, sizeof(RollRes) * n);
+  if (e == hipSuccess && rows_out) e = hipMalloc((void**)&drows, sizeof(double) * 10 * (size_t)rows_cap * n);
+  if (e == hipSuccess && ref_out) e = hipMalloc((void**)&dref, sizeof(double) * 3 * (size_t)ref_cap * n);
+  if (e == hipSuccess) e = hipMemcpyAsync(dj, hj.data(), sizeof(SimJob) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    RollArgs a = roll_args(c, n);
+    a.sims = dj;
+    a.arena = drows;
+    a.refv = dref;
+    a.ref_cap = ref_cap;
+    a.res = dr;
+    KTimer kt(c, 1);
+    e = launch_rollout(c->stream, SRC_EXPL, a);
+  }
+  std::vector<RollRes> hr(n);
+  if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), dr, sizeof(RollRes) * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && rows_out)
+    e = hipMemcpyAsync(rows_out, drows, sizeof(double) * 10 * (size_t)rows_cap * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && ref_out)
+    e = hipMemcpyAsync(ref_out, dref, sizeof(double) * 3 * (size_t)ref_cap * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(dj);
+  hipFree(dr);
+  if (drows) hipFree(drows);
+  if (dref) hipFree(dref);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("simulate: ") + hipGetErrorString(e));
+  for (int j = 0; j < n; j++) {
+    clrrt_rollout_result& o = out[j];
+    memset(&o, 0, sizeof(o));
+    o.outcome = hr[j].outcome;
+    o.nrows = hr[j].nrows;
+    o.costE = hr[j].costE;
+    o.costS = hr[j].costS;
+    for (int k = 0; k < 10; k++) o.final_state[k] = hr[j].st[k];
+    o.ref_back[0] = hr[j].bx; o.ref_back[1] = hr[j].by;
+    o.ref_vback = hr[j].vback;
+    o.ref_n = hr[j].refN;
+  }
+  return CLRRT_OK;
+}
+
 int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double* b, int32_t n, double* out) {
   if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 19) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));

@@ -56,7 +56,19 @@ struct SampleOut {
 //   SRC_SPEC : job j -> (sample s = j / K, candidate k = j % K), parent = tree node cand[s][k];
 //              a successful regular rollout is followed in the same lane by the goal-biased one
 //   SRC_LIST : explicit Job records (parity entry), parent = tree node
-enum { SRC_SPEC = 0, SRC_LIST = 2 };
+//   SRC_EXPL : explicit SimJob records (clrrt_simulate): parent state, reference generator and Vstart
+//              given directly; rows to arena[row_off], the reference (x, y, v) to refv[ref_off]
+enum { SRC_SPEC = 0, SRC_LIST = 2, SRC_EXPL = 3 };
+
+// Simulation::Simulation for an explicit state and reference (clrrt_simulate): gb = 0: the n points
+// a + i h (accumulated, getReference's LinearSpacedVector); gb = 1: getGoalReference from a.
+struct SimJob {
+  double st[10];
+  double ax, ay, hx, hy, vstart;
+  int32_t n, gb;
+  int64_t row_off;  // >= 0: stateArray rows at arena[row_off * 10 ...]
+  int64_t ref_off;  // >= 0: x[ref_cap], y[ref_cap], v[ref_cap] at refv[ref_off ...]
+};
 
 // Uniform grid over the static obstacles (built on the host by clrrt_set_obstacles): cell
 // (gx, gy) lists, ascending, every static obstacle whose inflated bounding circle (radius + vehicle
@@ -76,6 +88,9 @@ struct RollArgs {
   const clrrt_sample* __restrict__ samples;
   const int* __restrict__ cand;            // [B][K]
   const Job* __restrict__ jobs;
+  const SimJob* __restrict__ sims;         // SRC_EXPL
+  double* __restrict__ refv;               // SRC_EXPL: generated references
+  int ref_cap;
   const BakedObs* __restrict__ obs;
   double* __restrict__ arena;              // rows destination (LIST with row_off >= 0)
   double* __restrict__ slots;              // SPEC rows, see k_rollout (job-major, rows contiguous)

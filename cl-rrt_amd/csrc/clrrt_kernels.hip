@@ -898,16 +898,16 @@ __device__ __forceinline__ void finish_rollout(const Roll& r, double c7, double 
   out.refN = r.R.N;
 }
 
-// One whole rollout.  `ps` = parent state (10 doubles), (pbx, pby) = parent ref.back(),
-// pvb = parent ref.v.back().  rows (nullable) receives stateArray: element k of row i at
-// rows[(i * 10 + k) * es].
+// One whole rollout from parent state `ps` along reference R (ref.v generated from pvb = Vstart).  rows
+// (nullable) receives stateArray: element k of row i at rows[(i * 10 + k) * es].  init (nullable)
+// receives the Simulation state after its constructor (reference end and velocity profile).
 template <bool NEED_GAP>
-__device__ __forceinline__ void run_rollout(const St10& ps, double pbx, double pby, double pvb, int gb, double sx,
-                            double sy, const DevParams& p, const ObsView& ov, double* __restrict__ rows,
-                            int64_t es, RollRes& out, WorkCtr& w) {
-  RefD R = gb ? make_goal_ref(pbx, pby, p) : make_ref(pbx, pby, sx, sy, p);
+__device__ __forceinline__ void run_rollout_ref(const St10& ps, const RefD& R, double pvb, int gb, const DevParams& p,
+                                                const ObsView& ov, double* __restrict__ rows, int64_t es,
+                                                RollRes& out, WorkCtr& w, Roll* init = nullptr) {
   Roll r;
   roll_init(r, ps.v, R, pvb, gb != 0, p);
+  if (init) *init = r;
   double c7 = (double)r.wp, c8 = ps.v[8], c9 = ps.v[9];
   if (rows) {
 #pragma unroll
@@ -924,6 +924,16 @@ __device__ __forceinline__ void run_rollout(const St10& ps, double pbx, double p
   }
   finish_rollout(r, c7, c8, c9, outcome, steps, out);
   w.steps += (uint32_t)steps;
+}
+
+// One whole rollout of expandTree: toward (sx, sy) (getReference) or the goal (getGoalReference) from a
+// parent whose ref.back() is (pbx, pby) and ref.v.back() is pvb.
+template <bool NEED_GAP>
+__device__ __forceinline__ void run_rollout(const St10& ps, double pbx, double pby, double pvb, int gb, double sx,
+                            double sy, const DevParams& p, const ObsView& ov, double* __restrict__ rows,
+                            int64_t es, RollRes& out, WorkCtr& w) {
+  const RefD R = gb ? make_goal_ref(pbx, pby, p) : make_ref(pbx, pby, sx, sy, p);
+  run_rollout_ref<NEED_GAP>(ps, R, pvb, gb, p, ov, rows, es, out, w);
 }
 
 
@@ -1008,7 +1018,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   const int64_t pass_stride = slot * a.slot_jobs;
   if (act) {
     const clrrt_node* n = nullptr;
-    if (SRC == SRC_SPEC) {
+    if (SRC == SRC_EXPL) {
+      const SimJob& sj = a.sims[j];
+      RefD R;
+      if (sj.gb) {
+        R = make_goal_ref(sj.ax, sj.ay, a.p);
+      } else {
+        R.a1x = sj.ax; R.a1y = sj.ay; R.h1x = sj.hx; R.h1y = sj.hy;
+        R.a2x = R.a2y = R.h2x = R.h2y = 0.0;
+        R.n1 = sj.n; R.N = sj.n;
+        R.bx = sj.ax; R.by = sj.ay;
+      }
+#pragma unroll
+      for (int k = 0; k < 10; k++) ps.v[k] = sj.st[k];
+      RollRes out;
+      Roll ini;
+      run_rollout_ref<NEED_GAP>(ps, R, sj.vstart, sj.gb, a.p, ov, sj.row_off >= 0 ? a.arena + sj.row_off * 10 : nullptr,
+                                1, out, w, &ini);
+      a.res[j] = out;
+      if (sj.ref_off >= 0) {  // the reference the Simulation used, with the profile it generated
+        double* o = a.refv + sj.ref_off;
+        double x = ini.R.a1x, y = ini.R.a1y;
+        for (int i = 0; i < ini.R.N && i < a.ref_cap; i++) {
+          o[i] = x;
+          o[a.ref_cap + i] = y;
+          o[2 * a.ref_cap + i] = prof_v(ini.P, i);
+          ref_next(ini.R, i, x, y);
+        }
+      }
+      act = false;
+    } else if (SRC == SRC_SPEC) {
       const int id = a.cand[j];
       if (id < 0) {
         a.res[j].outcome = -1;
@@ -2496,6 +2535,7 @@ size_t rollout_prep_bytes() { return sizeof(RollInit); }
 
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
   if (src == SRC_SPEC) return launch_roll_t<SRC_SPEC>(st, a);
+  if (src == SRC_EXPL) return launch_roll_t<SRC_EXPL>(st, a);
   return launch_roll_t<SRC_LIST>(st, a);
 }
 

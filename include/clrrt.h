@@ -23,6 +23,8 @@
  *   clrrt_round_commit        Simulation) and its append half (RRT.addNode, rrtplanner.h:111-113), so the host
  *                             can all-gather accepted nodes across GPUs between the two halves
  *   clrrt_rollout_batch    <- Simulation::Simulation + propagate rrt/src/simulation.cpp:36-47,55-143
+ *   clrrt_simulate         <- Simulation::Simulation (rrt/include/rrt/simulation.h:18-19) for an explicit
+ *                             state and reference (the C++ Simulation adapter)
  *   clrrt_nn_batch         <- sortNodesExplore / sortNodesOptimize rrt/src/rrtplanner.cpp:227-268
  *   clrrt_get_counters     <- sim_count / fail_* globals rrt/src/rrt_node.cpp:21-24
  *
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 6
+#define CLRRT_ABI_VERSION 7
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -307,6 +309,23 @@ int clrrt_obstacle_distance(clrrt_ctx* ctx, const double* states, int32_t n, dou
 /* ---- kernel-level parity entries ---- */
 int clrrt_rollout_batch(clrrt_ctx* ctx, const clrrt_rollout_job* jobs, int32_t n,
                         clrrt_rollout_result* out, double* rows_out, int32_t rows_cap);
+/* Simulation::Simulation(RRT, state, ref, veh, GoalBiased, genProfile = true, Vstart) (simulation.h:18-19,
+ * simulation.cpp:36-143) for n explicit cases, evaluated by the rollout kernels' own code (the C++
+ * Simulation adapter, include/clrrt_adapter.hpp).  Per case: state (10 doubles), the reference as its
+ * generator -- goal_biased = 0: the ref_n points a + i h accumulated (getReference's LinearSpacedVector,
+ * functions.h:11-21); goal_biased = 1: getGoalReference (reference.cpp:25-70) from a with the context's goal
+ * (h, ref_n ignored) -- and Vstart.  Writes results[i], rows (min(nrows, rows_cap) of stateArray per case,
+ * rows_cap >= max steps + 1 or rows = NULL) and, with ref_out, the reference the Simulation used with the
+ * velocity profile it generated: x, y, v (3 x ref_cap doubles per case, first min(N, ref_cap) points). */
+typedef struct clrrt_sim_case {
+  double state[10];
+  double ax, ay, hx, hy;
+  double vstart;
+  int32_t ref_n;
+  int32_t goal_biased;
+} clrrt_sim_case;
+int clrrt_simulate(clrrt_ctx* ctx, const clrrt_sim_case* cases, int32_t n, clrrt_rollout_result* results,
+                   double* rows, int32_t rows_cap, double* ref_out, int32_t ref_cap);
 /* Candidate lists (<= sortLimit node ids per sample, ascending key).  mode CLRRT_MODE_EXACT orders
  * equal keys as the reference's std::sort does (replayed per tied sample, O(n * tree) scratch);
  * CLRRT_MODE_BATCH orders them by node index. */

@@ -10,6 +10,10 @@
  *   obstacle_to_c             car_msgs::Obstacle2D (old_collisioncheck.cpp:10-16 field use)
  *   Engine::expandTree        void expandTree(Vehicle&, MyRRT&, ros::Publisher*, const vector<Obstacle2D>&,
  *                             const vector<double>&)  (rrtplanner.h:87, rrtplanner.cpp:123-174)
+ *   Simulation                Simulation::Simulation(const MyRRT&, const vector<double>&, MyReference&,
+ *                             const Vehicle&, const bool&, const bool&, const double&)  (simulation.h:18-19)
+ *   dropin::expandTree /      the same with the reference's exact signatures, bound to one Engine
+ *   dropin::Simulation        (dropin::bind), for the unity build's call sites
  *   Engine::expandBudget      the Timer(200) loop of MotionPlanner::planMotion (motionplanner.cpp:39-43)
  *   Engine::checkObsDistance  double checkObsDistance(const vector<double>&)  (collision.h:41)
  *
@@ -17,8 +21,8 @@
  * ref.y = {front, back}, ref.v = {v.back()} — every field expandTree, feasibleNode, feasibleGoalBias,
  * getReference and Simulation read (rrtplanner.cpp:152,166,273-277,305).  Trajectories (Node::tra) are
  * complete.  The engine consumes the glibc rand() stream through its own restatement (clrrt_rng), so
- * `rng` must be seeded as the reference seeds rand(); Engine::expandTree advances the process's rand()
- * by the same three draws per iteration, keeping both streams equal.
+ * the engine's rng must be seeded as the reference seeds rand() (Engine::srand); Engine::expandTree
+ * advances the process's rand() by the same three draws per iteration, keeping both streams equal.
  */
 #pragma once
 #include <algorithm>
@@ -150,6 +154,8 @@ class Engine {
     o.reserve(det.size());
     for (const auto& d : det) o.push_back(obstacle_to_c(d));
     check(ctx_, clrrt_set_obstacles(ctx_, o.data(), (int32_t)o.size()), "clrrt_set_obstacles");
+    det_ = std::move(o);
+    det_set_ = true;
   }
 
   /* The device tree := RRT.tree (e.g. after MyRRT::addInitialNode or initializeTree). */
@@ -160,13 +166,51 @@ class Engine {
     for (const auto& n : rrt.tree) h.push_back(node_to_c(n));
     check(ctx_, clrrt_tree_load(ctx_, h.data(), (int64_t)h.size()), "clrrt_tree_load");
     synced_ = (int64_t)rrt.tree.size();
+    root_ = h.empty() ? clrrt_node{} : h.front();
+    last_ = h.empty() ? clrrt_node{} : h.back();
+  }
+  /* Forget the synced tree: the next expansion reloads RRT.tree (call after replacing RRT.tree by other
+   * means than expansion; a changed root or last synced node is also detected by itself). */
+  void invalidate() { synced_ = -1; }
+
+  /* The rand() stream (srand(seed) semantics) the expansion draws from; rng() for the explicit form. */
+  void srand(uint32_t seed) { clrrt_rng_seed(&rng_, seed); }
+  clrrt_rng& rng() { return rng_; }
+  /* The reference's failure counters (rrt_node.cpp:21-24) bumped as its expandTree bumps them, or null. */
+  void bind_counters(int* sim_count, int* fail_collision, int* fail_acclimit, int* fail_iterlimit) {
+    gc_[0] = sim_count; gc_[1] = fail_collision; gc_[2] = fail_acclimit; gc_[3] = fail_iterlimit;
+  }
+  const int64_t* counters() const { return counters_; }
+  /* One rollout's share of the counters (simulation.cpp:59,85,102,142): steps, then the failure it ended in. */
+  void count_rollout(int32_t outcome, int32_t steps) {
+    int64_t c[4] = {steps, outcome == CLRRT_ROLL_COLLISION, outcome == CLRRT_ROLL_ACCLIMIT,
+                    outcome == CLRRT_ROLL_ITERLIMIT};
+    for (int i = 0; i < 4; i++) {
+      counters_[i] += c[i];
+      if (gc_[i]) *gc_[i] += (int)c[i];
+    }
   }
 
-  /* expandTree: one iteration (exactly three rand() draws), appending 0-2 nodes to RRT.tree and
-   * bumping the reference's counters (sim_count, fail_*: rrt_node.cpp:21-24). */
+  /* expandTree (rrtplanner.h:87): one iteration (exactly three rand() draws of the engine's stream and of
+   * the process's), appending 0-2 nodes to RRT.tree, bumping the counters; the detections `det` are
+   * (re)loaded when they differ from the last ones loaded. */
+  template <class VehicleT, class RRTT, class PubT, class ObsVec>
+  void expandTree(VehicleT&, RRTT& RRT, PubT* /*ptrPub (unused)*/, const ObsVec& det,
+                  const std::vector<double>& /*Cxy (unused)*/) {
+    sync_obstacles(det);
+    int64_t c[4] = {0, 0, 0, 0};
+    run(RRT, rng_, 1, 0.0, CLRRT_MODE_EXACT, 16, c);
+    for (int i = 0; i < 3; i++) (void)rand();
+    for (int i = 0; i < 4; i++) {
+      counters_[i] += c[i];
+      if (gc_[i]) *gc_[i] += (int)c[i];
+    }
+  }
+  /* The same with an explicit stream and counter sink. */
   template <class VehicleT, class RRTT, class ObsVec>
-  void expandTree(VehicleT&, RRTT& rrt, void* /*ros::Publisher* (unused)*/, const ObsVec&,
+  void expandTree(VehicleT&, RRTT& rrt, void* /*ros::Publisher* (unused)*/, const ObsVec& det,
                   const std::vector<double>& /*Cxy (unused)*/, clrrt_rng& rng, int64_t counters[4]) {
+    sync_obstacles(det);
     run(rrt, rng, 1, 0.0, CLRRT_MODE_EXACT, 16, counters);
     for (int i = 0; i < 3; i++) (void)rand();
   }
@@ -189,10 +233,38 @@ class Engine {
   }
 
  private:
+  static bool same_node(const clrrt_node& a, const clrrt_node& b) {
+    for (int i = 0; i < 10; i++)
+      if (!(a.state[i] == b.state[i]) && !(a.state[i] != a.state[i] && b.state[i] != b.state[i])) return false;
+    return a.parent == b.parent && a.costE == b.costE && a.costS == b.costS && a.ref_back[0] == b.ref_back[0] &&
+           a.ref_back[1] == b.ref_back[1] && a.ref_front[0] == b.ref_front[0] && a.ref_front[1] == b.ref_front[1] &&
+           a.nrows == b.nrows;
+  }
+  /* RRT.tree is the synced tree plus nodes appended since?  (same length, same root, same last node) */
+  template <class RRTT>
+  bool tree_synced(const RRTT& rrt) const {
+    if (synced_ < 0 || (int64_t)rrt.tree.size() != synced_) return false;
+    if (synced_ == 0) return true;
+    return same_node(node_to_c(rrt.tree.front()), root_) && same_node(node_to_c(rrt.tree.back()), last_);
+  }
+  template <class ObsVec>
+  void sync_obstacles(const ObsVec& det) {
+    bool same = det_set_ && det_.size() == det.size();
+    if (same) {
+      size_t i = 0;
+      for (const auto& d : det) {
+        const clrrt_obstacle o = obstacle_to_c(d), &q = det_[i++];
+        if (o.cx != q.cx || o.cy != q.cy || o.theta != q.theta || o.size_x != q.size_x || o.size_y != q.size_y ||
+            o.vx != q.vx || o.vy != q.vy) { same = false; break; }
+      }
+    }
+    if (!same) set_obstacles(det);
+  }
+
   template <class RRTT>
   int64_t run(RRTT& rrt, clrrt_rng& rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
               int64_t counters[4]) {
-    if ((int64_t)rrt.tree.size() != synced_) load_tree(rrt);
+    if (!tree_synced(rrt)) load_tree(rrt);
     clrrt_counters c0, c1;
     check(ctx_, clrrt_get_counters(ctx_, &c0), "clrrt_get_counters");
     clrrt_stats st;
@@ -212,6 +284,10 @@ class Engine {
       }
     }
     synced_ = n;
+    if (!rrt.tree.empty()) {
+      root_ = node_to_c(rrt.tree.front());
+      last_ = node_to_c(rrt.tree.back());
+    }
     if (counters) {
       counters[0] += c1.sim_count - c0.sim_count;
       counters[1] += c1.fail_collision - c0.fail_collision;
@@ -222,8 +298,119 @@ class Engine {
   }
 
   clrrt_ctx* ctx_ = nullptr;
-  int64_t synced_ = 0;
+  int64_t synced_ = -1;  // nodes of RRT.tree the device holds (-1: unknown, reload)
+  clrrt_node root_{}, last_{};
+  clrrt_rng rng_{};
+  int64_t counters_[4] = {0, 0, 0, 0};
+  int* gc_[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<clrrt_obstacle> det_;
+  bool det_set_ = false;
 };
+
+/* The step h of a reference coordinate built by LinearSpacedVector (functions.h:11-21: val += h from v[0]):
+ * an h whose accumulation reproduces every value of v bit for bit (the device regenerates the reference
+ * by the same accumulation).  h = v[1] - v[0] is h rounded to the grid of v[0]; the true step lies within
+ * half an ulp of v[0] of it. */
+inline bool linspace_step(const std::vector<double>& v, double& h) {
+  const size_t N = v.size();
+  if (N < 2) { h = 0.0; return true; }
+  auto reproduces = [&](double c) {
+    double val = v[0];
+    for (size_t i = 0; i < N; i++, val += c)
+      if (!(val == v[i])) return false;
+    return true;
+  };
+  const double h0 = v[1] - v[0];
+  if (reproduces(h0)) { h = h0; return true; }
+  double up = h0, dn = h0;
+  const double span = std::fabs(std::nextafter(v[0], INFINITY) - v[0]) + std::fabs(h0) * 1e-15;
+  for (int k = 0; k < 1 << 14 && std::fabs(up - h0) <= span; k++) {
+    up = std::nextafter(up, INFINITY);
+    dn = std::nextafter(dn, -INFINITY);
+    if (reproduces(up)) { h = up; return true; }
+    if (reproduces(dn)) { h = dn; return true; }
+  }
+  return false;
+}
+
+/* Simulation (simulation.h:7-21): the constructor runs the closed-loop prediction on the device
+ * (clrrt_simulate, the rollout kernels' own code) and fills the members the reference fills: stateArray,
+ * costS, costE, goalReached, endReached, and ref.v (generateVelocityProfile, simulation.cpp:42-45).  The
+ * reference `ref` must be what getReference (a LinearSpacedVector line) or, with GoalBiased,
+ * getGoalReference produced -- the only references expandTree simulates; anything else throws.  The
+ * engine's params must be those of RRT (Engine::set_params(params_from(...))); genProfile = false (never
+ * used by the reference) throws.  The failure counters move as the reference's propagate moves them. */
+class Simulation {
+ public:
+  std::vector<std::vector<double>> stateArray;
+  std::vector<double> curvature;
+  std::vector<int> closestPoints;
+  std::vector<double> acmd, dcmd;
+  double costS = 0, costE = 0;
+  bool goalReached = false, endReached = false;
+  int32_t outcome = -1;  /* CLRRT_ROLL_* (the counter the reference bumps) */
+
+  template <class RRTT, class RefT, class VehicleT>
+  Simulation(Engine& eng, const RRTT& /*RRT (params)*/, const std::vector<double>& state, RefT& ref,
+             const VehicleT& /*veh (params)*/, const bool& GoalBiased, const bool& genProfile, const double& Vstart) {
+    if (!genProfile) throw Error("Simulation: genProfile = false is not supported (expandTree always passes true)");
+    if (ref.x.empty() || ref.x.size() != ref.y.size()) throw Error("Simulation: malformed reference");
+    clrrt_sim_case q{};
+    for (int i = 0; i < 10; i++) q.state[i] = i < (int)state.size() ? state[i] : 0.0;
+    q.ax = ref.x.front();
+    q.ay = ref.y.front();
+    q.vstart = Vstart;
+    q.goal_biased = GoalBiased ? 1 : 0;
+    q.ref_n = (int32_t)ref.x.size();
+    if (!GoalBiased && !(linspace_step(ref.x, q.hx) && linspace_step(ref.y, q.hy)))
+      throw Error("Simulation: the reference is not a getReference line");
+    const int32_t cap = (int32_t)std::max<size_t>(ref.x.size(), 1);
+    clrrt_rollout_result res;
+    std::vector<double> rows(10 * 1100), refo(3 * (size_t)cap);
+    check(eng.ctx(), clrrt_simulate(eng.ctx(), &q, 1, &res, rows.data(), 1100, refo.data(), cap), "clrrt_simulate");
+    if (res.ref_n != (int32_t)ref.x.size()) throw Error("Simulation: the reference is not the one getGoalReference builds");
+    for (int32_t i = 0; i < res.ref_n; i++)
+      if (!(refo[i] == ref.x[i]) || !(refo[cap + i] == ref.y[i]))
+        throw Error("Simulation: the reference is not the one getReference / getGoalReference builds");
+    ref.v.assign(refo.begin() + 2 * (size_t)cap, refo.begin() + 2 * (size_t)cap + res.ref_n);
+    stateArray.resize(res.nrows);
+    for (int32_t r = 0; r < res.nrows; r++) stateArray[r].assign(&rows[10 * (size_t)r], &rows[10 * (size_t)r] + 10);
+    costE = res.costE;
+    costS = res.costS;
+    outcome = res.outcome;
+    eng.count_rollout(res.outcome, res.nrows - 1);
+    endReached = res.outcome == CLRRT_ROLL_END;
+    goalReached = res.outcome == CLRRT_ROLL_GOAL;
+  }
+  bool isvalid() { return endReached; }  /* simulation.h:22-25 */
+};
+
+/* The reference's own signatures for its call sites, bound to one Engine:
+ *   clrrt_adapter::dropin::bind(engine);            once, after the engine is configured
+ *   expandTree(veh, RRT, pubPtr, det, Cxy);         rrtplanner.h:87 (motionplanner.cpp:41)
+ *   Simulation sim(RRT, state, ref, veh, GB, true, Vstart);   simulation.h:18-19 */
+namespace dropin {
+inline Engine*& bound() {
+  static Engine* e = nullptr;
+  return e;
+}
+inline void bind(Engine& e) { bound() = &e; }
+inline Engine& engine() {
+  if (!bound()) throw Error("clrrt_adapter::dropin: no Engine bound (dropin::bind)");
+  return *bound();
+}
+template <class VehicleT, class RRTT, class PubT, class ObsVec>
+void expandTree(VehicleT& veh, RRTT& RRT, PubT* ptrPub, const ObsVec& det, const std::vector<double>& Cxy) {
+  engine().expandTree(veh, RRT, ptrPub, det, Cxy);
+}
+class Simulation : public clrrt_adapter::Simulation {
+ public:
+  template <class RRTT, class RefT, class VehicleT>
+  Simulation(const RRTT& RRT, const std::vector<double>& state, RefT& ref, const VehicleT& veh, const bool& GoalBiased,
+             const bool& genProfile, const double& Vstart)
+      : clrrt_adapter::Simulation(engine(), RRT, state, ref, veh, GoalBiased, genProfile, Vstart) {}
+};
+}  // namespace dropin
 
 /* ---------------------------------------------------------------------------------------------
  * MotionPlanner::planMotion (motionplanner.cpp:8-77) without ROS.  The reference's callback reads

@@ -17,7 +17,7 @@ def _header_functions():
 
 def test_library_loads_and_exports_every_header_symbol():
     L = clrrt.lib()
-    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 6
+    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 7
     declared = _header_functions()
     assert len(declared) >= 25
     out = subprocess.run(["nm", "-D", "--defined-only", clrrt.LIB_PATH], capture_output=True, text=True).stdout
@@ -31,6 +31,7 @@ def test_abi_record_sizes_match_header():
     import ctypes as C
     assert C.sizeof(abi.Node) == 160
     assert C.sizeof(abi.Params) == 9 * 8 + 11 * 8 + 4 * 8 + 5 * 8 + 8 + 3 * 8 + 4 * 4
+    assert C.sizeof(abi.SimCase) == 15 * 8 + 2 * 4  # clrrt_sim_case
 
 
 def test_params_default_matches_reference_values():
