@@ -120,6 +120,7 @@ struct clrrt_ctx {
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
+  int roll_prio = 0;          // option "roll_prio": k_roll_run's wave issue priority (RollArgs::prio_mode)
   int roll_point_cache = 0;   // option "roll_point_cache": reference points in LDS (k_roll_run; off: see DESIGN §8)
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
@@ -1173,6 +1174,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_side_build") c->nn_side_build = value != 0;
   else if (k == "roll_handoff") c->roll_handoff = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
+  else if (k == "roll_prio" && value >= 0 && value <= 2) c->roll_prio = (int)value;
   else if (k == "roll_point_cache") c->roll_point_cache = value != 0;
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
@@ -1548,6 +1550,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.pflag = c->roll_pflag;
     }
     a.pcache_enable = c->roll_point_cache;
+    a.prio_mode = c->roll_prio;
     if (c->roll_persistent && c->dp.n_steps_max > 0)
       HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
     else

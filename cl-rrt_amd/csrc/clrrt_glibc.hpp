@@ -421,7 +421,7 @@ static __device__ __constant__ double d_atan2_cij[ATAN2_CIJ_ROWS * 7] = CLRRT_GL
 static const double h_atan2_cij[ATAN2_CIJ_ROWS * 7] = CLRRT_GLIBC_ATAN2_CIJ;
 
 // the cij row of u in [1/16, 1]: i = (TWO52 + TWO8 * u) - TWO52 (one rounding), minus 16
-CLRRT_HD inline const double* atan2_row(double u) {
+CLRRT_HD inline __attribute__((always_inline)) const double* atan2_row(double u) {
   const int i = (int)(fma_(u, at_two8, at_two52) - at_two52) - 16;
 #if defined(__HIP_DEVICE_COMPILE__)
   return d_atan2_cij + 7 * i;
@@ -430,7 +430,7 @@ CLRRT_HD inline const double* atan2_row(double u) {
 #endif
 }
 // d3 + v (d5 + v (d7 + v (d9 + v (d11 + v d13)))), contracted
-CLRRT_HD inline double atan2_poly(double v) {
+CLRRT_HD inline __attribute__((always_inline)) double atan2_poly(double v) {
   double p = fma_(v, at_d13, at_d11);
   p = fma_(v, p, at_d9);
   p = fma_(v, p, at_d7);
@@ -438,14 +438,14 @@ CLRRT_HD inline double atan2_poly(double v) {
   return fma_(v, p, at_d3);
 }
 // cij[2] + v (cij[3] + v (cij[4] + v (cij[5] + v cij[6]))), contracted
-CLRRT_HD inline double atan2_tpoly(const double* c, double v) {
+CLRRT_HD inline __attribute__((always_inline)) double atan2_tpoly(const double* c, double v) {
   double p = fma_(v, c[6], c[5]);
   p = fma_(v, p, c[4]);
   p = fma_(v, p, c[3]);
   return fma_(v, p, c[2]);
 }
 
-CLRRT_HD inline double atan2(double y, double x) {
+CLRRT_HD inline __attribute__((always_inline)) double atan2(double y, double x) {
   const uint32_t ux = hi_word(x), dx = (uint32_t)lo_word(x);
   const uint32_t uy = hi_word(y), dy = (uint32_t)lo_word(y);
   if ((ux & 0x7ff00000u) == 0x7ff00000u && ((ux & 0xfffffu) | dx) != 0) return x + y;  // x NaN

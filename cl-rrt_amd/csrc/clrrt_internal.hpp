@@ -115,6 +115,10 @@ struct RollArgs {
   int pcache_enable;  // option "roll_point_cache"
   int pcache_n;       // points per lane (0: off)
   int pcache_off;     // byte offset in the dynamic LDS
+  // k_roll_run's wave issue priority (option "roll_prio"): 0 default, 1 raised once the wave finds the
+  // job queue empty (the stragglers), 2 raised from the start.  A raised wave wins the SIMD's
+  // instruction-issue arbitration against the side stream's search waves that share its SIMD.
+  int prio_mode;
 };
 
 struct SelArgs {

@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       if (!ex) key = cost + key;
       if (!lex_less(key, n, keys[NN_K - 1], ids[NN_K - 1]) || key > kcap) continue;
       const NnRec& rec = nodes[b + k];
-      if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
+      if (feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len)) {
         topk_insert(keys, ids, key, n);
         if (seed && keys[NN_K - 1] < kcap) {
           kcap = keys[NN_K - 1];
@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(64) k_nn_delta_grid(const clrrt_sample* __rest
     if (!ex) key = cst + key;
     // (key, i) must precede the lane's 11th entry; a key at or above the seed cannot enter the merge
     if (!lex_less(key, i, keys[NN_K - 1], ids[NN_K - 1]) || !(key < kcap)) return;
-    if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) topk_insert(keys, ids, key, i);
+    if (feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len)) topk_insert(keys, ids, key, i);
   };
   const float4 gf = g.frame[0];
   const float gmin = ord_dec32(g.gmin[0]);
@@ -615,7 +615,7 @@ __global__ void k_nn_exact(const clrrt_sample* __restrict__ S, int B, const NnRe
   int cnt = 0;
   for (int i = 0; i < N && cnt < p.sort_limit; i++) {
     const NnRec& rec = nodes[a[i].id];
-    if (feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len)) {
+    if (feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len)) {
       cand[s * CAND_K + cnt] = a[i].id;
       ckey[s * CAND_K + cnt] = a[i].key;
       cnt++;
@@ -904,7 +904,8 @@ __device__ __forceinline__ void finish_rollout(const Roll& r, double c7, double 
 template <bool NEED_GAP>
 __device__ __forceinline__ void run_rollout_ref(const St10& ps, const RefD& R, double pvb, int gb, const DevParams& p,
                                                 const ObsView& ov, double* __restrict__ rows, int64_t es,
-                                                RollRes& out, WorkCtr& w, Roll* init = nullptr) {
+                                                RollRes& out, WorkCtr& w, Roll* init = nullptr,
+                                                PhaseClk* pc = nullptr) {
   Roll r;
   roll_init(r, ps.v, R, pvb, gb != 0, p);
   if (init) *init = r;
@@ -918,8 +919,10 @@ __device__ __forceinline__ void run_rollout_ref(const St10& ps, const RefD& R, d
   int steps = 0;
   for (int i = 0; i < p.n_steps_max; i++) {
     steps++;
-    int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9, w);
+    if (pc) pc->mark(0);
+    int o = roll_step<NEED_GAP>(r, p, ov, c7, c8, c9, w, pc);
     if (rows) store_row(rows + (int64_t)steps * 10 * es, es, r, c7, c8, c9);
+    if (pc) pc->mark(5);
     if (o >= 0) { outcome = o; break; }
   }
   finish_rollout(r, c7, c8, c9, outcome, steps, out);
@@ -1071,10 +1074,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       pbx = n->ref_back[0]; pby = n->ref_back[1]; pvb = n->ref_vback;
     }
   }
+#ifdef CLRRT_ROLL_PROFILE
+  PhaseClk pclk{};
+  pclk.last = __builtin_amdgcn_s_memtime();
+  PhaseClk* pc = &pclk;
+#else
+  PhaseClk* pc = nullptr;
+#endif
   if (act) {
     for (int pass = 0; pass < 2; pass++) {
       RollRes out;
-      run_rollout<NEED_GAP>(ps, pbx, pby, pvb, gb, sx, sy, a.p, ov, rows, es, out, w);
+      const RefD R = gb ? make_goal_ref(pbx, pby, a.p) : make_ref(pbx, pby, sx, sy, a.p);
+      run_rollout_ref<NEED_GAP>(ps, R, pvb, gb, a.p, ov, rows, es, out, w, nullptr, pc);
       if (pass == 1) {
         a.res_gb[j] = out;
         break;
@@ -1106,6 +1117,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     __syncthreads();
     if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
   }
+#ifdef CLRRT_ROLL_PROFILE
+  if (a.ctr && j < a.njobs)
+    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[32 + q], (unsigned long long)pclk.t[q]);
+#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1253,6 +1268,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   const bool absorber = !cont_on || (threadIdx.x >> 6) == 0;
   RollCont* __restrict__ cont = (RollCont*)a.cont;
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
+  bool raised = false;
+  if (a.prio_mode == 2) {
+    __builtin_amdgcn_s_setprio(3);
+    raised = true;
+  }
   int poll = 0;
   uint32_t idle_polls = 0;  // hand-off absorber: polls without work (spin limit)
   // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
@@ -1352,6 +1372,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           }
         }
         qdone = qdone || __ballot(exhausted) != 0;
+        if (qdone && !raised && a.prio_mode == 1) {
+          __builtin_amdgcn_s_setprio(3);
+          raised = true;
+        }
       }
       if (pc) pc->mark(6);
       continue;
@@ -2065,14 +2089,14 @@ __global__ void k_selftest_units(int unit, const double* __restrict__ in, const 
       d.ang_par = node_ang_par(a[4], a[5], a[2], a[3]);
       d.costE = 0.f;
       const NnRec r = nn_record(d, 0);
-      const bool brute = feasible_node(r.bx, r.by, r.ang_par, a[0], a[1], q.feas_len);
-      const bool walk = feasible_walk(a[0], a[1], r.bx, r.by, r.ca, r.sa, r.ang_par, q.feas_len);
+      const bool exact = feasible_node(r.bx, r.by, r.ang_par, a[0], a[1], q.feas_len);
+      const bool search = feasible_search(a[0], a[1], r.bx, r.by, r.ca, r.sa, r.ang_par, q.feas_len);
       const float qx = (float)(a[0] - r.x), qy = (float)(a[1] - r.y);
       const float feas2 = nn_feas2(q.feas_len);
       const bool pre = nn_prefilter(a[0], a[1], qx, qy, r.c, r.s, r.ca, r.sa, r.bx, r.by, 0.f, 1,
                                     __builtin_inff(), feas2);
-      out[3 * (int64_t)i] = brute ? 1.0 : 0.0;
-      out[3 * (int64_t)i + 1] = walk ? 1.0 : 0.0;
+      out[3 * (int64_t)i] = exact ? 1.0 : 0.0;
+      out[3 * (int64_t)i + 1] = search ? 1.0 : 0.0;
       out[3 * (int64_t)i + 2] = pre ? 1.0 : 0.0;
     } break;
     case CLRRT_UNIT_GOALBIAS: {
@@ -2282,7 +2306,7 @@ __global__ void __launch_bounds__(256) k_nn_seed(const clrrt_sample* __restrict_
     float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
     if (!ex) key = rec.costE + key;
     if (lex_less(key, rec.id, keys[NN_K - 1], ids[NN_K - 1]) &&
-        feasible_node(rec.bx, rec.by, rec.ang_par, sx, sy, p.feas_len))
+        feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len))
       topk_insert(keys, ids, key, rec.id);
   }
   ((unsigned int*)seed)[s] = ord_enc32(keys[NN_K - 1]);

@@ -261,7 +261,7 @@ __device__ __forceinline__ void scan_nodes(Lane& L, const NnRec* __restrict__ re
       float key = dubins_key(L.sx, L.sy, rec.x, rec.y, rec.c, rec.s);
       if (!L.ex) key = rec.costE + key;
       if (lex_less2(key, rec.id, L.keys[NN_K - 1], L.ids[NN_K - 1]) &&
-          feasible_node(rec.bx, rec.by, rec.ang_par, L.sx, L.sy, feas_len))
+          feasible_search(L.sx, L.sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, feas_len))
         topk_insert2(L.keys, L.ids, key, rec.id);
     }
   }

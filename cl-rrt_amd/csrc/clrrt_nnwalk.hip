@@ -541,7 +541,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   float kc = 0.f;    // ... and that key
   unsigned long long n_sup = 0, n_tile = 0, n_q = 0, n_ex = 0, n_und = 0, n_sure = 0, n_drop = 0;
 
-  auto refresh = [&]() {
+  auto refresh = [&]() __attribute__((always_inline)) {
     kth = uni(__shfl(lk, NN_K - 1, 64));
     idk = uni(__shfl(li, NN_K - 1, 64));
     if (SPLIT && w_less(kb, ib, kth, idk)) { kth = kb; idk = ib; }
@@ -559,7 +559,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   // of the last record is remembered with its run head (records of one run share their key).
   // Stage 2: the records past stage 1 whose bound still does not exceed the 11th entry; their exact
   // keys are computed once fewer than `room` slots remain (room 64: always).
-  auto drain_exact = [&](int room) {
+  auto drain_exact = [&](int room) __attribute__((always_inline)) {
     if (n2 == 0) return;
     {
       const int jj = lane < n2 ? s_q2[lane] : 0;
@@ -591,7 +591,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       if (!ex) key = r.costE + key;
       if (w_less(key, id, kth, idk)) {
         // feasibleNode in float, exactly as the reference within the float error of a limit
-        c = feasible_walk(sx, sy, r.bx, r.by, r.ca, r.sa, r.ang_par, p.feas_len);
+        c = feasible_search(sx, sy, r.bx, r.by, r.ca, r.sa, r.ang_par, p.feas_len);
       }
     }
     // remember the key of the queued record deepest inside a run of equal records (the longest runs,
@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   // upper bounds of surely feasible records tighten the 11th entry; the records whose lower bound does
   // not exceed it are queued for the exact keys (stage 2), which run on full waves of them.
   const float f2_sure = fmaxf((float)(p.feas_len * p.feas_len) * 1.002f + 1e-3f, (1e4f * dl) * (1e4f * dl));
-  auto stage1 = [&](bool ok, float4 pp, float4 qq, float ce, float& lbt, float& ubt) {
+  auto stage1 = [&](bool ok, float4 pp, float4 qq, float ce, float& lbt, float& ubt) __attribute__((always_inline)) {
     lbt = __builtin_inff();
     ubt = __builtin_inff();
     if (!ok) return;
@@ -659,7 +659,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     ubt = sure ? thi + 1e-6f * fabsf(thi) : __builtin_inff();
   };
   // upper bounds below the 11th entry enter the bound list (lanes 0..10)
-  auto ub_insert = [&](float ubt) {
+  auto ub_insert = [&](float ubt) __attribute__((always_inline)) {
     uint64_t mu = __ballot(ubt < kth);
     if (!mu) return false;
     while (mu) {
@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     }
     return true;
   };
-  auto enqueue = [&](bool ok, float lbt, int j) {
+  auto enqueue = [&](bool ok, float lbt, int j) __attribute__((always_inline)) {
     const bool keep = ok && !(lbt > kth);
     const uint64_t m = __ballot(keep);
     const int cnt = __popcll(m);
@@ -693,9 +693,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     n2 += cnt;
     __builtin_amdgcn_wave_barrier();
   };
-  auto drain = [&]() { drain_exact(64); };
+  auto drain = [&]() __attribute__((always_inline)) { drain_exact(64); };
   // Necessary conditions for record j to enter the list (the brute-force prefilter + turning bound).
-  auto prefilter = [&](int id, int hd, float4 pp, float4 qq, float ce) -> bool {
+  auto prefilter = [&](int id, int hd, float4 pp, float4 qq, float ce) __attribute__((always_inline)) -> bool {
     if (hd == hc && !w_less(kc, id, kth, idk)) return false;  // key known: kc
     const float qx = rsx - pp.x, qy = rsy - pp.y;
     const float d2 = qx * qx + qy * qy;

@@ -356,8 +356,9 @@ int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const doubl
  *                       the optimize key costE + dubinsDistance (rrtplanner.cpp:231,254,371-406) as the
  *                       nearest-node kernels evaluate them  [6 -> 2]
  *   CLRRT_UNIT_FEASIBLE sx, sy, node ref front x, y, ref back x, y, ref_res -> feasibleNode
- *                       (rrtplanner.cpp:271-289) as the brute-force search decides it, as the walk search
- *                       decides it, and 1 when the search prefilter lets the node through  [7 -> 3]
+ *                       (rrtplanner.cpp:271-289) evaluated exactly (new nodes, conflicts), as the nearest-node
+ *                       searches decide it (float with an exact fallback), and 1 when the brute-force
+ *                       prefilter lets the node through  [7 -> 3]
  *   CLRRT_UNIT_GOALBIAS goal[4], node x, y, ref back x, y -> feasibleGoalBias (rrtplanner.cpp:292-315)
  *                       [8 -> 1]
  *   CLRRT_UNIT_GOALREF  goal[4], parent ref back x, y, v0, ref_res -> N, v, x, y of getGoalReference

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <ctime>
 #include <chrono>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -78,9 +79,13 @@ struct Node {
 
 struct Obs { double cx, cy, th, sx, sy, vx, vy; };
 
+// Controller::dla (controller.h: the lookahead the reference keeps in its global controller object):
+// set by updateLookahead at each rollout's start and read by that rollout only; per thread, so that
+// orc_eval_iterations' threads do not share it.
+static thread_local double g_ctrl_dla = 0;
+
 struct Oracle {
   clrrt_params p;
-  double ctrl_dla = 0;
   int64_t sim_count = 0, fail_collision = 0, fail_acclimit = 0, fail_iterlimit = 0, rollouts = 0;
   vector<Obs> det;
   vector<Node> tree;
@@ -115,7 +120,7 @@ static double sat(double lo, double hi, double v) { return std::max(std::min(v, 
 // ---------------------------------------------------------------- controller (controller.cpp)
 static void update_lookahead(Oracle& o, double v) {  // controller.cpp:13-16
   double dla_c = o.p.ctrl_mindla - o.p.ctrl_tla * o.p.ctrl_dlavmin;
-  o.ctrl_dla = std::max(o.p.ctrl_mindla, dla_c + o.p.ctrl_tla * std::abs(v));
+  g_ctrl_dla = std::max(o.p.ctrl_mindla, dla_c + o.p.ctrl_tla * std::abs(v));
 }
 
 static int closest_point(const Ref& r, const Pt& q, int from) {  // controller.cpp:96-113
@@ -165,8 +170,8 @@ struct Ctrl {  // class Controller controller.h:8-28
 
   void update_waypoint(Oracle& o, const Ref& r, const Row& x) {  // controller.cpp:53-68
     update_lookahead(o, x[4]);
-    P.x = x[0] + o.ctrl_dla * r.dir * lm_cos(x[2]);  // a store between the two calls: no sincos
-    P.y = x[1] + o.ctrl_dla * r.dir * lm_sin(x[2]);
+    P.x = x[0] + g_ctrl_dla * r.dir * lm_cos(x[2]);  // a store between the two calls: no sincos
+    P.y = x[1] + g_ctrl_dla * r.dir * lm_sin(x[2]);
     IDwp = closest_point(r, P, IDwp);
     if ((size_t)IDwp >= r.x.size() - 1 - 2) endreached = true;
     if (at0(r.x, IDwp) == r.x.back() && at0(r.y, IDwp) == r.y.back()) endreached = true;
@@ -179,7 +184,7 @@ struct Ctrl {  // class Controller controller.h:8-28
   double steer(Oracle& o, const Ref& r, const Row& x) {  // :47-51
     const clrrt_vehicle& veh = o.p.veh;
     ym = lateral_error(r, x, IDwp, P);
-    double cmd = 2 * ((veh.L + veh.Kus * x[4] * x[4]) / pow(o.ctrl_dla, 2)) * ym;
+    double cmd = 2 * ((veh.L + veh.Kus * x[4] * x[4]) / pow(g_ctrl_dla, 2)) * ym;
     return sat(-veh.dmax, veh.dmax, cmd);
   }
   double accel(Oracle& o, const Ref& r, const Row& x) {  // :37-45 (LAlong = 2, :35)
@@ -407,7 +412,7 @@ static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
   const clrrt_vehicle& veh = o.p.veh;
   const double dt = o.p.sim_dt;
   for (int i = 0; i < (20 / dt); i++) {
-    o.sim_count++;
+    __atomic_fetch_add(&o.sim_count, 1, __ATOMIC_RELAXED);
     Row x = s.rows[i];
     // getControls controller.cpp:30-34 (braced init: steer before accel)
     c.update_waypoint(o, r, x);
@@ -420,27 +425,27 @@ static void propagate(Oracle& o, Sim& s, Ctrl c, const Ref& r) {  // :55-143
     x[9] = dc;
     s.rows.push_back(x);
     double Dobs = obs_distance(o, x);
-    if (Dobs == 0) { s.endReached = false; o.fail_collision++; s.outcome = CLRRT_ROLL_COLLISION; return; }
+    if (Dobs == 0) { s.endReached = false; __atomic_fetch_add(&o.fail_collision, 1, __ATOMIC_RELAXED); s.outcome = CLRRT_ROLL_COLLISION; return; }
     s.costE += x[4] * dt;
     double kappa = lm_tan(x[3]) / veh.L;
     s.costS += o.p.Wcost[0] * x[4] * dt + o.p.Wcost[1] * std::abs(kappa) +
                o.p.Wcost[2] * exp(-o.p.Wcost[3] * Dobs);
     if (o.p.bend) s.costS += o.p.Wcost[4] * dist_to_lane(x[0], x[1], o.p.lane_shift0, o.p.Cxy);
     double ay = std::abs(x[4] * dx[2]);
-    if (ay + o.p.ay_road_max > 3) { s.endReached = false; o.fail_acclimit++; s.outcome = CLRRT_ROLL_ACCLIMIT; return; }
+    if (ay + o.p.ay_road_max > 3) { s.endReached = false; __atomic_fetch_add(&o.fail_acclimit, 1, __ATOMIC_RELAXED); s.outcome = CLRRT_ROLL_ACCLIMIT; return; }
     double dg = sqrt(pow(x[0] - o.p.goal[0], 2) + pow(x[1] - o.p.goal[1], 2));
     double he = std::abs(angle_diff(x[2], o.p.goal[2]));
     double Ve = (x[4] - r.v.back());
     if (c.endreached && std::abs(Ve < 0.1)) { s.endReached = true; s.outcome = CLRRT_ROLL_END; return; }
     if ((dg <= 1) && (he < 0.05)) { s.goalReached = true; s.outcome = CLRRT_ROLL_GOAL; return; }
   }
-  o.fail_iterlimit++;
+  __atomic_fetch_add(&o.fail_iterlimit, 1, __ATOMIC_RELAXED);
 }
 
 // Simulation::Simulation :36-47 — mutates ref (fills ref.v)
 static Sim simulate(Oracle& o, const vector<double>& state, Ref& r, bool GB, double Vstart) {
   Sim s;
-  o.rollouts++;
+  __atomic_fetch_add(&o.rollouts, 1, __ATOMIC_RELAXED);
   s.rows.push_back(state);
   Ctrl c(o, r, state);
   s.rows.back()[7] = c.IDwp;
@@ -935,6 +940,20 @@ int orc_eval_iteration(void* h, double sx, double sy, int explore, int stable, c
   return n;
 }
 
+
+// n independent eval_iteration calls against the same frozen tree on `threads` host threads (the
+// tree is only read; the counters are updated atomically).  out: 2 records per sample, counts[k] of
+// them valid.  Test infrastructure for bench-size trees, where one call sorts millions of keys.
+void orc_eval_iterations(void* h, int n, const double* sx, const double* sy, const int* explore, int stable,
+                         int threads, clrrt_node* out, int* counts) {
+  std::vector<std::thread> pool;
+  const int T = std::max(1, std::min(threads, n));
+  for (int t = 0; t < T; t++)
+    pool.emplace_back([=]() {
+      for (int k = t; k < n; k += T) counts[k] = orc_eval_iteration(h, sx[k], sy[k], explore[k], stable, out + 2 * k);
+    });
+  for (auto& th : pool) th.join();
+}
 
 // ---- unit hooks (tests/test_ref_units.py): the same functions the tree path runs, one case per row.
 // OBB gap of the vehicle box at (x, y, th) against one obstacle at time t.

@@ -173,8 +173,11 @@ int main(int argc, char** argv) {
       grown = (int)b.tree.size() - 1;
     }
     bool ok = grown > 0;
+    // a child's first row is its parent's state with IDwp in column 7 (simulation.cpp:39-41)
     for (size_t i = 1; i < b.tree.size() && ok; i++)
-      if (b.tree[i].parentID == 0 && b.tree[i].tra.front() != rb.state) ok = false;
+      if (b.tree[i].parentID == 0)
+        for (int c = 0; c < 10; c++)
+          if (c != 7 && b.tree[i].tra.front()[c] != rb.state[c]) ok = false;
     if (!ok) { printf("FAIL: expandTree grew a stale tree (grown %d)\n", grown); failures++; }
     if (rand() != clrrt_rng_next(&eng.rng())) { printf("FAIL: rand() streams diverged\n"); failures++; }
   }

@@ -51,6 +51,8 @@ def lib():
             "orc_check_obs": (d, [vp, P(d)]),
             "orc_draw_samples": (None, [vp, i, P(d), P(i)]),
             "orc_eval_iteration": (i, [vp, d, d, i, i, P(abi.Node)]),
+            "orc_eval_iterations": (None, [vp, i, P(C.c_double), P(C.c_double), P(C.c_int), i, i, P(abi.Node),
+                                           P(C.c_int)]),
             "orc_extract_best_path": (i, [vp, P(i), i]),
             "orc_path_commit": (None, [vp, P(i), i]),
             "orc_path_size": (C.c_long, [vp]),
@@ -242,6 +244,19 @@ class Oracle:
         out = (abi.Node * 2)()
         n = self.L.orc_eval_iteration(self.h, sx, sy, 1 if explore else 0, 1 if stable else 0, out)
         return [out[i] for i in range(n)]
+
+    def eval_iterations(self, xs, ys, explore, stable=False, threads=8):
+        """eval_iteration for each (x, y, explore) against the same frozen tree, on host threads."""
+        n = len(xs)
+        x = np.ascontiguousarray(xs, dtype=np.float64)
+        y = np.ascontiguousarray(ys, dtype=np.float64)
+        e = np.ascontiguousarray(explore, dtype=np.int32)
+        out = (abi.Node * (2 * n))()
+        cnt = np.zeros(n, dtype=np.int32)
+        P = C.POINTER
+        self.L.orc_eval_iterations(self.h, n, _dp(x), _dp(y), e.ctypes.data_as(P(C.c_int)), 1 if stable else 0,
+                                   threads, out, cnt.ctypes.data_as(P(C.c_int)))
+        return [[out[2 * k + i] for i in range(cnt[k])] for k in range(n)]
 
 
 def obb_dist(a, b):

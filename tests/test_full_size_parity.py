@@ -8,7 +8,13 @@
   flag, state bits and float cost bits; for 48 of them the committed trajectory rows too.
 * cfg2 (50 static obstacles, B = 4096): two BATCH rounds, whole tree against the oracle's expand_batch,
   bit for bit (states, costs, rows).
-The 20-mover config-5 scene runs in tests/test_replan.py (test_replanning_queries_parity[moving20]).
+* cfg3 at the tree sizes the bench reaches (test_cfg3_bench_size_tree): one query grown past 2.2 M nodes
+  in pipelined BATCH rounds (clrrt_expand, the single-GPU bench path), where the large-tree search settings
+  engage (walk search, narrowed rollout grid, the N/512 exact-key budget).  On the next round (a) the
+  candidate lists of all 16384 samples from the default search equal brute force's, ids and key bits, and
+  (b) 128 samples' records inside the full round equal the oracle's eval_iteration on the frozen tree.
+The 20-mover config-5 scene runs in tests/test_replan.py (test_replanning_queries_parity[moving20],
+test_moving20_batch_reinit_from_found_path).
 """
 import numpy as np
 import pytest
@@ -107,6 +113,54 @@ def test_cfg3_full_batch_rounds_match_oracle():
     print(f"cfg3 full-batch rounds: {pl.size()[0]} nodes; oracle-checked {checked}")
     assert checked["nodes"] > 500 and checked["rows"] > 50
     pl.close()
+
+
+def test_cfg3_bench_size_tree():
+    import torch
+    B = 16384
+    target = 4096 * 512 + 100_000  # nn_walk_budget_keys' N/512 term exceeds its 4096 floor from 2.1 M nodes
+    max_nodes = 5 << 19
+    obs = scenes.urban_scene(200)
+    params = clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB)
+    pl = clrrt.Planner(params, max_nodes=max_nodes, max_rows=max_nodes * 64, max_batch=B)
+    try:
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        rng = clrrt.Rng(41)
+        while pl.size()[0] < target:
+            st = pl.expand(rng, n_iters=64 * B, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+            assert not st["capacity_stop"]
+        n_tree = pl.size()[0]
+        smp = rng.draw_samples(pl.params, B)
+        # (a) the default large-tree search against brute force (node-index tie order in both)
+        ids_w, keys_w = pl.sort_nodes_batch(smp, exact=False)
+        pl.set_option("nn_walk_min", 1 << 40)
+        ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
+        pl.set_option("nn_walk_min", 8192)
+        bad = np.nonzero((ids_w != ids_b).any(axis=1) | (keys_w.view(np.uint32) != keys_b.view(np.uint32)).any(axis=1))[0]
+        assert bad.size == 0, f"{n_tree} nodes: {bad.size} of {B} lists differ, e.g. {bad[:5]}"
+        assert (ids_b[:, 0] >= 0).sum() > B // 2
+        # (b) the round's records of 128 samples against the oracle
+        out = torch.empty((2 * B, REC), dtype=torch.uint8, device="cuda")
+        n = pl.round_eval(smp, out.data_ptr())
+        rec = _records(out[:n].cpu().numpy().tobytes(), n)
+        picks = sorted(np.random.default_rng(9).choice(B, 128, replace=False).tolist())
+        o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+        o.load_tree(pl.nodes_raw())
+        want = o.eval_iterations([smp[j].x for j in picks], [smp[j].y for j in picks],
+                                 [smp[j].explore for j in picks], stable=True, threads=16)
+        mine = _per_sample(rec, smp, picks)
+        nodes, bad = 0, []
+        for j, w in zip(picks, want):
+            got = mine[j]
+            nodes += len(w)
+            if not (len(got) == len(w) and all(_same_node(rec, i, r) for i, r in zip(got, w))):
+                bad.append((j, len(w), len(got)))
+        print(f"cfg3 bench-size tree: {n_tree} nodes, {B} lists = brute force, 128 samples ({nodes} nodes) = oracle")
+        assert not bad, f"{n_tree} nodes: {len(bad)} of 128 samples differ {bad[:5]}"
+        assert nodes > 20
+    finally:
+        pl.close()
 
 
 def test_cfg2_batch_tree_parity():

@@ -141,7 +141,7 @@ def test_device_matches_reference_fixture(unit):
         x = FIX[f"{unit}_in"]
         got = R.run_device(pl, unit, x)
         if unit == "feasible":
-            # the brute-force decider and the walk decider equal the reference; the search prefilter
+            # the exact decider and the searches' decider equal the reference; the brute-force prefilter
             # lets every feasible node through
             want = _fixture_out(unit)[:, 0]
             for col in (0, 1):

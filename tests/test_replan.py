@@ -272,6 +272,49 @@ def test_replanning_queries_parity(kind):
 
 
 @pytest.mark.gpu
+def test_moving20_batch_reinit_from_found_path():
+    """Config 5's defining branch on the full 20-mover scene: BATCH queries (B = 256, two rounds each,
+    rrtplanner.cpp:123-174 in BATCH tie order) find a goal-reaching path in query 0, and queries 1-3
+    re-initialise from it (initializeTree, rrtplanner.cpp:39-95: outcome KEPT = 3).  The goal sits 20 m
+    ahead instead of 40 m so the oracle reaches it in seconds; the trees equal the oracle's after every
+    re-init and every expansion."""
+    mode = abi.CLRRT_COLLISION_OBB
+    obs = _moving_scene(drop_208=False)
+    make = _make(mode)
+    B, R, seed, goal_w = 256, 2, 11, (20.0, 0.0, 0.0, 0.0)
+    o = Oracle(abi.default_params(collision_mode=mode), None)
+    pl = _planner(mode, max_batch=B)
+    ob, gb = OracleBackend(o, make), replan.PlannerBackend(pl, make)
+    Oracle.srand(seed)
+    rng = clrrt.Rng(seed)
+    pose = np.array([0.0, 0.0, 0.0, 0.0, 1.0, 0.0])
+    outcomes, path_lens = [], []
+    for q in range(4):
+        t = q * replan.QUERY_PERIOD
+        goal_c = replan.goal_in_car_frame(goal_w, pose)
+        obs_c = replan.obstacles_in_car_frame(obs, t, pose)
+        oc_o = ob.begin_query(pose, goal_c, obs_c)
+        oc_g = gb.begin_query(pose, goal_c, obs_c)
+        assert oc_o == oc_g, (q, oc_o, oc_g)
+        outcomes.append(oc_o)
+        _assert_same_tree(o, pl, f"q{q} re-init")
+        o.expand_batch(B * R, B, stable=True)
+        st = pl.expand(rng, n_iters=B * R, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+        assert st["rounds"] == R
+        _assert_same_tree(o, pl, f"q{q} expanded")
+        ids_o, rows_o = ob.end_query(pose)
+        ids_g, rows_g = gb.end_query(pose)
+        assert ids_o == ids_g
+        path_lens.append(len(ids_o))
+        assert np.array_equal(rows_g.view(np.uint64), rows_o.view(np.uint64))
+        pose = replan.advance_pose(pose, rows_o)
+    print("moving20 BATCH outcomes", outcomes, "committed path lengths", path_lens)
+    assert outcomes[0] == abi.REINIT_EMPTY and path_lens[0] > 0
+    assert outcomes.count(abi.REINIT_KEPT) >= 2, outcomes
+    pl.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["erased", "collision", "kept"])
 def test_reinit_outcomes_parity(case):
     """ALL_ERASED, COLLISION and KEPT outcomes through the C-ABI match the oracle."""

@@ -1,5 +1,5 @@
 """Per-phase wave time of the rollout kernel (build: make -C cl-rrt_amd/csrc prof; run with
-CLRRT_LIB=build/prof/libclrrt.so): cfg3 scene, BATCH expansion for `ms`."""
+CLRRT_LIB=cl-rrt_amd/prof/libclrrt.so): cfg3 scene, BATCH expansion for `ms`."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
