@@ -70,7 +70,6 @@ _SIGS = {
     "clrrt_work_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_kernel_time": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_int64)]),
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
-    "clrrt_set_nn_grid": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_obstacle_distance": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32, P(C.c_double)]),
@@ -455,15 +454,6 @@ class Planner:
         out = (C.c_int64 * 40)()
         self._chk(self.L.clrrt_debug_counters(self.h, out), "debug_counters")
         return list(out)
-
-    def set_nn_grid(self, min_nodes, modes=1, wave_budget=0):
-        """Trees of >= min_nodes nodes search the samples of `modes` (1 explore, 2 optimize) through
-        the spatial grid (0: always; a huge value: never)."""
-        self._chk(self.L.clrrt_set_nn_grid(self.h, int(min_nodes), int(modes), int(wave_budget)), "set_nn_grid")
-
-    def set_nn_grid_threshold(self, min_nodes):
-        """Grid search for both modes from min_nodes nodes (test helper)."""
-        self.set_nn_grid(min_nodes, 3, 0)
 
     def kernel_time(self, which):
         ms, n = C.c_double(), C.c_int64()

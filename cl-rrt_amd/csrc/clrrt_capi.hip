@@ -87,15 +87,11 @@ struct clrrt_ctx {
   int64_t* totals = nullptr;
   unsigned long long* work_ctr = nullptr;  // [3] algorithmic rollout work; [8..15] nn search statistics
   // spatial index of the tree (nearest-node search)
-  NnGridBufs nng{};
-  int* fb_list = nullptr;   // [max_batch] samples the grid search hands to brute force
-  int* fb_count = nullptr;
+  float* nn_seed = nullptr;  // [max_batch] the brute-force chunks' shared per-sample key caps
   // bounding box of the tree's finite node positions (x0, y0, x1, y1), maintained on the host
   double bbox[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   double* d_bbox = nullptr;  // [4] device result of launch_bbox
   double* h_bbox = nullptr;  // [4] pinned
-  int64_t nng_min_nodes = INT64_MAX;  // clrrt_set_nn_grid: off by default (brute force is faster on bench trees)
-  int64_t nno_min_nodes = INT64_MAX;  // place-ordered brute force from this tree size ("nn_ordered_min"; off)
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
   bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
   // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64;
@@ -109,8 +105,6 @@ struct clrrt_ctx {
   WalkBufs nnw_alt{};
   struct { int64_t n = -1; double ox, oy, x0, y0, x1, y1; float delta; } nnw_built;
   CompactBufs cmp{};                   // round compaction scratch
-  int nng_modes = 1;
-  int nng_budget = 0;
   // persistent rollouts (k_roll_prep + k_roll_run)
   int roll_persistent = 1;
   int nn_debug = 0;
@@ -120,16 +114,8 @@ struct clrrt_ctx {
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
-  int roll_prio = 0;          // option "roll_prio": k_roll_run's wave issue priority (RollArgs::prio_mode)
-  int roll_point_cache = 0;   // option "roll_point_cache": reference points in LDS (k_roll_run; off: see DESIGN §8)
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
-  int roll_handoff = 0;       // option "roll_handoff": donor waves hand their last rollouts to absorbers
-  void* roll_cont = nullptr;  // [roll_cont_cap] RollCont
-  int* roll_ready = nullptr;  // [roll_cont_cap]
-  int* roll_ctl = nullptr;    // [4]
-  int roll_cont_cap = 0;
-  int roll_epoch = 0;
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
   GoalRec* goal_recs = nullptr;
   int* bp_path = nullptr;  // [max_nodes + 2]: chain, then count and length
@@ -149,19 +135,8 @@ struct clrrt_ctx {
   // of the next round's samples over the same tree runs on `side` into the *2 buffers; the round
   // then merges in the nodes it appended (launch_nn_delta) and the buffers swap
   int nn_pipeline = 1;  // option "nn_pipeline"
-  // option "nn_delta_grid": appended-node search through a uniform grid instead of the chunked brute force
-  // (off: identical lists, but one lane per sample walks its cells' records with dependent loads, and on
-  // cfg3 the round time nearly doubles: 0.515 vs 0.955 M nodes/s)
-  int nn_delta_grid = 0;
-  DeltaGrid dg{};
   hipStream_t side = nullptr;
   hipEvent_t ev_tree = nullptr, ev_walk = nullptr, ev_commit = nullptr;
-  // option "nn_side_build": the next round's walk index is built on the side stream behind the
-  // appended-node search (only the side stream's next walk reads it), so the main stream goes on to the
-  // next round's rollouts; ev_built marks its end for any main-stream use of the index
-  int nn_side_build = 0;  // off: no measurable change on cfg3 (0.952 vs 0.958 M nodes/s)
-  hipEvent_t ev_built = nullptr;
-  bool nnw_side_pending = false;
   clrrt_sample* d_samples2 = nullptr;
   clrrt_sample* h_samples2 = nullptr;
   int* cand2 = nullptr;
@@ -291,7 +266,6 @@ static void derive(const clrrt_params& q, DevParams& d, int n_obs) {
   d.need_gap = (q.collision_mode == CLRRT_COLLISION_OBB) && d.use_exp;
 }
 
-static const int64_t kNngMaxCells = 1 << 20, kNngMaxSuper = kNngMaxCells / 64;
 
 static void bbox_reset(clrrt_ctx* c) {
   c->bbox[0] = c->bbox[1] = HUGE_VAL;
@@ -415,14 +389,11 @@ static void free_all(clrrt_ctx* c) {
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
                   c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
-                  c->nng.cellid, c->nng.count, c->nng.fill, c->nng.start, c->nng.cmin, c->nng.smin,
-                  c->nng.sorted, c->nng.fmin, c->nng.fmax, c->fb_list, c->fb_count, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag, c->nng.scount, c->nng.sfill, c->nng.sstart,
-                  c->nng.order, c->nng.nsamp, c->nng.tbox, c->nng.tcost, c->nng.home, c->nng.seed,
+                  c->nn_seed, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
                   c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
-                  c->cmp.tmp, c->roll_cont, c->roll_ready, c->roll_ctl, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2,
-                  c->dg.cnt, c->dg.fill, c->dg.cmin, c->dg.box, c->dg.gmin, c->dg.frame, c->dg.idx};
+                  c->cmp.tmp, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -431,7 +402,6 @@ static void free_all(clrrt_ctx* c) {
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
   if (c->ev_commit) hipEventDestroy(c->ev_commit);
-  if (c->ev_built) hipEventDestroy(c->ev_built);
   if (c->side) hipStreamDestroy(c->side);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
@@ -477,16 +447,6 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   c->partial_cap = std::max<int64_t>(B * 16, 4096) * NN_K;
   chk(dalloc(&c->pk, c->partial_cap));
   chk(dalloc(&c->pi, c->partial_cap));
-  // appended-node grid: a round appends <= 2 records per sample; the multi-rank commit appends every
-  // rank's (up to 8 ranks here, more fall back to the chunked search)
-  chk(dalloc(&c->dg.cnt, DG_NC + 2));
-  chk(dalloc(&c->dg.fill, DG_NC + 1));
-  chk(dalloc(&c->dg.cmin, DG_NC + 1));
-  chk(dalloc(&c->dg.box, 4 * (DG_NC + 1)));
-  chk(dalloc(&c->dg.gmin, 1));
-  chk(dalloc(&c->dg.frame, 1));
-  c->dg.cap = (int)std::min<int64_t>(16 * B, 1 << 30);
-  chk(dalloc(&c->dg.idx, c->dg.cap));
   chk(dalloc(&c->cand, B * CAND_K));
   chk(dalloc(&c->ckey, B * CAND_K));
   chk(dalloc(&c->ncand, B));
@@ -500,7 +460,6 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(hipEventCreateWithFlags(&c->ev_tree, hipEventDisableTiming));
   chk(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
   chk(hipEventCreateWithFlags(&c->ev_commit, hipEventDisableTiming));
-  chk(hipEventCreateWithFlags(&c->ev_built, hipEventDisableTiming));
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->res_gb, B * CAND_K));
@@ -516,25 +475,7 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->cmp.scanned, B));
   c->cmp.tmp_bytes = compact_scan_bytes((int)B);
   chk(hipMalloc(&c->cmp.tmp, std::max<size_t>(c->cmp.tmp_bytes, 256)));
-  chk(dalloc(&c->nng.cellid, c->cap.max_nodes));
-  chk(dalloc(&c->nng.sorted, c->cap.max_nodes));
-  chk(dalloc(&c->nng.count, kNngMaxCells + 2));
-  chk(dalloc(&c->nng.fill, kNngMaxCells + 2));
-  chk(dalloc(&c->nng.start, kNngMaxCells + 2));
-  chk(dalloc(&c->nng.cmin, kNngMaxCells + 2));
-  chk(dalloc(&c->nng.smin, kNngMaxSuper + 2));
-  chk(dalloc(&c->nng.scount, 2 * kNngMaxSuper + 4));
-  chk(dalloc(&c->nng.sfill, 2 * kNngMaxSuper + 4));
-  chk(dalloc(&c->nng.sstart, 2 * kNngMaxSuper + 4));
-  chk(dalloc(&c->nng.order, B));
-  chk(dalloc(&c->nng.nsamp, 1));
-  chk(dalloc(&c->nng.home, B));
-  chk(dalloc(&c->nng.seed, B));
-  chk(dalloc(&c->nng.tbox, c->cap.max_nodes / 256 + 2));
-  chk(dalloc(&c->nng.tcost, c->cap.max_nodes / 256 + 2));
-  chk(dalloc(&c->nng.fmin, 4 * kNngMaxSuper));
-  chk(dalloc(&c->nng.fmax, 4 * kNngMaxSuper));
-  chk(dalloc(&c->fb_list, B));
+  chk(dalloc(&c->nn_seed, B));
   chk(hipMalloc(&c->roll_prep, rollout_prep_bytes() * (size_t)B * CAND_K));
   chk(dalloc(&c->roll_q, 1));
   chk(dalloc(&c->roll_best, B));
@@ -545,16 +486,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
       c->n_cu = ncu;
   }
-  // hand-off slots: every lane of every wave of the largest persistent grid (roll_blocks <= 4 per CU)
-  c->roll_cont_cap = 4 * c->n_cu * 256;
-  chk(hipMalloc(&c->roll_cont, rollout_cont_bytes() * (size_t)c->roll_cont_cap));
-  chk(dalloc(&c->roll_ready, c->roll_cont_cap));
-  chk(dalloc(&c->roll_ctl, 4));
-  if (rc == CLRRT_OK) chk(hipMemset(c->roll_ready, 0, sizeof(int) * c->roll_cont_cap));
-  if (rc == CLRRT_OK) chk(hipMemset(c->roll_ctl, 0, sizeof(int) * 4));
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
-  chk(dalloc(&c->fb_count, 1));
   chk(dalloc(&c->work_ctr, 40));
   if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 40 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
@@ -1159,7 +1092,6 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return CLRRT_EINVAL;
   const std::string k(key);
   if (k == "roll_persistent") c->roll_persistent = value != 0;
-  else if (k == "nn_ordered_min" && value >= 0) c->nno_min_nodes = value;
   else if (k == "nn_walk_min" && value >= 0) c->nnw_min_nodes = value;
   else if (k == "nn_walk_stateless") c->nnw_stateless = value != 0;
   else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) c->nnw_bud_tiles = (int)value;
@@ -1170,12 +1102,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
-  else if (k == "nn_delta_grid") c->nn_delta_grid = value != 0;
-  else if (k == "nn_side_build") c->nn_side_build = value != 0;
-  else if (k == "roll_handoff") c->roll_handoff = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
-  else if (k == "roll_prio" && value >= 0 && value <= 2) c->roll_prio = (int)value;
-  else if (k == "roll_point_cache") c->roll_point_cache = value != 0;
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
     HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1190,14 +1117,6 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     }
   }
   else return fail(c, CLRRT_EINVAL, "unknown option or value: " + k);
-  return CLRRT_OK;
-}
-
-int clrrt_set_nn_grid(clrrt_ctx* c, int64_t min_nodes, int32_t modes, int32_t wave_budget) {
-  if (!c || min_nodes < 0 || modes < 0 || modes > 3 || wave_budget < 0) return CLRRT_EINVAL;
-  c->nng_min_nodes = min_nodes;
-  c->nng_modes = modes;
-  c->nng_budget = wave_budget;
   return CLRRT_OK;
 }
 
@@ -1264,8 +1183,9 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.CE, Mp));
   HIPC(c, dalloc(&w.ID, Mp));
   HIPC(c, dalloc(&w.HEAD, Mp));
-  HIPC(c, dalloc(&w.tiles, Mp / 64 + 1));
-  HIPC(c, dalloc(&w.supers, Mp / 1024 + 1));
+  // one record per tile / super-tile of the padded index (launch_nn_walk_build)
+  HIPC(c, dalloc(&w.tiles, walk_tile_count(c->cap.max_nodes) + 1));
+  HIPC(c, dalloc(&w.supers, walk_super_count(c->cap.max_nodes) + 1));
   HIPC(c, dalloc(&w.ovf_n, 1));
   HIPC(c, dalloc(&w.ovf, kWalkMaxOver));
   HIPC(c, dalloc(&w.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
@@ -1273,6 +1193,8 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.skeys, Mp));
   HIPC(c, dalloc(&w.sids, Mp));
   w.sorted_n = -1;
+  w.cap_nodes = c->cap.max_nodes;
+  w.cap_batch = (int)c->cap.max_batch;
   HIPC(c, dalloc(&w.P, Mp));  // last: marks the set complete
   return CLRRT_OK;
 }
@@ -1323,9 +1245,7 @@ static NnSetup nn_setup(clrrt_ctx* c) {
 
 // The walk search serves the tree as it is now (run_nn's choice).
 static bool walk_serves(clrrt_ctx* c, const NnSetup& su) {
-  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && su.region_ok;
-  const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && su.region_ok;
-  return !use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && su.region_ok;
+  return c->n_nodes >= c->nnw_min_nodes && su.region_ok;
 }
 
 // Any tree change other than clrrt_round_commit invalidates a prefetched search.
@@ -1347,23 +1267,12 @@ static bool walk_built_for(const clrrt_ctx* c, const NnSetup& su) {
   return b.n == c->n_nodes && b.ox == su.fr.ox && b.oy == su.fr.oy && b.delta == su.fr.delta && b.x0 == su.x0 &&
          b.y0 == su.y0 && b.x1 == su.x1 && b.y1 == su.y1;
 }
-// The main stream is about to use (or rebuild) the walk index: wait for a side-stream build of it.
-static int side_build_wait(clrrt_ctx* c) {
-  if (!c->nnw_side_pending) return CLRRT_OK;
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_built, 0));
-  c->nnw_side_pending = false;
-  return CLRRT_OK;
-}
-static int pre_roll_build(clrrt_ctx* c, const NnSetup& su, hipStream_t st = nullptr) {
-  KTimer kt(c, 0, st ? st : c->stream);
+static int pre_roll_build(clrrt_ctx* c, const NnSetup& su) {
+  KTimer kt(c, 0, c->stream);
   const int rw = ensure_walk(c);
   if (rw != CLRRT_OK) return rw;
   if (walk_built_for(c, su)) return CLRRT_OK;  // built ahead (next_round_build)
-  if (!st) {
-    const int r2 = side_build_wait(c);
-    if (r2 != CLRRT_OK) return r2;
-  }
-  HIPC(c, launch_nn_walk_build(st ? st : c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw,
+  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw,
                                c->nnw_alt.P ? &c->nnw_alt : nullptr));
   auto& b = c->nnw_built;
   b.n = c->n_nodes;
@@ -1375,23 +1284,12 @@ static int pre_roll_build(clrrt_ctx* c, const NnSetup& su, hipStream_t st = null
 // Pipelined rounds, right after a commit: the next round's index over the committed tree goes into
 // the other buffer set on the main stream while the side stream's search still reads this one (it
 // waits for nothing but the commit; the wait for the side search comes after it).
-// With nn_side_build, the build goes on the side stream behind the appended-node search (the side
-// stream's walk of the round after next is its only reader; it already waited for the commit); the
-// main stream then waits for the search alone.
 static int next_round_build(clrrt_ctx* c) {
   const NnSetup su = nn_setup(c);
   if (!walk_serves(c, su)) return CLRRT_OK;
-  int rc = side_build_wait(c);
-  if (rc != CLRRT_OK) return rc;
   std::swap(c->nnw, c->nnw_alt);
   c->nnw_built.n = -1;
-  if (!c->nn_side_build) return pre_roll_build(c, su);
-  HIPC(c, hipStreamWaitEvent(c->side, c->ev_commit, 0));
-  rc = pre_roll_build(c, su, c->side);
-  if (rc != CLRRT_OK) return rc;
-  HIPC(c, hipEventRecord(c->ev_built, c->side));
-  c->nnw_side_pending = true;
-  return CLRRT_OK;
+  return pre_roll_build(c, su);
 }
 
 static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
@@ -1422,8 +1320,7 @@ static int side_delta_launch(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
     const NnSetup su2 = nn_setup(c);  // the box includes the appended nodes
     const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n2 * NN_K));
     HIPC(c, launch_nn_delta(c->side, c->d_samples2, n2, c->nn, (int)first_new, nn, c->dp, su2.fr, c->pk, c->pi,
-                            max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nng.seed,
-                            c->nn_delta_grid ? &c->dg : nullptr));
+                            max_chunks, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->nn_seed));
   }
   HIPC(c, hipEventRecord(c->ev_walk, c->side));
   return CLRRT_OK;
@@ -1453,46 +1350,19 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   c->nn_bf_keys += (int64_t)n * c->n_nodes;
   c->nn_samples += n;
   int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
-  NnGrid g{};
   const NnSetup su = nn_setup(c);
-  const NnFrame fr = su.fr;
-  const double x0 = su.x0, y0 = su.y0, x1 = su.x1, y1 = su.y1;
-  const double W = x1 - x0, H = y1 - y0;
-  const bool region_ok = su.region_ok;
-  const bool use_grid = c->n_nodes >= c->nng_min_nodes && c->nng_modes != 0 && region_ok;
-  const bool ordered = !use_grid && c->n_nodes >= c->nno_min_nodes && region_ok;
-  if (!use_grid && !ordered && c->n_nodes >= c->nnw_min_nodes && region_ok) {
+  if (walk_serves(c, su)) {
     int rc = ensure_walk(c);
     if (rc != CLRRT_OK) return rc;
-    if ((rc = side_build_wait(c)) != CLRRT_OK) return rc;
     c->nnw_built.n = -1;
-    HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, fr, x0, y0, x1, y1, c->nnw, c->cand,
-                           c->ckey, c->ncand, c->ctie, c->work_ctr + 18, c->nnw_stateless));
+    HIPC(c, launch_nn_walk(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1, su.y1,
+                           c->nnw, c->cand, c->ckey, c->ncand, c->ctie, c->work_ctr + 18, c->nnw_stateless));
     if (scratch) HIPC(c, launch_nn_exact_only(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->ctie, scratch,
                                               c->cand, c->ckey, c->ncand));
     return CLRRT_OK;
   }
-  if (use_grid || ordered) {
-    double cs = std::max(0.05, std::sqrt(W * H * 4.0 / (double)c->n_nodes));
-    // square power-of-two grid (Morton cell numbering), at most kNngMaxCells cells
-    auto side = [&](double c) {
-      int n = 8;
-      while (n < std::ceil(std::max(W, H) / c)) n *= 2;
-      return n;
-    };
-    while ((double)side(cs) * side(cs) > (double)kNngMaxCells) cs *= 1.1;
-    g.x0 = x0; g.y0 = y0; g.cs = cs; g.inv = 1.0 / cs;
-    g.slack = 1e-9 * (1.0 + std::fabs(x0) + std::fabs(y0) + W + H);
-    g.gw = g.gh = side(cs);
-    g.sw = g.sh = g.gw / 8;
-    g.ncell = g.gw * g.gh;
-    g.modes = c->nng_modes;
-    g.budget = c->nng_budget;
-    HIPC(c, launch_nn_grid_build(st, c->nn, (int)c->n_nodes, g, c->nng));
-  }
   HIPC(c, launch_nn(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->pk, c->pi, c->cand, c->ckey,
-                    c->ncand, c->ctie, max_chunks, scratch, (use_grid || ordered) ? &g : nullptr, &c->nng, c->fb_list,
-                    c->fb_count, c->work_ctr + 8, fr, ordered));
+                    c->ncand, c->ctie, max_chunks, scratch, c->nn_seed, c->work_ctr + 8, su.fr));
   return CLRRT_OK;
 }
 
@@ -1537,20 +1407,11 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     const int64_t nt = c->n_nodes;
     const int eighths = nt < 300000 ? 7 : nt < 700000 ? 5 : nt < 1100000 ? 4 : 3;
     const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu)
-                       : c->roll_handoff  ? c->n_cu
                                           : std::max(1, (eighths * c->n_cu) / 8);
-    if (c->roll_persistent && c->roll_handoff) {
-      a.cont = c->roll_cont;
-      a.cont_ready = c->roll_ready;
-      a.cont_ctl = c->roll_ctl;
-      a.cont_epoch = ++c->roll_epoch;
-    }
     if (c->roll_priority) {
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
     }
-    a.pcache_enable = c->roll_point_cache;
-    a.prio_mode = c->roll_prio;
     if (c->roll_persistent && c->dp.n_steps_max > 0)
       HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
     else
@@ -1595,11 +1456,9 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
   }
   HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));
-  HIPC(c, hipMemcpyAsync(c->h_int + 3, c->roll_ctl + 3, sizeof(int), hipMemcpyDeviceToHost, st));
   if (merge_bbox) HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
   if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
-  if (c->h_int[3] != 0) return fail(c, CLRRT_EHIP, "rollout hand-off: a donated rollout was never published");
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
   c->counters.sim_count += c->h_totals[2];

@@ -99,26 +99,12 @@ struct RollArgs {
   RollRes* __restrict__ res_gb;            // SPEC: goal-biased rollout (outcome -1 = not run)
   unsigned long long* ctr;  // [3] steps, scan points, box tests (nullable)
   int njobs;
-  // persistent rollouts: hand-off of the last rollouts from donor waves to absorbers (k_roll_run);
-  // cont == nullptr: off.  cont_ctl = {published, claimed, donors alive, hand-off errors}
-  void* cont;
-  int* cont_ready;  // per slot: == cont_epoch once the slot is written
-  int* cont_ctl;
-  int cont_epoch, cont_donors;
   // persistent rollouts: queue order (nullable).  k_roll_prep flags the jobs likely to run long
   // (pflag[q], q = k B + s), the queue serves them first (perm[position] = q); results do not depend
   // on the order
   int* perm;
   int* pflag;
   int B;
-  // k_roll_run's per-lane reference-point cache in LDS (launch_rollout_persistent sizes it)
-  int pcache_enable;  // option "roll_point_cache"
-  int pcache_n;       // points per lane (0: off)
-  int pcache_off;     // byte offset in the dynamic LDS
-  // k_roll_run's wave issue priority (option "roll_prio"): 0 default, 1 raised once the wave finds the
-  // job queue empty (the stragglers), 2 raised from the start.  A raised wave wins the SIMD's
-  // instruction-issue arbitration against the side stream's search waves that share its SIMD.
-  int prio_mode;
 };
 
 struct SelArgs {
@@ -135,60 +121,8 @@ struct SelArgs {
   int B;
 };
 
-// Spatial index of the tree for the nearest-node search (clrrt_nngrid.hip): nodes bucketed by a
-// uniform grid of gw x gh cells (multiples of 8) of size cs from (x0, y0), numbered super-cell-major
-// (8x8 cells per super-cell, super-cell (X, Y) = cells [64 (Y sw + X), 64 (Y sw + X) + 64));
-// cell ncell collects the nodes outside the grid.
-struct NnGrid {
-  double x0, y0, cs, inv, slack;
-  int gw, gh, sw, sh, ncell;
-  int modes;   // sample modes searched through the grid: 1 explore, 2 optimize
-  int budget;  // node records a wave may read (0: automatic)
-  const uint32_t* start;  // [ncell + 2]: cell c holds recs[start[c] .. start[c+1])
-  const NnRec* recs;      // node records ordered by cell
-  const uint32_t* cmin;   // per cell: min costE (order-preserving encoding)
-  const uint32_t* smin;   // per super-cell
-  const uint32_t* gmin;   // [1] over all super-cells
-  const uint32_t* fmin;   // per super-cell [4] (int32): floor of min ref.back() x, y [mm], ang_par [urad]
-                          // in (-pi, pi] and shifted to [0, 2pi)
-  const uint32_t* fmax;   // per super-cell [4] (int32): ceil of the maxima
-};
-struct NnGridBufs {
-  int* cellid;
-  uint32_t *count, *fill, *start, *cmin, *smin, *fmin, *fmax;
-  NnRec* sorted;
-  uint32_t *scount, *sfill, *sstart;  // sample buckets [2 * super-cells + 2]
-  int* order;                         // [max_batch] samples ordered by bucket
-  int* nsamp;                         // [1] = B (device copy for the ordered brute force)
-  int* home;                          // [max_batch] first record of the ordered sample's cell
-  float* seed;                        // [max_batch] upper bound on each sample's 11th key
-  float4* tbox;                       // [max_nodes / 256 + 1] tile boxes of the ordered records
-  float* tcost;                       // [max_nodes / 256 + 1] tile minimum costs
-};
-hipError_t launch_nn_grid_build(hipStream_t st, const NnRec* nodes, int N, NnGrid& g, NnGridBufs& b);
-// b.order[0 .. B) = the samples ordered by mode and super-cell
-hipError_t launch_sample_order(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, NnGridBufs& b);
-hipError_t launch_nn_grid_search(hipStream_t st, const clrrt_sample* S, int B, const NnGrid& g, const DevParams& p,
-                                 int* cand, float* ckey, int* ncand, int* ctie, int cap, int* fb_list,
-                                 int* fb_count, NnGridBufs& b, unsigned long long* stats);
-
 // Frame of the brute-force search's float prune: positions relative to (ox, oy) in float are within
 // delta of the exact differences for every node and sample of the round.
-// Uniform grid over a round's appended records for the pipelined rounds' appended-node search
-// (k_nn_delta_grid): DG_G x DG_G cells + one cell (index DG_NC) for non-finite positions.
-#define DG_G 64
-#define DG_NC (DG_G * DG_G)
-struct DeltaGrid {
-  int* cnt;            // [DG_NC + 2]: counts, then exclusive starts; [DG_NC + 1] = total
-  int* fill;           // [DG_NC + 1]
-  unsigned int* cmin;  // [DG_NC + 1] minimum costE per cell (order-preserving encoding)
-  unsigned int* box;   // [4 (DG_NC + 1)] x0, y0, -x1, -y1 of the cell's float positions (encoded minima)
-  unsigned int* gmin;  // [1] minimum costE of all records
-  float4* frame;       // [1] x0, y0, 1 / cell, cell (float frame coordinates)
-  int* idx;            // [capacity] record indices in cell order
-  int cap;
-};
-
 struct NnFrame {
   double ox, oy;
   float delta;
@@ -232,8 +166,13 @@ struct WalkBufs {
   int* sids;
   int64_t sorted_n;
   double sorted_x0, sorted_y0, sorted_scale;
+  int64_t cap_nodes;  // the buffers hold an index of up to this many nodes (checked at every launch)
+  int cap_batch;      // and searches of up to this many samples
 };
 size_t walk_sort_bytes(int n);
+// Tile / super-tile records an index of up to n nodes needs (WalkBufs::tiles, ::supers).
+int64_t walk_tile_count(int64_t n);
+int64_t walk_super_count(int64_t n);
 // Candidate lists of samples S[0 .. B) (same output as the brute force: cand, ckey, ncand, ctie);
 // (x0, y0, x1, y1) = box holding every finite node position (the Morton frame).
 hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
@@ -247,22 +186,16 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
                                  bool stateless);
 // Pipelined BATCH rounds: merges into (cand, ckey, ncand) -- the lists over nodes [0, first) -- the
-// nodes [first, first + count) appended since (k_nn_partial over them, or k_nn_delta_grid when `dg` is
-// given and can hold them, + k_nn_merge_delta).
+// nodes [first, first + count) appended since (k_nn_partial over them + k_nn_merge_delta).
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
-                           float* ckey, int* ncand, int* ctie, float* seed, const DeltaGrid* dg = nullptr);
-// Brute-force candidate lists of the samples fb_list[0 .. *fb_count) (the walk search's hand-offs).
-hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                                const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
-                                int* ncand, int* ctie, int max_chunks, const int* fb_list, const int* fb_count);
-
+                           float* ckey, int* ncand, int* ctie, float* seed);
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
-// selection involves equal keys are re-sorted with the replay of std::sort.
+// selection involves equal keys are re-sorted with the replay of std::sort.  seed: [B] scratch for the
+// chunks' shared key caps (or null).
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
-                     int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats, const NnFrame& fr, bool ordered);
+                     int max_chunks, KeyId* exact_scratch, float* seed, unsigned long long* stats, const NnFrame& fr);
 // EXACT mode after a search that filled ctie: std::sort replay for the tied samples.
 hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
@@ -274,7 +207,6 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, v
                                      int blocks);
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t rollout_prep_bytes();
-size_t rollout_cont_bytes();
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);

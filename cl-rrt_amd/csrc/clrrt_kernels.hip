@@ -76,23 +76,13 @@ __device__ __forceinline__ float prune_r(float slack) {
 //   * not deep inside a turning circle when (cost +) 14.9 > kth (inside -> Dubins key >= rho pi).
 // Survivors are queued per lane; a second pass runs nn_prefilter, the exact Dubins key and
 // feasibleNode on the queue, so lanes stay converged instead of diverging node by node.
-// sidx != nullptr: lanes t < *scount search sample sidx[t] (samples ordered by place, or the grid
-// search's over-budget samples).
-// tbox != nullptr: the nodes are ordered by place (cell order) with per-tile float bounding boxes in
-// the frame and minimum costs, and the samples by place too.  Chunk c then takes the tiles
-// c, c + nchunks, c + 2 nchunks, ... (every chunk spans the whole tree), visited outward from the
-// tile holding the block's home cell so the lists fill with near nodes first; a tile none of whose
-// nodes can pass any lane's Euclidean prune is skipped by the whole block.  List entries are the
-// records' node ids.
 #define NN_QCAP 32
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, NnFrame fr, float* __restrict__ pk,
-                                                    int* __restrict__ pi, const int* __restrict__ sidx,
-                                                    const int* __restrict__ scount, const float4* __restrict__ tbox,
-                                                    const float* __restrict__ tcost, const int* __restrict__ home,
-                                                    const float* __restrict__ seed, unsigned long long* tstat) {
-  int tiles_seen = 0, tiles_done = 0, n_queued = 0, n_exact = 0;
+                                                    int* __restrict__ pi, const float* __restrict__ seed,
+                                                    unsigned long long* tstat) {
+  int n_queued = 0, n_exact = 0;
   __shared__ float4 s_r[256];   // node x, y and ref.back() x, y relative to the frame origin (float)
   __shared__ double2 s_p[256];  // node x, y
   __shared__ float4 s_f[256];   // c, s, ca, sa
@@ -103,9 +93,8 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   const int c = blockIdx.y;
   const int n0 = c * chunk;
   const int n1 = min(N, n0 + chunk);
-  if (sidx && (int)(blockIdx.x * blockDim.x) >= *scount) return;
-  const bool act = sidx ? t < *scount : t < B;
-  const int s = act && sidx ? sidx[t] : t;
+  const bool act = t < B;
+  const int s = t;
   double sx = 0, sy = 0;
   int ex = 1;
   if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
@@ -164,31 +153,11 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       }
     }
   };
-  const int ntile = (N + 255) >> 8;
-  int tcount, i0 = 0;
-  if (tbox) {
-    tcount = c < ntile ? (ntile - 1 - c) / nchunks + 1 : 0;
-    const int ht = home[blockIdx.x * blockDim.x] >> 8;  // the block's first sample's home tile
-    i0 = min(max(0, (ht - c + nchunks - 1) / nchunks), max(0, tcount - 1));
-  } else {
-    tcount = (n1 - n0 + 255) >> 8;
-  }
+  const int tcount = (n1 - n0 + 255) >> 8;
   for (int it = 0; it < tcount; it++) {
-    int b;
-    if (tbox) {
-      // i0, i0 + 1, i0 - 1, i0 + 2, ... clipped to [0, tcount)
-      const int lo = i0, hi = tcount - 1 - i0;  // steps available below / above
-      const int sym = min(lo, hi);
-      int i;
-      if (it <= 2 * sym) i = (it & 1) ? i0 + (it + 1) / 2 : i0 - it / 2;
-      else if (hi > lo) i = i0 + (it - lo);
-      else i = i0 - (it - hi);
-      b = (c + i * nchunks) << 8;
-    } else {
-      b = n0 + (it << 8);
-    }
+    const int b = n0 + (it << 8);
     const int m = min(256, N - b);
-    bool need = act;
+    const bool need = act;
     if (seed && act) {  // pick up tighter bounds published by the sample's other chunks
       const float kc = ord_dec32(__atomic_load_n(&gcap[s], __ATOMIC_RELAXED));
       if (kc < kcap) {
@@ -196,22 +165,6 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
         const float R = prune_r(fminf(keys[NN_K - 1], kcap));
         rr = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
       }
-    }
-    if (tbox) {
-      // the tile's Euclidean bound (the same float positions the node test uses)
-      const float4 bx = tbox[b >> 8];
-      const float ex0 = fmaxf(fmaxf(bx.x - rsx, rsx - bx.z), 0.f);
-      const float ey0 = fmaxf(fmaxf(bx.y - rsy, rsy - bx.w), 0.f);
-      const float bd2 = (ex0 * ex0 + ey0 * ey0) * (1.f - 1e-6f);
-      float lim = rr;
-      if (!ex) {
-        const float R = prune_r(fminf(keys[NN_K - 1], kcap) - tcost[b >> 8]);
-        lim = R < 0.f ? -1.f : (R + fr.delta) * (R + fr.delta);
-      }
-      need = act && !(bd2 > lim);  // NaN bounds never skip
-      tiles_seen++;
-      if (!__syncthreads_or(need)) continue;
-      tiles_done++;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
@@ -221,7 +174,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
       s_f[i] = make_float4(rec.c, rec.s, rec.ca, rec.sa);
       s_c[i] = rec.costE;
       s_p[i] = make_double2(rec.x, rec.y);
-      s_id[i] = tbox ? rec.id : b + i;
+      s_id[i] = b + i;
     }
     __syncthreads();
     if (!need) continue;
@@ -278,11 +231,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
 #pragma unroll
     for (int j = 0; j < NN_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
   }
-  if (tstat) {  // diagnostics: tiles considered / searched per block, queued pairs, exact keys
-    if (threadIdx.x == 0) {
-      atomicAdd(&tstat[0], (unsigned long long)tiles_seen);
-      atomicAdd(&tstat[1], (unsigned long long)tiles_done);
-    }
+  if (tstat) {  // diagnostics: queued pairs, exact keys
     atomicAdd(&tstat[2], (unsigned long long)n_queued);
     atomicAdd(&tstat[3], (unsigned long long)n_exact);
   }
@@ -290,11 +239,10 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
 
 __global__ void k_nn_merge(int B, int nchunks, int limit, const float* __restrict__ pk,
                            const int* __restrict__ pi, int* __restrict__ cand, float* __restrict__ ckey,
-                           int* __restrict__ ncand, int* __restrict__ ctie, const int* __restrict__ sidx,
-                           const int* __restrict__ scount) {
+                           int* __restrict__ ncand, int* __restrict__ ctie) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sidx ? t >= *scount : t >= B) return;
-  const int s = sidx ? sidx[t] : t;
+  if (t >= B) return;
+  const int s = t;
   float keys[NN_K];
   int ids[NN_K];
 #pragma unroll
@@ -386,211 +334,6 @@ __global__ void k_nn_merge_delta(int B, int nchunks, int limit, const float* __r
   }
   ncand[s] = n;
   ctie[s] = tie;
-}
-
-// Appended-node search through a uniform grid (pipelined BATCH rounds; replaces the chunked brute force
-// of launch_nn_delta when a DeltaGrid is given).  The round's appended records [first, first + n) are
-// bucketed by their float frame position into DG_G x DG_G cells over their bounding box (records with
-// non-finite positions into an extra cell every sample visits); per cell the bounding box of those float
-// positions and the minimum costE are kept.  One lane per sample then visits only the cells that can hold
-// a record able to enter its list: the cell range of the prune radius of the seed (the walk list's
-// `limit`-th key: a larger key cannot enter the merged list, an equal one sorts after it since every
-// appended id is larger), and per cell the tile bound of k_nn_partial's place-ordered path (cell box
-// distance against the prune radius of min(11th key, seed) minus the cell's minimum cost).  The records
-// visited go through k_nn_partial's tests unchanged (Euclidean prune, feasibleNode margins, turning
-// circle, the key's lower bound, exact key, feasibleNode), so the lane's list holds the 11 smallest
-// (key, id) pairs of every appended record that can enter, and k_nn_merge_delta's result is the one the
-// brute force gives.
-__global__ void k_dg_init(DeltaGrid g) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= DG_NC) {
-    g.cnt[i] = 0;
-    g.fill[i] = 0;
-    g.cmin[i] = 0xffffffffu;
-#pragma unroll
-    for (int q = 0; q < 4; q++) g.box[4 * i + q] = 0xffffffffu;
-  }
-  if (i == 0) g.gmin[0] = 0xffffffffu;
-}
-
-// grid frame over the finite float positions: x0, y0, 1 / cell, cell (one block)
-__global__ void __launch_bounds__(256) k_dg_bounds(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
-  float x0 = __builtin_inff(), y0 = __builtin_inff(), x1 = -__builtin_inff(), y1 = -__builtin_inff();
-  float cm = __builtin_inff();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const float fx = (float)(nodes[i].x - fr.ox), fy = (float)(nodes[i].y - fr.oy);
-    cm = fminf(cm, nodes[i].costE);
-    if (!(isfinite(fx) && isfinite(fy))) continue;
-    x0 = fminf(x0, fx); x1 = fmaxf(x1, fx);
-    y0 = fminf(y0, fy); y1 = fmaxf(y1, fy);
-  }
-  __shared__ float r[5][256];
-  r[0][threadIdx.x] = x0; r[1][threadIdx.x] = y0; r[2][threadIdx.x] = -x1; r[3][threadIdx.x] = -y1;
-  r[4][threadIdx.x] = cm;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
-      for (int q = 0; q < 5; q++) r[q][threadIdx.x] = fminf(r[q][threadIdx.x], r[q][threadIdx.x + o]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    x0 = r[0][0]; y0 = r[1][0]; x1 = -r[2][0]; y1 = -r[3][0];
-    float cs = fmaxf(x1 - x0, y1 - y0) * (1.0f / DG_G) * 1.0001f;
-    if (!(cs > 1e-3f)) cs = 1e-3f;  // also no finite position at all
-    if (!isfinite(x0)) { x0 = 0.f; y0 = 0.f; }
-    g.frame[0] = make_float4(x0, y0, 1.0f / cs, cs);
-    g.gmin[0] = ord_enc32(r[4][0]);
-  }
-}
-
-__device__ __forceinline__ int dg_cell(const float4& gf, float fx, float fy) {
-  if (!(isfinite(fx) && isfinite(fy))) return DG_NC;
-  const int gx = min(max((int)floorf((fx - gf.x) * gf.z), 0), DG_G - 1);
-  const int gy = min(max((int)floorf((fy - gf.y) * gf.z), 0), DG_G - 1);
-  return gy * DG_G + gx;
-}
-
-__global__ void __launch_bounds__(256) k_dg_count(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 gf = g.frame[0];
-  const float fx = (float)(nodes[i].x - fr.ox), fy = (float)(nodes[i].y - fr.oy);
-  const int c = dg_cell(gf, fx, fy);
-  atomicAdd(&g.cnt[c], 1);
-  atomicMin(&g.cmin[c], ord_enc32(nodes[i].costE));
-  atomicMin(&g.box[4 * c], ord_enc32(fx));
-  atomicMin(&g.box[4 * c + 1], ord_enc32(fy));
-  atomicMin(&g.box[4 * c + 2], ord_enc32(-fx));
-  atomicMin(&g.box[4 * c + 3], ord_enc32(-fy));
-}
-
-// exclusive scan of the DG_NC + 1 counts in place (one block of 1024); cnt[DG_NC + 1] = total
-__global__ void __launch_bounds__(1024) k_dg_scan(DeltaGrid g) {
-  constexpr int per = (DG_NC + 1 + 1023) / 1024;
-  __shared__ int s[1024];
-  const int b = threadIdx.x * per;
-  int v[per], sum = 0;
-#pragma unroll
-  for (int q = 0; q < per; q++) {
-    v[q] = b + q <= DG_NC ? g.cnt[b + q] : 0;
-    sum += v[q];
-  }
-  s[threadIdx.x] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int t = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += t;
-    __syncthreads();
-  }
-  int run = s[threadIdx.x] - sum;
-#pragma unroll
-  for (int q = 0; q < per; q++) {
-    if (b + q <= DG_NC) g.cnt[b + q] = run;
-    run += v[q];
-  }
-  if (threadIdx.x == 1023) g.cnt[DG_NC + 1] = s[1023];
-}
-
-__global__ void __launch_bounds__(256) k_dg_scatter(const NnRec* __restrict__ nodes, int n, NnFrame fr, DeltaGrid g) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 gf = g.frame[0];
-  const int c = dg_cell(gf, (float)(nodes[i].x - fr.ox), (float)(nodes[i].y - fr.oy));
-  g.idx[g.cnt[c] + atomicAdd(&g.fill[c], 1)] = i;
-}
-
-__global__ void __launch_bounds__(64) k_nn_delta_grid(const clrrt_sample* __restrict__ S, int B,
-                                                      const NnRec* __restrict__ nodes, DevParams p, NnFrame fr,
-                                                      DeltaGrid g, const float* __restrict__ seed,
-                                                      float* __restrict__ pk, int* __restrict__ pi) {
-  // explore samples in the first half of the grid, optimize samples in the second: a wave then holds one
-  // kind only (optimize radii, which subtract the costE, span most of the cells; explore radii a few)
-  const int half = (int)gridDim.x >> 1;
-  const bool want_ex = (int)blockIdx.x < half;
-  const int s = ((int)blockIdx.x - (want_ex ? 0 : half)) * (int)blockDim.x + (int)threadIdx.x;
-  if (s >= B || (S[s].explore != 0) != want_ex) return;
-  const double sx = S[s].x, sy = S[s].y;
-  const bool ex = want_ex;
-  const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
-  const float dl = fr.delta;
-  float keys[NN_K];
-  int ids[NN_K];
-#pragma unroll
-  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
-  const float kcap = ord_dec32(((const unsigned int*)seed)[s]);
-  const float flen = (float)p.feas_len - 2.f * dl;
-  const float fl2 = flen > 0.f ? flen * flen : 0.f;
-  const float c45 = 0.69276f;
-  const float rho = 4.77f, rin = rho - 0.01f - 4.f * dl;
-  const float rin2 = rin > 0.f ? rin * rin : -1.f;
-  auto lim_of = [&](float slack) -> float {  // (prune radius + delta)^2; -1: nothing can enter
-    const float R = prune_r(slack);
-    return R < 0.f ? -1.f : (R + dl) * (R + dl);
-  };
-  auto test = [&](int i) {
-    const NnRec& rec = nodes[i];
-    const float kt = fminf(keys[NN_K - 1], kcap);
-    const float cst = rec.costE;
-    const float qx = (float)(rec.x - fr.ox), qy = (float)(rec.y - fr.oy);
-    const float dx = rsx - qx, dy = rsy - qy;
-    const float d2 = dx * dx + dy * dy;
-    const float lim = lim_of(ex ? kt : kt - cst);
-    if (!((d2 <= lim) || (lim != lim))) return;  // a NaN limit never prunes
-    const float vx = rsx - (float)(rec.bx - fr.ox), vy = rsy - (float)(rec.by - fr.oy);
-    const float dot = vx * rec.ca + vy * rec.sa, vv = vx * vx + vy * vy;
-    const bool ang_bad = (vv < fl2) || (dot < -1e-3f) || (dot * dot < c45 * c45 * vv && dot >= 0.f);
-    const float tx = rec.c * dx - rec.s * dy, ty = fabsf(rec.s * dx + rec.c * dy);
-    const bool deep = tx * tx + (ty - rho) * (ty - rho) <= rin2;
-    const bool in_bad = deep && !((ex ? 14.9f : cst + 14.9f) <= kt);
-    if (ang_bad || in_bad) return;
-    const float qx2 = (float)(sx - rec.x), qy2 = (float)(sy - rec.y);
-    const float tx2 = rec.c * qx2 - rec.s * qy2, ty2 = fabsf(rec.s * qx2 + rec.c * qy2);
-    float lb = dubins_lb(tx2, ty2);
-    if (!ex) lb = cst + lb;
-    if (lb > keys[NN_K - 1]) return;
-    float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
-    if (!ex) key = cst + key;
-    // (key, i) must precede the lane's 11th entry; a key at or above the seed cannot enter the merge
-    if (!lex_less(key, i, keys[NN_K - 1], ids[NN_K - 1]) || !(key < kcap)) return;
-    if (feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len)) topk_insert(keys, ids, key, i);
-  };
-  const float4 gf = g.frame[0];
-  const float gmin = ord_dec32(g.gmin[0]);
-  // cell range from the initial radius (bounds only shrink)
-  const float lim0 = lim_of(ex ? kcap : kcap - gmin);
-  int gx0 = 0, gx1 = DG_G - 1, gy0 = 0, gy1 = DG_G - 1;
-  if (lim0 < 0.f) {
-    gx1 = gy1 = -1;  // nothing can enter
-  } else if (lim0 < __builtin_inff() && isfinite(rsx) && isfinite(rsy)) {
-    const float R = sqrtf(lim0) * 1.0001f + 1e-3f;
-    gx0 = max(0, (int)floorf((rsx - R - gf.x) * gf.z) - 1);
-    gx1 = min(DG_G - 1, (int)floorf((rsx + R - gf.x) * gf.z) + 1);
-    gy0 = max(0, (int)floorf((rsy - R - gf.y) * gf.z) - 1);
-    gy1 = min(DG_G - 1, (int)floorf((rsy + R - gf.y) * gf.z) + 1);
-  }
-  for (int gy = gy0; gy <= gy1; gy++)
-    for (int gx = gx0; gx <= gx1; gx++) {
-      const int c = gy * DG_G + gx;
-      const int a = g.cnt[c], e = g.cnt[c + 1];
-      if (a == e) continue;
-      // the cell's bound: distance from the sample to the box of its records' float positions
-      const float bx0 = ord_dec32(g.box[4 * c]), by0 = ord_dec32(g.box[4 * c + 1]);
-      const float bx1 = -ord_dec32(g.box[4 * c + 2]), by1 = -ord_dec32(g.box[4 * c + 3]);
-      const float ex0 = fmaxf(fmaxf(bx0 - rsx, rsx - bx1), 0.f);
-      const float ey0 = fmaxf(fmaxf(by0 - rsy, rsy - by1), 0.f);
-      const float bd2 = (ex0 * ex0 + ey0 * ey0) * (1.f - 1e-6f);
-      const float kt = fminf(keys[NN_K - 1], kcap);
-      const float lim = lim_of(ex ? kt : kt - ord_dec32(g.cmin[c]));
-      if (bd2 > lim) continue;  // NaN bounds never skip
-      for (int q = a; q < e; q++) test(g.idx[q]);
-    }
-  for (int q = g.cnt[DG_NC]; q < g.cnt[DG_NC + 1]; q++) test(g.idx[q]);  // non-finite positions
-#pragma unroll
-  for (int j = 0; j < NN_K; j++) {
-    pk[(size_t)s * NN_K + j] = keys[j];
-    pi[(size_t)s * NN_K + j] = ids[j];
-  }
 }
 
 // EXACT mode, samples whose candidate selection involves equal keys: rebuild the full (id, key)
@@ -782,11 +525,11 @@ struct PhaseClk {
 template <bool NEED_GAP>
 __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
                                          double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr,
-                                         PtCache pts = {nullptr, 0}) {
+                                         int = 0) {
   double Px, Py;
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
   w.scan += (uint32_t)(r.R.N - r.wp);
-  double dla = update_waypoint(r, p, Px, Py, false, pts);
+  double dla = update_waypoint(r, p, Px, Py, false);
 #ifdef CLRRT_DUP_WP
   {
     double z = 0.0;
@@ -797,7 +540,7 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   }
 #endif
   if (pc) pc->mark(1);
-  double ym = lateral_error(r, Px, Py, pts);
+  double ym = lateral_error(r, Px, Py);
 #ifdef CLRRT_DUP_LAT
   {
     double z = 0.0;
@@ -1173,11 +916,6 @@ template <bool NEED_GAP>
 __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
   glibc::stage_tables();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j == 0 && a.cont) {  // k_roll_run's hand-off counters (the error count accumulates)
-    a.cont_ctl[0] = 0;
-    a.cont_ctl[1] = 0;
-    a.cont_ctl[2] = a.cont_donors;
-  }
   if (j >= a.njobs) return;
   const int id = a.cand[j];
   int* pflag = a.pflag ? a.pflag + (j % CAND_K) * a.B + j / CAND_K : nullptr;  // queue position q = k B + s
@@ -1209,21 +947,12 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
 #ifndef REFILL_MIN
 #define REFILL_MIN 16
 #endif
-#ifndef CLRRT_DONATE_MAX  // a donor wave hands off its rollouts once at most this many are left
-#define CLRRT_DONATE_MAX 16
-#endif
-struct RollCont {  // a rollout in flight, handed from a donor wave to an absorber (k_roll_run)
-  Roll r;
-  double c7, c8, c9;
-  int32_t j, k, s, pass, steps, pad;
-};
-size_t rollout_cont_bytes() { return sizeof(RollCont); }
 
 #ifndef CLRRT_ABANDON_EVERY  // steps between checks for an earlier candidate's success (power of 2)
 #define CLRRT_ABANDON_EVERY 16
 #endif
 
-template <bool NEED_GAP, bool HANDOFF>
+template <bool NEED_GAP>
 #ifndef CLRRT_ROLL_WAVES
 #define CLRRT_ROLL_WAVES 1
 #endif
@@ -1233,17 +962,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int lane = threadIdx.x & 63;
-  // this lane's reference-point cache: after the obstacle tables, a.pcache_n points x 256 lanes
-  double2* const pts_base = (double2*)((char*)lds + a.pcache_off) + threadIdx.x;
-  int pts_n = 0;  // points of the current rollout's reference in the cache
-  auto pts = [&]() -> PtCache { return PtCache{pts_base, pts_n}; };
   const int64_t slot = (int64_t)a.slot_rows * 10;
   const int64_t pass_stride = slot * a.slot_jobs;
   WorkCtr w{0, 0, 0};
   Roll r;
   double c7 = 0, c8 = 0, c9 = 0;
   int j = -1, k = 0, s = 0, pass = 0, steps = 0;
-  auto refill_pts = [&]() { pts_n = a.pcache_n > 0 ? fill_points(r.R, pts_base, a.pcache_n) : 0; };
   bool exhausted = false;
   PhaseClk pclk{};
 #ifdef CLRRT_ROLL_PROFILE
@@ -1257,24 +981,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   unsigned long long scan_sum = 0, scan_wave = 0, scan_long = 0, scan_long_pts = 0, chain_steps = 0;
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
-  // Hand-off of the last rollouts (a.cont != nullptr).  Rollout lengths are very uneven (most end
-  // within ~30 steps, the longest run the full 500-step horizon), so once the job queue is empty most
-  // waves keep a few long rollouts and hold their SIMD for the rest of the launch.  Instead, wave 0 of
-  // each block is an absorber and the other waves are donors: a donor whose queue has run out and
-  // which has <= CLRRT_DONATE_MAX rollouts left writes their state to a.cont and exits, freeing its SIMD
-  // for work queued on other streams (the next round's nearest-node search); absorbers take the
-  // donated rollouts into idle lanes and continue them (same job, same rows, same results).
-  constexpr bool cont_on = HANDOFF;  // a.cont != nullptr
-  const bool absorber = !cont_on || (threadIdx.x >> 6) == 0;
-  RollCont* __restrict__ cont = (RollCont*)a.cont;
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
-  bool raised = false;
-  if (a.prio_mode == 2) {
-    __builtin_amdgcn_s_setprio(3);
-    raised = true;
-  }
-  int poll = 0;
-  uint32_t idle_polls = 0;  // hand-off absorber: polls without work (spin limit)
+
   // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
   // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
   // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
@@ -1294,7 +1002,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           // goal-biased rollout from the node this rollout would append (expandTree :163-173)
           const RefD R = make_goal_ref(out.bx, out.by, a.p);
           roll_init(r, out.st, R, out.vback, true, a.p);
-          refill_pts();
           c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
           pass = 1;
           steps = 0;
@@ -1314,27 +1021,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (pc) pc->mark(0);
     const uint64_t parked = __ballot(fin >= 0);
     const uint64_t busy0 = __ballot(j >= 0 && fin < 0);
-    if (cont_on && !absorber && qdone && __popcll(busy0 | parked) <= CLRRT_DONATE_MAX) {
-      finish_parked();  // may start goal-biased rollouts
-      const bool give = j >= 0;
-      const uint64_t gm = __ballot(give);
-      if (gm) {
-        const int leader = __ffsll((unsigned long long)gm) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&a.cont_ctl[0], __popcll(gm));
-        base = __shfl(base, leader, 64);
-        if (give) {
-          const int q = base + __popcll(gm & ((1ull << lane) - 1));
-          RollCont& cc = cont[q];
-          cc.r = r;
-          cc.c7 = c7; cc.c8 = c8; cc.c9 = c9;
-          cc.j = j; cc.k = k; cc.s = s; cc.pass = pass; cc.steps = steps;
-          __hip_atomic_store(&a.cont_ready[q], a.cont_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      if (lane == 0) atomicSub(&a.cont_ctl[2], 1);
-      break;
-    }
     const uint64_t m0 = __ballot(j < 0 && !qdone);
     // once the queue is empty, finish parked rollouts at once: a goal-biased follow-up (up to the whole
     // horizon) must not wait for other lanes to end
@@ -1364,7 +1050,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               j = -1;
             } else {
               r = prep[j].r;
-              refill_pts();
               c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
               pass = 0;
               steps = 0;
@@ -1372,73 +1057,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           }
         }
         qdone = qdone || __ballot(exhausted) != 0;
-        if (qdone && !raised && a.prio_mode == 1) {
-          __builtin_amdgcn_s_setprio(3);
-          raised = true;
-        }
       }
       if (pc) pc->mark(6);
       continue;
-    }
-    if (cont_on && absorber && qdone) {
-      const uint64_t idle = __ballot(j < 0);
-      if (idle && (busy0 == 0 || ++poll >= 32)) {
-        poll = 0;
-        // claim up to popcount(idle) donated rollouts (never past the published count)
-        const int leader = __ffsll((unsigned long long)idle) - 1;
-        int got = 0, h = 0;
-        if (lane == leader) {
-          const int want = __popcll(idle);
-          for (;;) {
-            h = __hip_atomic_load(&a.cont_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int t = __hip_atomic_load(&a.cont_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int n = min(want, t - h);
-            if (n <= 0) break;
-            if (atomicCAS(&a.cont_ctl[1], h, h + n) == h) { got = n; break; }
-          }
-        }
-        got = __shfl(got, leader, 64);
-        h = __shfl(h, leader, 64);
-        if (got) {
-          idle_polls = 0;
-          const int rk = __popcll(idle & ((1ull << lane) - 1));
-          if (j < 0 && rk < got) {
-            const int q = h + rk;
-            // the donor published the slot count before writing the slot: wait for its flag
-            int spins = 0;
-            while (__hip_atomic_load(&a.cont_ready[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.cont_epoch) {
-              __builtin_amdgcn_s_sleep(2);
-              if (++spins > (1 << 24)) break;
-            }
-            if (spins > (1 << 24)) {
-              atomicAdd(&a.cont_ctl[3], 1);  // reported by the host as an error
-            } else {
-              const RollCont& cc = cont[q];
-              r = cc.r;
-              refill_pts();
-              c7 = cc.c7; c8 = cc.c8; c9 = cc.c9;
-              j = cc.j; k = cc.k; s = cc.s; pass = cc.pass; steps = cc.steps;
-              fin = -1;
-            }
-          }
-          continue;
-        }
-        if (busy0 == 0) {
-          // nothing to run: done once no donor remains and every donated rollout is claimed
-          const int d = __hip_atomic_load(&a.cont_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int hh = __hip_atomic_load(&a.cont_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int tt = __hip_atomic_load(&a.cont_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (parked == 0 && d <= 0 && hh >= tt) break;
-          // backstop (the launcher keeps the grid resident): ~1 s of polling without a donor finishing
-          // ends the wave and is reported by the host as an error instead of hanging the GPU
-          if (++idle_polls > (1 << 22)) {
-            if (lane == 0) atomicAdd(&a.cont_ctl[3], 1);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(8);
-          continue;
-        }
-      }
     }
     if (busy0 == 0) {
       if (parked == 0 && qdone) break;
@@ -1453,7 +1074,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
     const int best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
     if (pc) pc->mark(6);
-    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc, pts());
+    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
 #ifdef CLRRT_ROLL_PROFILE
     {
       unsigned it = r.scan_it, mx_ = it;
@@ -1484,7 +1105,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       j = -1;
     }
   }
-  if (a.ctr) {  // per-wave sums (no block barrier: donor waves leave early)
+  if (a.ctr) {  // per-wave sums (no block barrier)
     unsigned long long v0 = w.steps, v1 = w.scan, v2 = w.box;
 #pragma unroll
     for (int q = 32; q > 0; q >>= 1) {
@@ -2234,135 +1855,18 @@ __global__ void k_obs_distance(DevParams p, const BakedObs* __restrict__ obs, co
 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
-                                  float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
-                                  const int* scount, const float4* tbox = nullptr, const float* tcost = nullptr,
-                                  const int* home = nullptr, const float* seed = nullptr,
+                                  float* ckey, int* ncand, int* ctie, int max_chunks, const float* seed = nullptr,
                                   unsigned long long* tstat = nullptr);
-
-// Per 256-node tile of the place-ordered records: bounding box of the float frame positions the
-// brute-force prune uses, and the minimum cost (NaN if any cost is NaN).
-__global__ void __launch_bounds__(256) k_tile_bounds(const NnRec* __restrict__ recs, int N, NnFrame fr,
-                                                     float4* __restrict__ tbox, float* __restrict__ tcost) {
-  __shared__ float s[5][256];
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  float x0 = __builtin_inff(), y0 = __builtin_inff(), x1 = -__builtin_inff(), y1 = -__builtin_inff();
-  float cm = __builtin_inff();
-  if (i < N) {
-    const NnRec& r = recs[i];
-    const float x = (float)(r.x - fr.ox), y = (float)(r.y - fr.oy);
-    // NaN positions make the box NaN (never skipped)
-    x0 = x; x1 = x; y0 = y; y1 = y;
-    cm = r.costE;
-  }
-  s[0][threadIdx.x] = x0; s[1][threadIdx.x] = y0; s[2][threadIdx.x] = x1; s[3][threadIdx.x] = y1;
-  s[4][threadIdx.x] = cm;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if ((int)threadIdx.x < off) {
-      const int o = threadIdx.x + off;
-      const float a0 = s[0][threadIdx.x], b0 = s[0][o], a1 = s[1][threadIdx.x], b1 = s[1][o];
-      const float a2 = s[2][threadIdx.x], b2 = s[2][o], a3 = s[3][threadIdx.x], b3 = s[3][o];
-      const float a4 = s[4][threadIdx.x], b4 = s[4][o];
-      // NaN-propagating min / max
-      s[0][threadIdx.x] = (a0 != a0 || b0 != b0) ? __builtin_nanf("") : fminf(a0, b0);
-      s[1][threadIdx.x] = (a1 != a1 || b1 != b1) ? __builtin_nanf("") : fminf(a1, b1);
-      s[2][threadIdx.x] = (a2 != a2 || b2 != b2) ? __builtin_nanf("") : fmaxf(a2, b2);
-      s[3][threadIdx.x] = (a3 != a3 || b3 != b3) ? __builtin_nanf("") : fmaxf(a3, b3);
-      s[4][threadIdx.x] = (a4 != a4 || b4 != b4) ? __builtin_nanf("") : fminf(a4, b4);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    tbox[blockIdx.x] = make_float4(s[0][0], s[1][0], s[2][0], s[3][0]);
-    tcost[blockIdx.x] = s[4][0];
-  }
-}
-
-// Seed of the place-ordered search: the 11th smallest key (of feasible nodes) among the place-ordered
-// records around the sample's home cell (5 tiles), an upper bound on its 11th key over the tree
-// (+inf when fewer than 11 are found).  seed[s] for sample s.
-__global__ void __launch_bounds__(256) k_nn_seed(const clrrt_sample* __restrict__ S, int B,
-                                                 const NnRec* __restrict__ recs, int N, DevParams p,
-                                                 const int* __restrict__ order, const int* __restrict__ home,
-                                                 float* __restrict__ seed) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= B) return;
-  const int s = order[t];
-  const double sx = S[s].x, sy = S[s].y;
-  const int ex = S[s].explore;
-  float keys[NN_K];
-  int ids[NN_K];
-#pragma unroll
-  for (int j = 0; j < NN_K; j++) { keys[j] = __builtin_inff(); ids[j] = 0x7fffffff; }
-  const int ht = home[t] >> 8;
-  const int a = max(0, (ht - 2) << 8), b = min(N, (ht + 3) << 8);
-  const float feas2 = nn_feas2(p.feas_len);
-  for (int k = a; k < b; k++) {
-    const NnRec& rec = recs[k];
-    const float qx = (float)(sx - rec.x), qy = (float)(sy - rec.y);
-    if (!nn_prefilter(sx, sy, qx, qy, rec.c, rec.s, rec.ca, rec.sa, rec.bx, rec.by, rec.costE, ex, keys[NN_K - 1],
-                      feas2))
-      continue;
-    float key = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
-    if (!ex) key = rec.costE + key;
-    if (lex_less(key, rec.id, keys[NN_K - 1], ids[NN_K - 1]) &&
-        feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len))
-      topk_insert(keys, ids, key, rec.id);
-  }
-  ((unsigned int*)seed)[s] = ord_enc32(keys[NN_K - 1]);
-}
-
-hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
-                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
-                            int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
-                            float4* tbox, float* tcost, const int* home, float* seed,
-                            unsigned long long* tstat) {
-  hipLaunchKernelGGL(k_tile_bounds, dim3((N + 255) / 256), dim3(256), 0, st, sorted, N, fr, tbox, tcost);
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_nn_seed, dim3((B + 255) / 256), dim3(256), 0, st, S, B, sorted, N, p, order, home, seed);
-  LAUNCH_CHECK();
-  return launch_nn_brute(st, S, B, sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, order, nsamp,
-                         tbox, tcost, home, seed, tstat);
-}
-
-hipError_t launch_nn_sorted(hipStream_t st, const clrrt_sample* S, int B, const NnRec* sorted, int N,
-                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
-                            int* ncand, int* ctie, int max_chunks, const int* order, const int* nsamp,
-                            float4* tbox, float* tcost, const int* home, float* seed,
-                            unsigned long long* tstat);
 
 hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                      const DevParams& p, float* pk, int* pi, int* cand, float* ckey, int* ncand, int* ctie,
-                     int max_chunks, KeyId* exact_scratch, const NnGrid* grid, NnGridBufs* gbufs, int* fb_list,
-                     int* fb_count, unsigned long long* stats, const NnFrame& fr, bool ordered) {
-  if (ordered) {
-    // place-ordered records (built by launch_nn_grid_build) and place-ordered samples
-    hipError_t e = launch_sample_order(st, S, B, *grid, *gbufs);
-    if (e != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)gbufs->nsamp, B, 1, st)) != hipSuccess) return e;
-    e = launch_nn_sorted(st, S, B, gbufs->sorted, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks,
-                         gbufs->order, gbufs->nsamp, gbufs->tbox, gbufs->tcost, gbufs->home, gbufs->seed,
-                         stats ? stats + 5 : nullptr);
-    if (e != hipSuccess) return e;
-  } else if (grid) {
-    // budget: a sample visiting more nodes than a brute-force chunk costs goes to brute force
-    hipError_t e = hipMemsetAsync(fb_count, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
-    const int cap = grid->budget > 0 ? grid->budget : max(8192, N / 16);
-    e = launch_nn_grid_search(st, S, B, *grid, p, cand, ckey, ncand, ctie, cap, fb_list, fb_count, *gbufs, stats);
-    if (e != hipSuccess) return e;
-    if (stats) {
-      e = hipMemcpyAsync(stats + 4, fb_count, sizeof(int), hipMemcpyDeviceToDevice, st);  // low word: fallbacks
-      if (e != hipSuccess) return e;
-    }
-    e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
-    if (e != hipSuccess) return e;
-  } else {
+                     int max_chunks, KeyId* exact_scratch, float* seed, unsigned long long* stats, const NnFrame& fr) {
+  {
     // shared per-sample key caps start at +inf (order-preserving encoding of +inf = 0xff800000)
-    hipError_t e = gbufs ? hipMemsetD32Async((hipDeviceptr_t)gbufs->seed, 0xff800000u, B, st) : hipSuccess;
+    hipError_t e = seed ? hipMemsetD32Async((hipDeviceptr_t)seed, 0xff800000u, B, st) : hipSuccess;
     if (e != hipSuccess) return e;
-    e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, nullptr, nullptr,
-                        nullptr, nullptr, nullptr, gbufs ? gbufs->seed : nullptr, stats ? stats + 5 : nullptr);
+    e = launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, seed,
+                        stats ? stats + 5 : nullptr);
     if (e != hipSuccess) return e;
   }
   if (exact_scratch) {
@@ -2373,38 +1877,10 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
   return hipSuccess;
 }
 
-hipError_t launch_nn_brute_list(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
-                                const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand, float* ckey,
-                                int* ncand, int* ctie, int max_chunks, const int* fb_list, const int* fb_count) {
-  return launch_nn_brute(st, S, B, nodes, N, p, fr, pk, pi, cand, ckey, ncand, ctie, max_chunks, fb_list, fb_count);
-}
-
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
-                           float* ckey, int* ncand, int* ctie, float* seed, const DeltaGrid* dg) {
+                           float* ckey, int* ncand, int* ctie, float* seed) {
   if (count <= 0 || B <= 0) return hipSuccess;
-  if (dg && count <= dg->cap) {
-    const NnRec* base = nodes + first;
-    hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 255) / 256), dim3(256), 0, st, B, p.sort_limit, ckey, ncand, seed);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_dg_init, dim3((DG_NC + 1 + 255) / 256), dim3(256), 0, st, *dg);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_dg_bounds, dim3(1), dim3(256), 0, st, base, count, fr, *dg);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_dg_count, dim3((count + 255) / 256), dim3(256), 0, st, base, count, fr, *dg);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_dg_scan, dim3(1), dim3(1024), 0, st, *dg);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_dg_scatter, dim3((count + 255) / 256), dim3(256), 0, st, base, count, fr, *dg);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_nn_delta_grid, dim3(2 * ((B + 63) / 64)), dim3(64), 0, st, S, B, base, p, fr, *dg, seed, pk,
-                       pi);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 255) / 256), dim3(256), 0, st, B, 1, p.sort_limit, pk, pi, first,
-                       cand, ckey, ncand, ctie);
-    LAUNCH_CHECK();
-    return hipSuccess;
-  }
   const int groups = (B + 255) / 256;
   int nchunks = (count + 255) / 256;
   const int want = max(1, 2048 / max(1, groups));
@@ -2415,7 +1891,7 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
   hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 255) / 256), dim3(256), 0, st, B, p.sort_limit, ckey, ncand, seed);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes + first, count, chunk,
-                     nchunks, p, fr, pk, pi, nullptr, nullptr, nullptr, nullptr, nullptr, seed, nullptr);
+                     nchunks, p, fr, pk, pi, seed, nullptr);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      first, cand, ckey, ncand, ctie);
@@ -2434,9 +1910,8 @@ hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, co
 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                   const DevParams& p, const NnFrame& fr, float* pk, int* pi, int* cand,
-                                  float* ckey, int* ncand, int* ctie, int max_chunks, const int* sidx,
-                                  const int* scount, const float4* tbox, const float* tcost, const int* home,
-                                  const float* seed, unsigned long long* tstat) {
+                                  float* ckey, int* ncand, int* ctie, int max_chunks, const float* seed,
+                                  unsigned long long* tstat) {
   int threads = 256;
   int groups = (B + 255) / 256;
   int nchunks = (N + 255) / 256;
@@ -2447,10 +1922,10 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
   chunk = (chunk + 255) & ~255;  // tiles of 256 nodes never straddle chunks
   nchunks = (N + chunk - 1) / chunk;
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(threads), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, fr, pk, pi, sidx, scount, tbox, tcost, home, seed, tstat);
+                     p, fr, pk, pi, seed, tstat);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
-                     cand, ckey, ncand, ctie, sidx, scount);
+                     cand, ckey, ncand, ctie);
   LAUNCH_CHECK();
   return hipSuccess;
 }
@@ -2513,43 +1988,22 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   RollInit* pr = (RollInit*)prep;
   RollArgs a = a0;
   a.B = B;
-  // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then the reference-point cache:
-  // whatever the tables leave of the 160 KB a workgroup may use (the glibc tables take ~10 KB of static
-  // LDS), up to 32 points x 256 lanes
-  const size_t obs_lds = a.p.need_gap ? 0 : (roll_lds_bytes(a0) + 15) / 16 * 16;
-  {
-    const size_t budget = 160 * 1024 - 12 * 1024;
-    const int n = obs_lds < budget ? (int)std::min<size_t>(32, (budget - obs_lds) / (256 * sizeof(double2))) : 0;
-    a.pcache_n = a.pcache_enable && n >= 4 ? n : 0;
-    a.pcache_off = (int)obs_lds;
-  }
-  const size_t lds = obs_lds + (size_t)a.pcache_n * 256 * sizeof(double2);
-  const void* fn = a.p.need_gap ? (a.cont ? (const void*)&k_roll_run<true, true> : (const void*)&k_roll_run<true, false>)
-                                : (a.cont ? (const void*)&k_roll_run<false, true> : (const void*)&k_roll_run<false, false>);
+  // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP)
+  const size_t lds = a.p.need_gap ? 0 : (roll_lds_bytes(a0) + 15) / 16 * 16;
+  const void* fn = a.p.need_gap ? (const void*)&k_roll_run<true> : (const void*)&k_roll_run<false>;
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
-  int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
-  if (a.cont) {
-    // hand-off absorbers wait for every donor wave of the grid: the grid must be resident at once
-    int occ = 0, dev = 0, ncu = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, lds)) != hipSuccess) return e;
-    nb = std::max(1, std::min(nb, std::max(1, occ) * ncu));
-  }
-  a.cont_donors = nb * 3;  // waves 1..3 of each block (launch_bounds 256)
+  const int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
   if (a.p.need_gap) {
     hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    if (a.cont) hipLaunchKernelGGL((k_roll_run<true, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
-    else hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    hipLaunchKernelGGL((k_roll_run<true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    if (a.cont) hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
-    else hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    hipLaunchKernelGGL((k_roll_run<false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   }
   LAUNCH_CHECK();
   return hipSuccess;

@@ -55,9 +55,6 @@ namespace clrrt {
 #ifndef WALK_APBINS
 #define WALK_APBINS 8  // ang_par sectors (top key bits)
 #endif
-#ifndef WALK_THBINS
-#define WALK_THBINS 1  // heading sectors within an ang_par sector (1: none)
-#endif
 #ifndef WALK_SECTOR_BITS
 #define WALK_SECTOR_BITS 3
 #endif
@@ -99,17 +96,7 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   const float a = (float)nodes[i].ang_par;
   int bin = (int)floorf((a + 3.14159265f) * (WALK_APBINS / 6.2831853f));
   bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
-#if WALK_THBINS > 1
-  // then the heading octant: tiles of similar headings sharpen the turning bound
-  const float th = atan2f(-nodes[i].s, nodes[i].c);  // (c, s) = (cos, sin)(-heading)
-  int tb = (int)floorf((th + 3.14159265f) * (WALK_THBINS / 6.2831853f));
-  tb = tb < 0 ? 0 : (tb >= WALK_THBINS ? WALK_THBINS - 1 : tb);
-  bin = bin * WALK_THBINS + tb;
-  keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | ((uint64_t)k << (32 - WALK_SECTOR_BITS)) |
-            (__float_as_uint(nodes[i].costE) >> (WALK_SECTOR_BITS + 0));
-#else
   keys[i] = ((uint64_t)bin << 61) | ((uint64_t)k << 29) | (__float_as_uint(nodes[i].costE) >> 3);
-#endif
   vals[i] = i;
 }
 
@@ -302,27 +289,10 @@ __device__ __forceinline__ void walk_key_range(float tx, float ty, float pos_err
   const float t2 = tx * tx + ty * (ty - 2.f * rho);  // dc^2 - rho^2
   if (t2 <= -0.01f) {
     // surely inside the circle: dubins_key's inside branch, rho (alpha + asin(qx / df) - asin(rho sin(alpha)
-    // / df)) with alpha = 2 pi - acos((5 rho^2 - df^2) / (4 rho^2)) (>= rho pi = 14.98 anywhere), restated
-    // with atan2: asin(qx / df) = atan2(qx, qy + rho), sin(alpha) = -sqrt(1 - c^2).  Its gradient grows
-    // like 1 / sqrt(1 - c^2) and df / sqrt(df^2 - (rho sin alpha)^2): the margin carries those factors,
-    // and near their poles the plain rho pi bound stays (tests/test_nnwalk_bounds.py, jittered offsets)
+    // / df)) with alpha = 2 pi - acos((5 rho^2 - df^2) / (4 rho^2)), is >= rho pi = 14.98 anywhere
+    // (a tighter bracket cut exact keys 3x but cost more in the visits: cfg3 0.94 -> 0.89 M nodes/s)
     lo = 14.9f;
     hi = __builtin_inff();
-#ifdef WALK_INSIDE_BRACKET  // off: it cuts exact keys 3x but costs more in the visits (cfg3 0.94 -> 0.89 M nodes/s)
-    const float df2 = tx * tx + (ty + rho) * (ty + rho);
-    const float cA = fminf(fmaxf((5.f * rho * rho - df2) * (1.f / (4.f * rho * rho)), -1.f), 1.f);
-    const float sA = fsqrt(fmaxf((1.f - cA) * (1.f + cA), 0.f));
-    const float u = rho * sA;
-    const float w = fsqrt(fmaxf(df2 - u * u, 0.f));
-    const float cw = w * frcp(fsqrt(df2));
-    if (sA >= 0.05f && cw >= 0.05f) {
-      const float alpha = 6.28318531f - atan2_apx(sA, cA);
-      const float L = rho * (alpha + atan2_apx(tx, ty + rho) + atan2_apx(u, w));
-      const float m = 2e-3f + 1e-4f * L + pos_err * (8.f + 8.f * frcp(sA) + 8.f * frcp(cw));
-      lo = fmaxf(L - m, 14.9f);
-      hi = L + m;
-    }
-#endif
     return;
   }
   if (!(t2 > -0.01f)) {  // NaN
@@ -980,6 +950,12 @@ __global__ void __launch_bounds__(64) k_walk_merge(const int* __restrict__ ovf_n
   walk_emit(lk, li, lane, s, sort_limit, cand, ckey, ncand, ctie);
 }
 
+int64_t walk_tile_count(int64_t n) {
+  const int64_t sz = WALK_TILE * WALK_SUPER;
+  return (n + sz - 1) / sz * WALK_SUPER;
+}
+int64_t walk_super_count(int64_t n) { return walk_tile_count(n) / WALK_SUPER; }
+
 size_t walk_sort_bytes(int n) {
   size_t bytes = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
@@ -1076,6 +1052,7 @@ hipError_t launch_nn_walk(hipStream_t st, const clrrt_sample* S, int B, const Nn
 hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const NnFrame& fr, double x0, double y0,
                                 double x1, double y1, WalkBufs& w, const WalkBufs* prev) {
   if (N <= 0) return hipSuccess;
+  if (N > w.cap_nodes) return hipErrorInvalidValue;  // the buffers' shapes (alloc_walk)
   const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   const double span = fmax(x1 - x0, y1 - y0);
@@ -1146,6 +1123,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
                                  bool stateless) {
   if (N <= 0 || B <= 0) return hipSuccess;
+  if (N > w.cap_nodes || B > w.cap_batch) return hipErrorInvalidValue;
   const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   const double span = fmax(x1 - x0, y1 - y0);
@@ -1185,6 +1163,11 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
     // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
     // claimed records exit at once) and the merge
     const int nl = (nsup + w.nch - 1) / w.nch;
+    if (2 * sizeof(float) * (size_t)nl > 64 * 1024) {
+      e = hipFuncSetAttribute((const void*)&k_walk_search<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(2 * sizeof(float) * (size_t)nl));
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL((k_walk_search<true, true>), dim3(w.max_over * w.nch), dim3(64), 2 * sizeof(float) * (size_t)nl,
                        st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
                        ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 7
+#define CLRRT_ABI_VERSION 8
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -397,23 +397,15 @@ int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
 int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
 
-/* Nearest-node search strategy (every strategy returns the identical candidate lists): trees of at
- * least `min_nodes` nodes search the samples whose mode bit is set in `modes` (1 = explore,
- * 2 = optimize) through the per-round spatial grid index, the rest by brute force.  A wave of the
- * grid search that has read `wave_budget` node records (0: automatic) hands its unfinished samples
- * to brute force.  Default: off (min_nodes = INT64_MAX; the brute-force search with its prefilter
- * is faster on the benchmark trees), modes 1 (explore), automatic budget. */
-int clrrt_set_nn_grid(clrrt_ctx* ctx, int64_t min_nodes, int32_t modes, int32_t wave_budget);
 /* Execution knobs (results never depend on them): "roll_persistent" (1: candidate rollouts run on
  * persistent waves with a job queue, default; 0: one lane per candidate), "roll_blocks" (persistent
- * blocks of 256 lanes; 0: two per compute unit), "nn_ordered_min" (trees of at least this many
- * nodes use the place-ordered brute-force search that skips far node tiles; default: never). */
+ * blocks of 256 lanes; 0: by tree size), "nn_walk_min" (trees of at least this many nodes use the
+ * walk search, default 8192; below it the brute force), "nn_walk_stateless", "nn_walk_budget_tiles",
+ * "nn_walk_budget_keys", "nn_walk_chunks", "nn_walk_max_over", "nn_walk_double", "nn_pipeline",
+ * "roll_priority", "side_priority" (see clrrt_capi.hip). */
 int clrrt_set_option(clrrt_ctx* ctx, const char* key, int64_t value);
-/* Nearest-node search diagnostics since the last clrrt_reset_counters.  Grid search: out[0] waves,
- * out[1] node records read, out[2] rings walked, out[3] waves stopped by the read budget, out[4]
- * samples handed to brute force by the LAST search.  Brute force: out[5] / out[6] node tiles
- * considered / searched (place-ordered strategy), out[7] (sample, node) pairs passing the float
- * prefilter, out[8] exact Dubins keys evaluated.  Walk search: out[10] super-tiles visited, out[11]
+/* Nearest-node search diagnostics since the last clrrt_reset_counters.  out[0..6] unused (0).  Brute
+ * force: out[7] (sample, node) pairs passing the float prefilter, out[8] exact Dubins keys evaluated.  Walk search: out[10] super-tiles visited, out[11]
  * tiles visited, out[12] nodes passing the prefilter, out[13] exact Dubins keys evaluated, out[14..18]
  * shader clocks per phase when the "nn_debug" option is 2 (diagnostics). */
 int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[19]);

@@ -36,13 +36,10 @@ def _scene(kind):
 
 
 def _nn_strategy(pl, name):
-    """Select the nearest-node search: 'brute' (node order), 'ordered' (place-ordered brute force with
-    tile skipping), 'grid' (wave-uniform grid search + brute-force fallback) or 'walk' (one wave per
-    sample over place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes).  'walk_split*':
+    """Select the nearest-node search: 'brute' (node order) or 'walk' (one wave per sample over
+    place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes).  'walk_split*':
     the walk with a budget of one tile, so every sample hands its search to the split waves and the
     merge (the overflow path of large trees), 7 waves per sample (odd interleave)."""
-    pl.set_nn_grid(0 if name == "grid" else 1 << 40, 3, 0)
-    pl.set_option("nn_ordered_min", 0 if name == "ordered" else 1 << 40)
     pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
     pl.set_option("nn_walk_stateless", name.endswith("stateless"))
     split = name.startswith("walk_split")
@@ -99,9 +96,7 @@ def test_rollout_parity(kind):
     assert flips == 0 and not drift
 
 
-@pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "grid"),
-                                           ("obb200", "grid"), ("empty", "ordered"), ("obb200", "ordered"),
-                                           ("empty", "walk"), ("obb200", "walk"), ("moving", "walk"),
+@pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "walk"), ("obb200", "walk"), ("moving", "walk"),
                                            ("obb200", "walk_stateless"), ("obb200", "walk_split"),
                                            ("moving", "walk_split"), ("obb200", "walk_split_stateless")])
 def test_nearest_node_parity(kind, strategy):
@@ -140,9 +135,7 @@ def _compare_trees(o, pl, label):
 
 @pytest.mark.parametrize("kind,seed,iters,strategy", [("empty", 1, 200, "brute"), ("obb200", 3, 300, "brute"),
                                                       ("empty", 2, 300, "brute"), ("obb200", 5, 300, "brute"),
-                                                      ("moving", 4, 250, "brute"), ("obb200", 3, 300, "grid"),
-                                                      ("moving", 4, 250, "grid"), ("obb200", 5, 300, "ordered"),
-                                                      ("moving", 4, 250, "ordered"), ("empty", 1, 200, "walk"),
+                                                      ("moving", 4, 250, "brute"), ("empty", 1, 200, "walk"),
                                                       ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk"),
                                                       ("obb200", 5, 300, "walk_stateless"),
                                                       ("obb200", 3, 300, "walk_split")])
@@ -181,10 +174,8 @@ def test_exact_mode_tree_parity(kind, seed, iters, strategy):
 
 
 @pytest.mark.parametrize("kind,batch,strategy,persistent", [("empty", 64, "brute", 1), ("obb200", 256, "brute", 1),
-                                                             ("moving", 128, "brute", 1), ("obb200", 256, "grid", 1),
-                                                             ("moving", 128, "grid", 1), ("obb200", 256, "brute", 0),
-                                                             ("obb200", 256, "ordered", 1),
-                                                             ("moving", 128, "ordered", 1), ("empty", 64, "walk", 1),
+                                                             ("moving", 128, "brute", 1), ("obb200", 256, "brute", 0),
+                                                             ("empty", 64, "walk", 1),
                                                              ("obb200", 256, "walk", 1), ("moving", 128, "walk", 1)])
 def test_batch_mode_tree_parity(kind, batch, strategy, persistent):
     mode, obs = _scene(kind)
@@ -284,10 +275,9 @@ def test_exact_mode_bitwise(kind, seed, iters):
         assert np.array_equal(rows.view(np.uint64), np.ascontiguousarray(o.rows(i)).view(np.uint64)), i
 
 
-def test_nn_grid_matches_brute_force_large_tree():
-    """Full-size property: on a BATCH-grown tree of ~100k nodes the grid, place-ordered and walk
-    searches return exactly the brute-force candidate lists (ids and keys) for every sample of a
-    16384-sample batch."""
+def test_walk_matches_brute_force_large_tree():
+    """Full-size property: on a BATCH-grown tree of ~100k nodes the walk searches return exactly the
+    brute-force candidate lists (ids and keys) for every sample of a 16384-sample batch."""
     mode, obs = _scene("obb200")
     pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                        max_batch=16384)
@@ -299,7 +289,7 @@ def test_nn_grid_matches_brute_force_large_tree():
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    for strategy in ("grid", "ordered", "walk", "walk_stateless"):
+    for strategy in ("walk", "walk_stateless"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
@@ -317,22 +307,16 @@ def test_nn_grid_matches_brute_force_large_tree():
 @pytest.mark.gpu
 def test_pipelined_batch_rounds_identical():
     """Full-size property: BATCH rounds with the next round's walk search overlapped with the current
-    round's rollouts (+ the merge of the appended nodes, launch_nn_delta), and rounds whose last
-    rollouts move between waves (roll_handoff), grow exactly the tree of plain rounds (every node
-    record and trajectory row).  So do the scheduling and search options: the rollout queue order
-    (roll_priority), the persistent grid width (roll_blocks), the reference-point cache
-    (roll_point_cache), the single-buffered walk index (nn_walk_double), the walk without overflow
-    split (budget 0) or with every sample split (budget 1), the appended-node search through the grid
-    instead of the chunked brute force (nn_delta_grid) and the next index built on the side stream
-    (nn_side_build)."""
+    round's rollouts (+ the merge of the appended nodes, launch_nn_delta) grow exactly the tree of
+    plain rounds (every node record and trajectory row).  So do the scheduling and search options: the
+    rollout queue order (roll_priority), the persistent grid width (roll_blocks), the single-buffered
+    walk index (nn_walk_double) and the walk without overflow split (budget 0) or with every sample
+    split (budget 1)."""
     mode, obs = _scene("obb200")
     trees = []
-    variants = [dict(nn_pipeline=0, roll_handoff=0), dict(nn_pipeline=1, roll_handoff=0),
-                dict(nn_pipeline=1, roll_handoff=1), dict(roll_priority=0, roll_blocks=512),
-                dict(roll_point_cache=1, nn_walk_double=0),
-                dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
-                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5),
-                dict(nn_delta_grid=1, nn_side_build=1)]
+    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(roll_priority=0, roll_blocks=512),
+                dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
+                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
@@ -349,29 +333,6 @@ def test_pipelined_batch_rounds_identical():
     assert trees[0][2] > 20000
     for t in trees[1:]:
         assert trees[0][0] == t[0] and trees[0][1] == t[1]
-
-
-@pytest.mark.gpu
-def test_delta_grid_matches_chunked_large_tree():
-    """The appended-node search through the grid (k_nn_delta_grid) against the chunked brute force
-    (k_nn_partial) over 40 pipelined cfg3 rounds (trees past 250 k nodes, where the appended records are
-    a small fraction of the tree): identical trees, record for record and row for row."""
-    mode, obs = _scene("obb200")
-    trees = []
-    for grid in (1, 0):
-        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 27,
-                           max_batch=16384)
-        pl.set_option("nn_delta_grid", grid)
-        pl.set_obstacles(obs)
-        pl.tree_init()
-        st = pl.expand(clrrt.Rng(21), n_iters=16384 * 40, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
-        assert st["rounds"] == 40
-        n, nr = pl.size()
-        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n))
-        pl.close()
-    print(f"delta grid: {trees[0][2]} nodes")
-    assert trees[0][2] > 200000
-    assert trees[0][0] == trees[1][0] and trees[0][1] == trees[1][1]
 
 
 @pytest.mark.gpu

@@ -9,5 +9,5 @@ out=../../build/$1; mkdir -p $out
 /opt/rocm/bin/hipcc $FLAGS $2 -c -o $out/k.o clrrt_kernels.hip &
 /opt/rocm/bin/hipcc $FLAGS $2 -c -o $out/w.o clrrt_nnwalk.hip &
 wait
-/opt/rocm/bin/hipcc $FLAGS -shared -o $out/libclrrt.so $out/k.o clrrt_nngrid.o $out/w.o clrrt_capi.o
+/opt/rocm/bin/hipcc $FLAGS -shared -o $out/libclrrt.so $out/k.o $out/w.o clrrt_capi.o
 rm -f $out/k.o $out/w.o
