@@ -136,6 +136,12 @@ struct clrrt_ctx {
   // then merges in the nodes it appended (launch_nn_delta) and the buffers swap
   int nn_pipeline = 1;  // option "nn_pipeline"
   hipStream_t side = nullptr;
+  // option "cu_split" (k = 1..7): the rollouts run on their own stream restricted to k/8 of the CUs and
+  // the side stream (the next round's search) on the other CUs, so no search wave shares a SIMD with a
+  // rollout wave; 0: one unrestricted main stream for both (default)
+  int cu_split = 0;
+  hipStream_t roll_st = nullptr;
+  hipEvent_t ev_rs0 = nullptr, ev_rs1 = nullptr;
   hipEvent_t ev_tree = nullptr, ev_walk = nullptr, ev_commit = nullptr;
   clrrt_sample* d_samples2 = nullptr;
   clrrt_sample* h_samples2 = nullptr;
@@ -403,6 +409,9 @@ static void free_all(clrrt_ctx* c) {
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
   if (c->ev_commit) hipEventDestroy(c->ev_commit);
   if (c->side) hipStreamDestroy(c->side);
+  if (c->roll_st) hipStreamDestroy(c->roll_st);
+  if (c->ev_rs0) hipEventDestroy(c->ev_rs0);
+  if (c->ev_rs1) hipEventDestroy(c->ev_rs1);
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
   if (c->h_bbox) hipHostFree(c->h_bbox);
@@ -1103,6 +1112,27 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
+  else if (k == "cu_split" && value >= 0 && value <= 7) {
+    HIPC(c, hipStreamSynchronize(c->side));
+    if (c->roll_st) HIPC(c, hipStreamSynchronize(c->roll_st));
+    HIPC(c, hipStreamDestroy(c->side));
+    c->side = nullptr;
+    if (c->roll_st) HIPC(c, hipStreamDestroy(c->roll_st));
+    c->roll_st = nullptr;
+    c->cu_split = (int)value;
+    if (value == 0) {
+      HIPC(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    } else {
+      // CU i goes to the rollouts when i mod 8 < k: k/8 of every run of 8 CU indices
+      const int nw = (c->n_cu + 31) / 32;
+      std::vector<uint32_t> mr(nw, 0u), ms(nw, 0u);
+      for (int i = 0; i < c->n_cu; i++) ((i % 8) < value ? mr : ms)[i / 32] |= 1u << (i % 32);
+      HIPC(c, hipExtStreamCreateWithCUMask(&c->roll_st, (uint32_t)nw, mr.data()));
+      HIPC(c, hipExtStreamCreateWithCUMask(&c->side, (uint32_t)nw, ms.data()));
+      if (!c->ev_rs0) HIPC(c, hipEventCreateWithFlags(&c->ev_rs0, hipEventDisableTiming));
+      if (!c->ev_rs1) HIPC(c, hipEventCreateWithFlags(&c->ev_rs1, hipEventDisableTiming));
+    }
+  }
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
     HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1390,8 +1420,16 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     if (rc != CLRRT_OK) return rc;
   }
   if (during_roll) HIPC(c, hipEventRecord(c->ev_tree, st));
+  // the rollouts' stream: the main one, or (cu_split) their CU-restricted stream, ordered after the
+  // main stream's work so far and joined back right after the launch
+  hipStream_t rst = st;
+  if (c->roll_st) {
+    rst = c->roll_st;
+    HIPC(c, hipEventRecord(c->ev_rs0, st));
+    HIPC(c, hipStreamWaitEvent(rst, c->ev_rs0, 0));
+  }
   {
-    KTimer kt(c, 1);
+    KTimer kt(c, 1, rst);
     RollArgs a = roll_args(c, n * CAND_K);
     a.res = c->res_spec;
     a.res_gb = c->res_gb;
@@ -1407,15 +1445,20 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     const int64_t nt = c->n_nodes;
     const int eighths = nt < 300000 ? 7 : nt < 700000 ? 5 : nt < 1100000 ? 4 : 3;
     const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu)
+                       : c->cu_split > 0  ? std::max(1, (c->cu_split * c->n_cu) / 8)
                                           : std::max(1, (eighths * c->n_cu) / 8);
     if (c->roll_priority) {
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
     }
     if (c->roll_persistent && c->dp.n_steps_max > 0)
-      HIPC(c, launch_rollout_persistent(st, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
+      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
     else
-      HIPC(c, launch_rollout(st, SRC_SPEC, a));
+      HIPC(c, launch_rollout(rst, SRC_SPEC, a));
+  }
+  if (c->roll_st) {
+    HIPC(c, hipEventRecord(c->ev_rs1, rst));
+    HIPC(c, hipStreamWaitEvent(st, c->ev_rs1, 0));
   }
   if (during_roll) {  // queued behind the rollout kernel, whose persistent blocks take the CUs first
     int rc = during_roll();
