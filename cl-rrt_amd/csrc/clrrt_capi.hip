@@ -114,6 +114,7 @@ struct clrrt_ctx {
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
+  int roll_coop = 1;          // option "roll_coop": wave-cooperative collision checks in k_roll_run
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
@@ -1112,6 +1113,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
+  else if (k == "roll_coop") c->roll_coop = value != 0;
   else if (k == "cu_split" && value >= 0 && value <= 7) {
     HIPC(c, hipStreamSynchronize(c->side));
     if (c->roll_st) HIPC(c, hipStreamSynchronize(c->roll_st));
@@ -1447,6 +1449,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     const int blocks = c->roll_blocks > 0 ? std::min(c->roll_blocks, 4 * c->n_cu)
                        : c->cu_split > 0  ? std::max(1, (c->cu_split * c->n_cu) / 8)
                                           : std::max(1, (eighths * c->n_cu) / 8);
+    a.coop_enable = c->roll_coop;
     if (c->roll_priority) {
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;

@@ -105,6 +105,8 @@ struct RollArgs {
   int* perm;
   int* pflag;
   int B;
+  int coop_off;     // k_roll_run's cooperative collision scratch: byte offset in the dynamic LDS
+  int coop_enable;  // option "roll_coop": use it where it applies (launch_rollout_persistent)
 };
 
 struct SelArgs {

@@ -520,44 +520,18 @@ struct PhaseClk {
   }
 };
 
-// One Euler step of Simulation::propagate (simulation.cpp:58-137).  Fills the logged row columns
-// 7..9 and returns CLRRT_ROLL_* or -1 to continue.
-template <bool NEED_GAP>
-__device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
-                                         double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr,
-                                         int = 0) {
+// One Euler step of Simulation::propagate (simulation.cpp:58-137), in two parts around the collision
+// check: roll_step_pre (controls, ODE, the heading's trigonometry; fills the logged row columns 7..9,
+// returns the heading rate for the lateral-acceleration test) and roll_step_post (costs, limits, end
+// and goal tests with the checkObsDistance value Dobs; returns CLRRT_ROLL_* or -1 to continue).
+__device__ __forceinline__ double roll_step_pre(Roll& r, const DevParams& p, double& col7, double& col8,
+                                                double& col9, WorkCtr& w, PhaseClk* pc) {
   double Px, Py;
   // Controller::getControls (controller.cpp:30-34): waypoint, steer, accel
   w.scan += (uint32_t)(r.R.N - r.wp);
   double dla = update_waypoint(r, p, Px, Py, false);
-#ifdef CLRRT_DUP_WP
-  {
-    double z = 0.0;
-    asm volatile("" : "+v"(z));
-    const double Pxb = r.x0 + z + dla * 1.0 * glibc::cos(r.x2 + z);
-    const double Pyb = r.x1 + z + dla * 1.0 * glibc::sin(r.x2 + z);
-    Px = fmin(Px, Pxb); Py = fmin(Py, Pyb);
-  }
-#endif
   if (pc) pc->mark(1);
   double ym = lateral_error(r, Px, Py);
-#ifdef CLRRT_DUP_LAT
-  {
-    double z = 0.0;
-    asm volatile("" : "+v"(z));
-    ym = fmin(ym, lateral_error(r, Px + z, Py));
-  }
-#endif
-#ifdef CLRRT_DUP_SCAN
-  {
-    double z = 0.0;
-    asm volatile("" : "+v"(z));
-    Roll r2 = r;
-    r2.wp = r.wp - (r.wp > 0 ? 1 : 0);  // rescan from the previous waypoint (same argmin region)
-    scan_waypoint(r2, Px + z, Py, false);
-    ym = fmin(ym, ym + (double)(r2.wp - r.wp) * z);
-  }
-#endif
   const double dc = steer_cmd(r, p, dla, ym);
   const double vref = prof_v(r.P, r.wp + 2);  // ref.v[IDwp + 2]: the PI error and the logged column 8
   const double ac = accel_cmd(r, p, vref);
@@ -568,34 +542,15 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   r.t3 = glibc::tan(r.x3);
   r.cwp = glibc::cos(r.x2);  // independent of sincos / tan: their latencies overlap
   r.swp = glibc::sin(r.x2);
-#ifdef CLRRT_DUP_TRIG  // diagnostics: the phase evaluated twice (same values) to measure its cost
-  {
-    double z = 0.0;
-    asm volatile("" : "+v"(z));
-    double s2b, c2b;
-    glibc::sincos(r.x2 + z, s2b, c2b);
-    const double t3b = glibc::tan(r.x3 + z);
-    r.s2 = fmin(r.s2, s2b); r.c2 = fmin(r.c2, c2b); r.t3 = fmin(r.t3, t3b);
-  }
-#endif
   if (pc) pc->mark(3);
   col7 = (double)r.wp;
   col8 = vref;
   col9 = dc;
-  // collision (simulation.cpp:83-86)
-  double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);
-#ifdef CLRRT_DUP_COLL
-  {
-    double z = 0.0;
-    asm volatile("" : "+v"(z));
-    Roll r2 = r;
-    r2.x0 += z;
-    uint32_t tb = 0;
-    Dobs = fmin(Dobs, obs_distance<NEED_GAP>(r2, p, ov, tb));
-  }
-#endif
-  if (pc) pc->mark(4);
-  if (Dobs == 0) return CLRRT_ROLL_COLLISION;
+  return d2;
+}
+
+__device__ __forceinline__ int roll_step_post(Roll& r, const DevParams& p, double Dobs, double d2) {
+  if (Dobs == 0) return CLRRT_ROLL_COLLISION;  // simulation.cpp:83-86
   // costs (simulation.cpp:89-95)
   r.costE += r.x4 * p.dt;
   double kappa = r.t3 / p.L;
@@ -616,6 +571,121 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
   const double dg2 = ex * ex + ey * ey;
   if (dg2 <= 1.0000000000000004 && sqrt(dg2) <= 1 && (fabs(angle_diff(r.x2, p.g2)) < 0.05)) return CLRRT_ROLL_GOAL;
   return -1;
+}
+
+template <bool NEED_GAP>
+__device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsView& ov, double& col7,
+                                         double& col8, double& col9, WorkCtr& w, PhaseClk* pc = nullptr) {
+  const double d2 = roll_step_pre(r, p, col7, col8, col9, w, pc);
+  // collision (simulation.cpp:83-86)
+  const double Dobs = obs_distance<NEED_GAP>(r, p, ov, w.box);
+  if (pc) pc->mark(4);
+  return roll_step_post(r, p, Dobs, d2);
+}
+
+// Wave-cooperative checkObsDistance without the gap value (k_roll_run; OBB collision with the static
+// grid): the same value and box-test count as obs_distance<false> for every lane with act set, but
+// the SAT tests of all lanes run spread over the wave.  Each lane culls its own candidates (its grid
+// cell's static obstacles, then the moving ones) and queues the survivors (lane, obstacle) in LDS; the
+// queued pairs are then tested 64 at a time, one per lane, each against its owner's vehicle box, and
+// every overlap lowers the owner's first-overlap index.  The result only depends on whether some
+// survivor overlaps (Dobs = 0; checkObsDistance returns at its first overlap, old_collisioncheck.cpp:
+// 24-51) and, for the work counter, on the smallest overlapping index (the lists ascend, so that is the
+// reference's first overlap).  A lane outside the grid's float frame takes obs_distance itself.
+// Called by every lane of the wave (wave-uniform control flow).
+struct CoopLds {
+  Box4* veh;      // [64] vehicle boxes
+  double* t;      // [64] prediction time of each lane's step
+  int* hit;       // [64] smallest overlapping obstacle index (INT_MAX: none)
+  uint32_t* q;    // [cap] queued pairs: lane << 16 | moving << 15 | obstacle
+  int cap;
+};
+#define COOP_QCAP 512
+constexpr size_t kCoopLdsPerWave = 64 * sizeof(Box4) + 64 * sizeof(double) + 64 * sizeof(int) + COOP_QCAP * sizeof(uint32_t);
+
+__device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p, const ObsView& ov, uint32_t& tests,
+                                    const CoopLds& cl) {
+  const int lane = threadIdx.x & 63;
+  double t = 0.0, vpx = 0.0, vpy = 0.0;
+  float fvx = 0.f, fvy = 0.f, ft = 0.f;
+  bool use = false;  // this lane's check goes through the queue
+  int a = 0, ae = 0;
+  if (act) {
+    t = p.obs_use_pred ? r.x6 : 0.0;
+    vpx = r.x0 + 1.424 * r.c2;
+    vpy = r.x1 + 1.424 * r.s2;
+    fvx = (float)vpx; fvy = (float)vpy; ft = (float)t;
+    use = isfinite(fvx) && isfinite(fvy) && isfinite(ft);
+    if (use) {
+      const int gx = (int)floorf((fvx - ov.gx0) * ov.ginv), gy = (int)floorf((fvy - ov.gy0) * ov.ginv);
+      if (gx >= 0 && gx < ov.gw && gy >= 0 && gy < ov.gh) {
+        const int cell = gy * ov.gw + gx;
+        a = ov.gstart[cell];
+        ae = ov.gstart[cell + 1];
+      }
+    }
+  }
+  cl.hit[lane] = 0x7fffffff;
+  cl.t[lane] = t;
+  bool veh_done = false, need_veh = false;
+  int nq = 0;  // wave-uniform
+  auto flush = [&]() {
+    if (need_veh && !veh_done) {  // setVertices of the lanes with a queued survivor
+      Box4 vb;
+      veh_box(vpx, vpy, r.x2, vb);
+      cl.veh[lane] = vb;
+      veh_done = true;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i0 = 0; i0 < nq; i0 += 64) {
+      const int i = i0 + lane;
+      if (i < nq) {
+        const uint32_t e = cl.q[i];
+        const int owner = (int)(e >> 16), jj = (int)(e & 0x7fffu);
+        const Box4 vb = cl.veh[owner];
+        const float gap = (e & 0x8000u) ? obs_sat(vb, ov, jj, cl.t[owner]) : obs_sat_static(vb, ov, jj);
+        if (gap == 0) atomicMin(&cl.hit[owner], jj);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    nq = 0;
+  };
+  auto push = [&](bool surv, int jj, uint32_t mv) {
+    const uint64_t m = __ballot(surv);
+    const int c = __popcll(m);
+    if (c == 0) return;
+    if (nq + c > cl.cap) flush();
+    if (surv) {
+      cl.q[nq + __popcll(m & ((1ull << lane) - 1))] = ((uint32_t)lane << 16) | mv | (uint32_t)jj;
+      need_veh = true;
+    }
+    nq += c;
+  };
+  __builtin_amdgcn_wave_barrier();
+  for (int k = 0;; k++) {  // static candidates: the lane's grid cell list
+    const bool has = use && a + k < ae;
+    if (__ballot(has) == 0) break;
+    const int jj = has ? (int)ov.gitems[a + k] : 0;
+    push(has && !obs_culled(ov, jj, ft, fvx, fvy), jj, 0u);
+  }
+  for (int k = 0; k < ov.nmov; k++) {  // moving candidates (every lane)
+    const int jj = (int)ov.gmov[k];
+    push(use && !obs_culled(ov, jj, ft, fvx, fvy), jj, 0x8000u);
+  }
+  flush();
+  double D = 10000;
+  if (use) {
+    const int h = cl.hit[lane];
+    if (h != 0x7fffffff) {
+      tests += h + 1;
+      D = 0.0;
+    } else {
+      tests += ov.n;
+    }
+  } else if (act) {
+    D = obs_distance<false>(r, p, ov, tests);  // outside the float frame: the lane's own scan
+  }
+  return D;
 }
 
 // One stateArray row; es = element stride (1 for row-major rows, the job count for the slot
@@ -952,16 +1022,27 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
 #define CLRRT_ABANDON_EVERY 16
 #endif
 
-template <bool NEED_GAP>
 #ifndef CLRRT_ROLL_WAVES
 #define CLRRT_ROLL_WAVES 1
 #endif
+// COOP: the collision check is obs_distance_coop (OBB collision without the gap value, static grid built,
+// the per-wave LDS scratch after the obstacle tables at a.coop_off)
+template <bool NEED_GAP, bool COOP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLL_WAVES))) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
                                                   int* __restrict__ qnext, int* __restrict__ best, int B) {
   extern __shared__ float4 lds[];
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
   const int lane = threadIdx.x & 63;
+  CoopLds cl{};
+  if constexpr (COOP) {
+    char* base = (char*)lds + a.coop_off + (size_t)(threadIdx.x >> 6) * kCoopLdsPerWave;
+    cl.veh = (Box4*)base;
+    cl.t = (double*)(base + 64 * sizeof(Box4));
+    cl.hit = (int*)(base + 64 * sizeof(Box4) + 64 * sizeof(double));
+    cl.q = (uint32_t*)(base + 64 * sizeof(Box4) + 64 * sizeof(double) + 64 * sizeof(int));
+    cl.cap = COOP_QCAP;
+  }
   const int64_t slot = (int64_t)a.slot_rows * 10;
   const int64_t pass_stride = slot * a.slot_jobs;
   WorkCtr w{0, 0, 0};
@@ -1065,35 +1146,49 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       if (parked == 0 && qdone) break;
       continue;
     }
-    if (j < 0 || fin >= 0) continue;
-    steps++;
-    // The abandon check's load of best[s] is issued BEFORE this step's row stores: vmcnt counts loads
-    // and stores in issue order, so a load issued after the stores would wait for all ten of them to
-    // complete (measured: ~60% of the kernel's wave time); issued here it only waits for the previous
-    // step's stores, long retired.
-    const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
-    const int best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
-    if (pc) pc->mark(6);
-    int o = roll_step<NEED_GAP>(r, a.p, ov, c7, c8, c9, w, pc);
+    // the lanes with a rollout in flight take a step; with the cooperative collision check (COOP) the
+    // whole wave takes part in its SAT tests, so the check sits outside the lanes' divergent region
+    const bool act = j >= 0 && fin < 0;
+    if (!COOP && !act) continue;
+    int best_s = 0x7fffffff;
+    double d2 = 0.0;
+    if (act) {
+      steps++;
+      // The abandon check's load of best[s] is issued BEFORE this step's row stores: vmcnt counts loads
+      // and stores in issue order, so a load issued after the stores would wait for all ten of them to
+      // complete (measured: ~60% of the kernel's wave time); issued here it only waits for the previous
+      // step's stores, long retired.
+      const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
+      best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
+      if (pc) pc->mark(6);
+      d2 = roll_step_pre(r, a.p, c7, c8, c9, w, pc);
+    }
+    double Dobs;
+    if constexpr (COOP) {
+      Dobs = obs_distance_coop(act, r, a.p, ov, w.box, cl);
+      if (!act) continue;
+    } else {
+      Dobs = obs_distance<NEED_GAP>(r, a.p, ov, w.box);
+    }
+    if (pc) pc->mark(4);
+    int o = roll_step_post(r, a.p, Dobs, d2);
 #ifdef CLRRT_ROLL_PROFILE
     {
       unsigned it = r.scan_it, mx_ = it;
 #pragma unroll
       for (int q = 32; q > 0; q >>= 1) mx_ = max(mx_, (unsigned)__shfl_xor((int)mx_, q, 64));
       scan_sum += it;
-      const uint64_t act = __ballot(true);
-      if (lane == __ffsll((unsigned long long)act) - 1) {
+      const uint64_t actm = __ballot(true);
+      if (lane == __ffsll((unsigned long long)actm) - 1) {
         scan_wave += mx_;
-        scan_long += __popcll(act);  // active lanes of this wave step
-        scan_long_pts += 1;          // wave steps
+        scan_long += __popcll(actm);  // active lanes of this wave step
+        scan_long_pts += 1;           // wave steps
       }
       chain_steps++;
     }
 #endif
     w.steps++;
-#ifndef CLRRT_NO_ROWS
     store_row(a.slots + pass * pass_stride + j * slot + (int64_t)steps * 10, 1, r, c7, c8, c9);
-#endif
     if (pc) pc->mark(5);
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
@@ -1988,9 +2083,17 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   RollInit* pr = (RollInit*)prep;
   RollArgs a = a0;
   a.B = B;
-  // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP)
-  const size_t lds = a.p.need_gap ? 0 : (roll_lds_bytes(a0) + 15) / 16 * 16;
-  const void* fn = a.p.need_gap ? (const void*)&k_roll_run<true> : (const void*)&k_roll_run<false>;
+  // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then (COOP) the cooperative
+  // collision check's per-wave scratch, when the static grid is built and the whole fits the 160 KB a
+  // workgroup may use beside the glibc tables' static LDS (~12 KB)
+  const size_t obs_lds = a.p.need_gap ? 0 : (roll_lds_bytes(a0) + 15) / 16 * 16;
+  const bool coop = a.coop_enable && !a.p.need_gap && a.p.coll_mode == CLRRT_COLLISION_OBB && a.p.n_obs > 0 && a.grid.gw > 0 &&
+                    obs_lds + 4 * kCoopLdsPerWave <= 148 * 1024;
+  a.coop_off = (int)obs_lds;
+  const size_t lds = obs_lds + (coop ? 4 * kCoopLdsPerWave : 0);
+  const void* fn = a.p.need_gap ? (const void*)&k_roll_run<true, false>
+                   : coop       ? (const void*)&k_roll_run<false, true>
+                                : (const void*)&k_roll_run<false, false>;
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
   const int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
@@ -1998,12 +2101,15 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
     hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_roll_run<true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   } else {
     hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_roll_run<false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    if (coop)
+      hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    else
+      hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   }
   LAUNCH_CHECK();
   return hipSuccess;

@@ -19,8 +19,10 @@
  *
  * A node coming back from the device carries its reference in endpoint form: ref.x = {front, back},
  * ref.y = {front, back}, ref.v = {v.back()} — every field expandTree, feasibleNode, feasibleGoalBias,
- * getReference and Simulation read (rrtplanner.cpp:152,166,273-277,305).  Trajectories (Node::tra) are
- * complete.  The engine consumes the glibc rand() stream through its own restatement (clrrt_rng), so
+ * getReference and Simulation read (rrtplanner.cpp:152,166,273-277,305) — unless
+ * Engine::set_full_reference(true): then ref.x / ref.y / ref.v hold all N points, as the reference's own
+ * Node does (regenerated from the iterations' samples and the device's Simulation).  Trajectories
+ * (Node::tra) are complete.  The engine consumes the glibc rand() stream through its own restatement (clrrt_rng), so
  * the engine's rng must be seeded as the reference seeds rand() (Engine::srand); Engine::expandTree
  * advances the process's rand() by the same three draws per iteration, keeping both streams equal.
  */
@@ -140,13 +142,26 @@ class Engine {
     cap.max_batch = max_batch;
     cap.max_obstacles = max_obstacles;
     check(nullptr, clrrt_create(&p, &cap, device, &ctx_), "clrrt_create");
+    p_ = p;
   }
   ~Engine() { clrrt_destroy(ctx_); }
   Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
 
   clrrt_ctx* ctx() { return ctx_; }
-  void set_params(const clrrt_params& p) { check(ctx_, clrrt_set_params(ctx_, &p), "clrrt_set_params"); }
+  void set_params(const clrrt_params& p) {
+    check(ctx_, clrrt_set_params(ctx_, &p), "clrrt_set_params");
+    p_ = p;
+  }
+  /* Node::ref of the nodes an expansion appends: the endpoint form (default) or all N points of ref.x /
+   * ref.y / ref.v, so the Node equals the reference's field for field.  The full form is regenerated
+   * after each expansion: each iteration's sample is re-drawn from the stream (sampleAroundVehicle), the
+   * regular node's reference is getReference's LinearSpacedVector from the parent's ref.back() to the
+   * sample (reference.cpp:9-23; a sample whose line does not end at the node's ref.back() bit for bit
+   * produced no node), and ref.v -- and the goal-biased node's whole reference (getGoalReference,
+   * reference.cpp:27-69) -- come from the device's Simulation of the node (clrrt_simulate), whose end
+   * state must equal the node's.  Costs one rollout per appended node. */
+  void set_full_reference(bool on) { full_ref_ = on; }
 
   template <class ObsVec>
   void set_obstacles(const ObsVec& det) {
@@ -265,6 +280,7 @@ class Engine {
   int64_t run(RRTT& rrt, clrrt_rng& rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
               int64_t counters[4]) {
     if (!tree_synced(rrt)) load_tree(rrt);
+    const clrrt_rng rng0 = rng;
     clrrt_counters c0, c1;
     check(ctx_, clrrt_get_counters(ctx_, &c0), "clrrt_get_counters");
     clrrt_stats st;
@@ -282,6 +298,7 @@ class Engine {
         check(ctx_, clrrt_tree_rows(ctx_, hd.row_offset, hd.nrows, rows.data()), "clrrt_tree_rows");
         rrt.tree.push_back(node_from_c<typename std::decay<decltype(rrt.tree[0])>::type>(hd, rows.data()));
       }
+      if (full_ref_) full_references(rrt, first, h, rng0, st.iterations);
     }
     synced_ = n;
     if (!rrt.tree.empty()) {
@@ -297,7 +314,72 @@ class Engine {
     return st.iterations;
   }
 
+  /* The full references of the appended nodes rrt.tree[first ..] (headers h), see set_full_reference. */
+  template <class RRTT>
+  void full_references(RRTT& rrt, int64_t first, const std::vector<clrrt_node>& h, clrrt_rng rng0, int64_t iters) {
+    std::vector<clrrt_sample> smp((size_t)std::max<int64_t>(iters, 0));
+    if (iters > 0) check(ctx_, clrrt_draw_samples(&p_, &rng0, (int32_t)iters, smp.data()), "clrrt_draw_samples");
+    std::vector<clrrt_sim_case> q(h.size());
+    size_t j = 0;  // next sample
+    for (size_t k = 0; k < h.size(); k++) {
+      const clrrt_node& n = h[k];
+      const auto& par = rrt.tree[(size_t)n.parent];
+      clrrt_sim_case& c = q[k];
+      c = clrrt_sim_case{};
+      for (int i = 0; i < 10; i++) c.state[i] = i < (int)par.state.size() ? par.state[i] : 0.0;
+      const double bx = par.ref.x.back(), by = par.ref.y.back();
+      c.ax = bx;
+      c.ay = by;
+      c.vstart = par.ref.v.back();
+      // a regular node: the first remaining sample whose getReference line ends at the node's ref.back()
+      bool regular = false;
+      for (size_t t = j; t < smp.size() && !regular; t++) {
+        const double L = std::sqrt(std::pow(smp[t].x - bx, 2) + std::pow(smp[t].y - by, 2));
+        const int N = (int)std::round(L / p_.ref_res) + 1;  // reference.cpp:15
+        if (N < 2) continue;
+        const double hx = (smp[t].x - bx) / static_cast<double>(N - 1), hy = (smp[t].y - by) / static_cast<double>(N - 1);
+        double vx = bx, vy = by;
+        for (int i = 1; i < N; i++) { vx += hx; vy += hy; }
+        if (vx == n.ref_back[0] && vy == n.ref_back[1]) {
+          regular = true;
+          j = t + 1;
+          c.hx = hx; c.hy = hy; c.ref_n = N; c.goal_biased = 0;
+        }
+      }
+      if (!regular) {  // the goal-biased node of the regular node just before it (rrtplanner.cpp:163-173)
+        if (k == 0 || n.parent != first + (int64_t)k - 1)
+          throw Error("set_full_reference: an appended node matches no sample of the expansion");
+        c.goal_biased = 1;
+      }
+    }
+    // the cases are independent (each parent's ref.v.back() is in its header): chunks of 512
+    int32_t cap = 2048;
+    for (const auto& c : q) cap = std::max(cap, c.ref_n);
+    const size_t chunk = 512;
+    std::vector<clrrt_rollout_result> res(chunk);
+    std::vector<double> ref(3 * (size_t)cap * chunk);
+    for (size_t k0 = 0; k0 < q.size(); k0 += chunk) {
+      const size_t m = std::min(chunk, q.size() - k0);
+      check(ctx_, clrrt_simulate(ctx_, &q[k0], (int32_t)m, res.data(), nullptr, 0, ref.data(), cap), "clrrt_simulate");
+      for (size_t i = 0; i < m; i++) {
+        const clrrt_rollout_result& r = res[i];
+        const clrrt_node& hd = h[k0 + i];
+        const double* rx = &ref[3 * (size_t)cap * i];
+        if (r.ref_n < 1 || r.ref_n > cap) throw Error("set_full_reference: reference longer than the buffer");
+        bool same = r.nrows == hd.nrows && rx[r.ref_n - 1] == hd.ref_back[0] && rx[cap + r.ref_n - 1] == hd.ref_back[1];
+        for (int t = 0; t < 10 && same; t++) same = r.final_state[t] == hd.state[t];
+        if (!same) throw Error("set_full_reference: the re-simulated node differs from the expansion's");
+        auto& node = rrt.tree[(size_t)first + k0 + i];
+        node.ref.x.assign(rx, rx + r.ref_n);
+        node.ref.y.assign(rx + cap, rx + cap + r.ref_n);
+        node.ref.v.assign(rx + 2 * (size_t)cap, rx + 2 * (size_t)cap + r.ref_n);
+      }
+    }
+  }
+
   clrrt_ctx* ctx_ = nullptr;
+  clrrt_params p_{};
+  bool full_ref_ = false;
   int64_t synced_ = -1;  // nodes of RRT.tree the device holds (-1: unknown, reload)
   clrrt_node root_{}, last_{};
   clrrt_rng rng_{};

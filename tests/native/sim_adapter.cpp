@@ -6,8 +6,12 @@
 //     Python side to compare with the CPU oracle (tests/test_native_sim_adapter.py);
 //   * dropin::expandTree (rrtplanner.h:87) on a second tree whose size equals the synced one but whose root
 //     differs: the engine must reload it (the new nodes grow from the new root);
-//   * a reference that is no getReference line is refused.
-// Usage: sim_adapter <in.bin> <out.bin>; prints a summary, exit 0 on success.
+//   * a reference that is no getReference line is refused;
+//   * with <tree.in> <tree.out>: Engine::set_full_reference(true) on trees grown from a root built as
+//     addInitialNode builds it (rrtplanner.cpp:22-36), by expandTree iterations (EXACT) or one BATCH
+//     expandBudget call; writes every node's parent and full ref.x / ref.y / ref.v for the Python side to
+//     compare with the oracle's Node::ref.
+// Usage: sim_adapter <in.bin> <out.bin> [<tree.in> <tree.out>]; prints a summary, exit 0 on success.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -180,6 +184,52 @@ int main(int argc, char** argv) {
           if (c != 7 && b.tree[i].tra.front()[c] != rb.state[c]) ok = false;
     if (!ok) { printf("FAIL: expandTree grew a stale tree (grown %d)\n", grown); failures++; }
     if (rand() != clrrt_rng_next(&eng.rng())) { printf("FAIL: rand() streams diverged\n"); failures++; }
+  }
+  if (argc >= 5) {  // full references of grown trees
+    std::ifstream tin(argv[3], std::ios::binary);
+    std::ofstream tout(argv[4], std::ios::binary);
+    const int ntrees = rd<int32_t>(tin);
+    for (int q = 0; q < ntrees; q++) {
+      const int seed = rd<int32_t>(tin), iters = rd<int32_t>(tin), batch = rd<int32_t>(tin);
+      (void)rd<int32_t>(tin);
+      Node root;
+      root.state.resize(10);
+      for (double& v : root.state) v = rd<double>(tin);
+      const int N = (int)std::floor(std::sqrt(std::pow(1.0, 2) + std::pow(0.0, 2)) / 0.1);  // addInitialNode
+      root.ref.x = LinearSpacedVector(0, 1, N);
+      root.ref.y = LinearSpacedVector(0, 0, N);
+      root.ref.v.assign(N, root.state[4]);
+      root.ref.dir = 1;
+      root.parentID = -1;
+      root.tra = {root.state};
+      MyRRT t;
+      t.goalPose = goal;
+      t.tree = {root};
+      eng.invalidate();
+      eng.set_full_reference(true);
+      eng.srand(seed);
+      std::srand(seed);
+      if (batch == 0) {
+        for (int it = 0; it < iters; it++) clrrt_adapter::dropin::expandTree(veh, t, (void*)nullptr, det, vector<double>{0, 0, 0});
+      } else {
+        eng.expandBudget(t, eng.rng(), iters, 0.0, CLRRT_MODE_BATCH, batch, nullptr);
+      }
+      eng.set_full_reference(false);
+      const int32_t nn = (int32_t)t.tree.size();
+      tout.write((const char*)&nn, 4);
+      for (const auto& nd : t.tree) {
+        const int32_t hdr[2] = {nd.parentID, (int32_t)nd.ref.x.size()};
+        tout.write((const char*)hdr, sizeof hdr);
+        if (nd.ref.y.size() != nd.ref.x.size() || nd.ref.v.size() != nd.ref.x.size()) {
+          printf("FAIL: node reference arrays of unequal length\n");
+          failures++;
+        }
+        tout.write((const char*)nd.ref.x.data(), 8 * nd.ref.x.size());
+        tout.write((const char*)nd.ref.y.data(), 8 * nd.ref.x.size());
+        tout.write((const char*)nd.ref.v.data(), 8 * nd.ref.x.size());
+      }
+      printf("full references: tree %d (%s), %d nodes\n", q, batch ? "BATCH" : "EXACT", nn);
+    }
   }
   printf("sim_adapter: %d simulations, counters sim_count %lld fail_collision %lld; failures %d\n", n,
          (long long)eng.counters()[0], (long long)eng.counters()[1], failures);

@@ -309,12 +309,13 @@ def test_pipelined_batch_rounds_identical():
     """Full-size property: BATCH rounds with the next round's walk search overlapped with the current
     round's rollouts (+ the merge of the appended nodes, launch_nn_delta) grow exactly the tree of
     plain rounds (every node record and trajectory row).  So do the scheduling and search options: the
-    rollout queue order (roll_priority), the persistent grid width (roll_blocks), the single-buffered
+    rollout queue order (roll_priority), the persistent grid width (roll_blocks), the per-lane collision
+    checks instead of the wave-cooperative ones (roll_coop), the single-buffered
     walk index (nn_walk_double) and the walk without overflow split (budget 0) or with every sample
     split (budget 1)."""
     mode, obs = _scene("obb200")
     trees = []
-    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(roll_priority=0, roll_blocks=512),
+    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(roll_priority=0, roll_blocks=512), dict(roll_coop=0),
                 dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
                 dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
     for opts in variants:

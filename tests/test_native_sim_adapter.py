@@ -77,3 +77,61 @@ def test_native_simulation_adapter_matches_oracle(coll):
         outcomes.append(outcome)
     assert pos == len(buf)
     print("outcomes", np.bincount(outcomes, minlength=5))
+
+
+@pytest.mark.gpu
+def test_native_full_reference_nodes_match_oracle():
+    """Engine::set_full_reference (include/clrrt_adapter.hpp): nodes grown by expandTree (EXACT) and by a
+    BATCH expandBudget carry the reference's full Node::ref -- all N points of ref.x / ref.y / ref.v
+    (getReference / getGoalReference, reference.cpp:9-70, and generateVelocityProfile, :72-170) -- equal
+    to the oracle's, bit for bit, node for node."""
+    from oracle_binding import Oracle
+    assert os.path.exists(EXE), "tests/native/sim_adapter not built (make -C cl-rrt_amd/csrc)"
+    goal = (40.0, 0.0, 0.0, 0.0)
+    obs = T.scene(200, 0)
+    root = np.array([0.0, 0.0, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0, 0.0, 0.0])
+    trees = [(5, 120, 0), (6, 512, 128)]
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        tin, tout = os.path.join(td, "t.bin"), os.path.join(td, "tout.bin")
+        with open(fin, "wb") as f:
+            f.write(struct.pack("<iii", 1, len(obs), 0))
+            f.write(np.array(goal, dtype="<f8").tobytes())
+            f.write(np.ascontiguousarray(obs, dtype="<f8").tobytes())
+        with open(tin, "wb") as f:
+            f.write(struct.pack("<i", len(trees)))
+            for seed, iters, batch in trees:
+                f.write(struct.pack("<iiii", seed, iters, batch, 0))
+                f.write(root.astype("<f8").tobytes())
+        out = subprocess.run([EXE, fin, fout, tin, tout], capture_output=True, text=True, timeout=300)
+        print(out.stdout)
+        assert out.returncode == 0, out.stdout + out.stderr
+        buf = open(tout, "rb").read()
+    pos = 0
+    for seed, iters, batch in trees:
+        o = Oracle(T.params(1, goal), obs)
+        Oracle.srand(seed)
+        o.init_tree(root)
+        if batch:
+            o.expand_batch(iters, batch, stable=True)
+        else:
+            o.expand(iters)
+        (n,) = struct.unpack_from("<i", buf, pos); pos += 4
+        assert n == o.size() and n > 20, (seed, n, o.size())
+        on = o.nodes()
+        full = 0
+        for i in range(n):
+            par, N = struct.unpack_from("<ii", buf, pos); pos += 8
+            x = np.frombuffer(buf, "<f8", N, pos); pos += 8 * N
+            y = np.frombuffer(buf, "<f8", N, pos); pos += 8 * N
+            v = np.frombuffer(buf, "<f8", N, pos); pos += 8 * N
+            assert par == on["parent"][i], (seed, i)
+            ox, oy, ov = o.ref(i)
+            assert N == len(ox), (seed, i, N, len(ox))
+            for a, b in ((x, ox), (y, oy), (v, ov)):
+                assert np.array_equal(a.view(np.uint64), np.ascontiguousarray(b, dtype=np.float64).view(np.uint64)), (seed, i)
+            full += N > 2
+        print(f"tree seed {seed} ({'BATCH' if batch else 'EXACT'}): {n} nodes, {full} with full references")
+        assert full > 10
+    assert pos == len(buf)
+

@@ -26,6 +26,7 @@ for label, jl in (("1 lane", longest[:1]), ("8 lanes, 8 jobs", longest[:8]), ("6
                   ("65536 copies", longest[:1] * 65536), ("131072 copies", longest[:1] * 131072)):
     for rep in range(3):
         pl.reset_counters()
+        pl.enable_timing(True)  # resets the kernel timers (kernel_time accumulates)
         r = pl.simulate_batch(jl)
         ms, n = pl.kernel_time(1)
     steps = max(x["nrows"] - 1 for x in r)
@@ -35,6 +36,7 @@ for label, jl in (("1 lane", longest[:1]), ("8 lanes, 8 jobs", longest[:8]), ("6
 med = jobs[int(np.argsort(nr)[len(nr) // 2])]
 for label, jl in (("median job, 1 lane", [med]), ("median, 4096 copies", [med] * 4096)):
     for rep in range(3):
+        pl.enable_timing(True)
         r = pl.simulate_batch(jl)
         ms, n = pl.kernel_time(1)
     steps = max(x["nrows"] - 1 for x in r)

@@ -31,17 +31,24 @@ print("tree", pl.size()[0], "jobs", len(jobs), "longest rollouts (steps):", nr[o
 pl.enable_timing(True)
 for label, jl in (("1 lane, longest", [jobs[order[0]]]), ("1 lane, 2nd", [jobs[order[1]]]),
                   ("1 lane, 8th", [jobs[order[7]]]), ("64 copies of the longest", [jobs[order[0]]] * 64),
-                  ("1 lane, median", [jobs[order[len(order) // 2]]])):
+                  ("1 lane, median", [jobs[order[len(order) // 2]]]),
+                  ("64 distinct longest", [jobs[i] for i in order[:64]]),
+                  ("64 distinct, random", [jobs[i] for i in np.random.default_rng(3).choice(len(jobs), 64, False)]),
+                  ("longest + 63 random", [jobs[order[0]]] + [jobs[i] for i in
+                                                              np.random.default_rng(4).choice(len(jobs), 63, False)])):
     pl.reset_counters()
+    pl.enable_timing(True)  # resets the kernel timers (kernel_time accumulates)
     r = pl.simulate_batch(jl)
     ms, _ = pl.kernel_time(1)
     d = pl.debug_counters()
     steps = sum(x["nrows"] - 1 for x in r)
     lanes = len(jl)
+    smax = max(x["nrows"] - 1 for x in r)
     ph = np.array(d[32:40], dtype=np.float64) / max(1, steps)  # per lane-step (per lane clocks)
     tot = ph.sum()
     print(f"{label:28s} kernel {ms:.3f} ms, {steps // lanes} steps/lane, {tot:,.0f} clk per step "
-          f"({ms * 1e-3 * 2.4e9 / max(1, steps // lanes):,.0f} wall clk/step at 2.4 GHz)")
+          f"({ms * 1e-3 * 2.4e9 / max(1, steps // lanes):,.0f} wall clk/step at 2.4 GHz; longest lane {smax} steps, "
+          f"{ms * 1e-3 * 2.4e9 / max(1, smax):,.0f} wall clk per its step)")
     for nm, v in zip(NAMES, ph):
         if v > 0:
             print(f"    {nm:32s} {v:9,.0f} clk  {v / max(1, tot) * 100:5.1f}%")
