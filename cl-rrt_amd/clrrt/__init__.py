@@ -451,7 +451,7 @@ class Planner:
                 "walk_clk_visit": out[16], "walk_clk_drain": out[17], "walk_clk_total": out[18]}
 
     def debug_counters(self):
-        out = (C.c_int64 * 40)()
+        out = (C.c_int64 * 64)()
         self._chk(self.L.clrrt_debug_counters(self.h, out), "debug_counters")
         return list(out)
 

@@ -150,6 +150,19 @@ struct clrrt_ctx {
   float* ckey2 = nullptr;
   int* ncand2 = nullptr;
   int* ctie2 = nullptr;
+  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (expand_lag2).
+  // Lag 2 keeps a third list set (*3), a third walk index set and a second side stream (allocated on
+  // first use).
+  int nn_lag = 2;
+  clrrt_sample* d_samples3 = nullptr;
+  clrrt_sample* h_samples3 = nullptr;
+  int* cand3 = nullptr;
+  float* ckey3 = nullptr;
+  int* ncand3 = nullptr;
+  int* ctie3 = nullptr;
+  WalkBufs nnw3{};
+  hipStream_t side2 = nullptr;
+  hipEvent_t ev_lag[3] = {nullptr, nullptr, nullptr};
   // clrrt_round_prefetch: declared next samples; pf_state 1 = their walk was launched (lists in the
   // *2 buffers, merge pending), 2 = merged and swapped in for pf_samples
   std::vector<clrrt_sample> pf_next, pf_samples;
@@ -400,11 +413,19 @@ static void free_all(clrrt_ctx* c) {
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
                   c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
-                  c->cmp.tmp, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2};
+                  c->cmp.tmp, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->d_samples3, c->cand3, c->ckey3,
+                  c->ncand3, c->ctie3, c->nnw3.keys, c->nnw3.keys2, c->nnw3.vals, c->nnw3.vals2, c->nnw3.tmp, c->nnw3.P,
+                  c->nnw3.Q, c->nnw3.CE, c->nnw3.ID, c->nnw3.tiles, c->nnw3.supers, c->nnw3.sorder, c->nnw3.HEAD,
+                  c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
   if (c->h_samples2) hipHostFree(c->h_samples2);
+  if (c->h_samples3) hipHostFree(c->h_samples3);
+  if (c->side2) hipStreamSynchronize(c->side2);
+  if (c->side2) hipStreamDestroy(c->side2);
+  for (auto e : c->ev_lag)
+    if (e) hipEventDestroy(e);
   if (c->side) hipStreamSynchronize(c->side);
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
@@ -498,8 +519,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   }
   chk(dalloc(&c->d_bbox, 4));
   chk(hipHostMalloc((void**)&c->h_bbox, sizeof(double) * 4, hipHostMallocDefault));
-  chk(dalloc(&c->work_ctr, 40));
-  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 40 * sizeof(unsigned long long)));
+  chk(dalloc(&c->work_ctr, 64));
+  if (rc == CLRRT_OK) chk(hipMemset(c->work_ctr, 0, 64 * sizeof(unsigned long long)));
   chk(hipHostMalloc((void**)&c->h_samples, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_samples2, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   chk(hipHostMalloc((void**)&c->h_totals, sizeof(int64_t) * 8, hipHostMallocDefault));
@@ -1048,18 +1069,18 @@ int clrrt_reset_counters(clrrt_ctx* c) {
   memset(&c->counters, 0, sizeof(c->counters));
   c->nn_bf_keys = c->nn_samples = 0;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 40 * sizeof(unsigned long long), c->stream));
+  HIPC(c, hipMemsetAsync(c->work_ctr, 0, 64 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return CLRRT_OK;
 }
 
-int clrrt_debug_counters(clrrt_ctx* c, int64_t out[40]) {
+int clrrt_debug_counters(clrrt_ctx* c, int64_t out[64]) {
   if (!c || !out) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipStreamSynchronize(c->stream));
-  unsigned long long h[40];
+  unsigned long long h[64];
   HIPC(c, hipMemcpy(h, c->work_ctr, sizeof(h), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 40; i++) out[i] = (int64_t)h[i];
+  for (int i = 0; i < 64; i++) out[i] = (int64_t)h[i];
   return CLRRT_OK;
 }
 
@@ -1109,6 +1130,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
+  else if (k == "nn_lag" && (value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
@@ -1231,17 +1253,18 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   return CLRRT_OK;
 }
 
-// Walk-search configuration of the current set (+ its buffers on first use).
-static int ensure_walk(clrrt_ctx* c) {
-  c->nnw.bud_tiles = c->nnw_bud_tiles;
+// Walk-search configuration of a set (+ its buffers on first use).
+static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
+  w.bud_tiles = c->nnw_bud_tiles;
   // the exact-key budget grows with the tree (denser trees: more near-tied keys per sample; the cfg3
   // sweeps: 4096 best at <= 1.6 M nodes, 8192 at 4.7 M, where 4096 overflows more samples than there
   // are records)
-  c->nnw.bud_ex = c->nnw_bud_ex > 0 ? (int)std::max<int64_t>(c->nnw_bud_ex, c->n_nodes >> 9) : 0;
-  c->nnw.max_over = c->nnw_max_over;
-  c->nnw.nch = c->nnw_chunks;
-  return alloc_walk(c, c->nnw);
+  w.bud_ex = c->nnw_bud_ex > 0 ? (int)std::max<int64_t>(c->nnw_bud_ex, c->n_nodes >> 9) : 0;
+  w.max_over = c->nnw_max_over;
+  w.nch = c->nnw_chunks;
+  return alloc_walk(c, w);
 }
+static int ensure_walk(clrrt_ctx* c) { return ensure_walk_set(c, c->nnw); }
 
 // Search region (the sampling region and the tree's box) and the float frame of the searches.
 struct NnSetup {
@@ -1612,6 +1635,260 @@ int clrrt_round_prefetch(clrrt_ctx* c, const clrrt_sample* next, int32_t n) {
   return CLRRT_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Lag-2 pipelined BATCH rounds (option "nn_lag" 2).  BATCH rounds commit every sample, so the samples of
+// the next rounds are known ahead.  The walk search of round r+2's samples runs over the tree T_r (the
+// tree round r's rollouts start from) on a side stream, beside rounds r and r+1; after round r+1's
+// commit the nodes those two rounds appended, [|T_r|, |T_{r+2}|), are searched and merged in
+// (launch_nn_delta: every appended id is larger than every older one, so the merged lists equal a search
+// over T_{r+2}).  A search thus has two rounds' time instead of one.  Three list sets rotate (this
+// round's, round r+1's being merged, round r+2's being searched), three walk index sets (the one being
+// searched by round r+1's walk, the one by round r+2's, the one being built for the next), and two side
+// streams (round r+1's merge must not wait behind round r+2's walk).  Results are those of plain rounds.
+struct LagSlot {
+  clrrt_sample* d = nullptr;
+  clrrt_sample* h = nullptr;
+  int* cand = nullptr;
+  float* ckey = nullptr;
+  int* ncand = nullptr;
+  int* ctie = nullptr;
+  hipEvent_t ev = nullptr;  // recorded after its merge
+  int n = 0;                // samples searched (0: none)
+  int64_t tree_n = 0;       // size of the tree its walk searched
+  int stream = 0;           // side stream index
+};
+
+static int lag_alloc(clrrt_ctx* c) {
+  if (c->side2) return CLRRT_OK;
+  const int64_t B = c->cap.max_batch;
+  HIPC(c, dalloc(&c->d_samples3, B));
+  HIPC(c, dalloc(&c->cand3, B * CAND_K));
+  HIPC(c, dalloc(&c->ckey3, B * CAND_K));
+  HIPC(c, dalloc(&c->ncand3, B));
+  HIPC(c, dalloc(&c->ctie3, B));
+  HIPC(c, hipHostMalloc((void**)&c->h_samples3, sizeof(clrrt_sample) * B, hipHostMallocDefault));
+  for (auto& e : c->ev_lag) HIPC(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (c->cu_split > 0) {  // the same CUs as the side stream
+    const int nw = (c->n_cu + 31) / 32;
+    std::vector<uint32_t> ms(nw, 0u);
+    for (int i = 0; i < c->n_cu; i++)
+      if ((i % 8) >= c->cu_split) ms[i / 32] |= 1u << (i % 32);
+    HIPC(c, hipExtStreamCreateWithCUMask(&c->side2, (uint32_t)nw, ms.data()));
+  } else {
+    HIPC(c, hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking));
+  }
+  return CLRRT_OK;
+}
+
+static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t batch,
+                       clrrt_stats* out) {
+  int rc = lag_alloc(c);
+  if (rc != CLRRT_OK) return rc;
+  clrrt_stats st{};
+  const auto t0 = std::chrono::steady_clock::now();
+  clrrt_rng work = *rng, committed = *rng;
+  std::deque<clrrt_sample> pending;
+  const int cur = batch;
+  const int64_t nodes_before = c->n_nodes;
+  hipStream_t sides[2] = {c->side, c->side2};
+  WalkBufs* W[3] = {&c->nnw, &c->nnw_alt, &c->nnw3};
+  int64_t built_n[3] = {-1, -1, -1};  // the tree size each walk set's index was built for
+  double built_f[3][7] = {};           // ... and its frame (fr.ox, fr.oy, fr.delta, x0, y0, x1, y1)
+  // list sets: this round's (c->*), round r+1's (A) and round r+2's (B)
+  LagSlot A, B;
+  A.d = c->d_samples2; A.h = c->h_samples2; A.cand = c->cand2; A.ckey = c->ckey2; A.ncand = c->ncand2;
+  A.ctie = c->ctie2; A.ev = c->ev_lag[0];
+  B.d = c->d_samples3; B.h = c->h_samples3; B.cand = c->cand3; B.ckey = c->ckey3; B.ncand = c->ncand3;
+  B.ctie = c->ctie3; B.ev = c->ev_lag[1];
+  hipEvent_t cur_ev = c->ev_lag[2];  // the event of the set this round's lists are in
+  bool have_cur = false;             // this round's lists come from slot A of the previous round
+  int cur_stream = 0;
+  double last_round_ms = 0;
+  auto frame_of = [](const NnSetup& su, double* f) {
+    f[0] = su.fr.ox; f[1] = su.fr.oy; f[2] = su.fr.delta; f[3] = su.x0; f[4] = su.y0; f[5] = su.x1; f[6] = su.y1;
+  };
+  // the index of the tree as it is now into walk set k (incremental from the set built before, if any)
+  auto build = [&](int k, const NnSetup& su) -> int {
+    double f[7];
+    frame_of(su, f);
+    if (built_n[k] == c->n_nodes && std::equal(f, f + 7, built_f[k])) return CLRRT_OK;
+    int r2 = ensure_walk_set(c, *W[k]);
+    if (r2 != CLRRT_OK) return r2;
+    const WalkBufs* prev = nullptr;
+    for (int q = 1; q <= 2 && !prev; q++) {
+      const WalkBufs* w = W[(k + 3 - q) % 3];
+      if (w->P && w->sorted_n > 0) prev = w;
+    }
+    KTimer kt(c, 0, c->stream);
+    HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, *W[k], prev));
+    built_n[k] = c->n_nodes;
+    std::copy(f, f + 7, built_f[k]);
+    return CLRRT_OK;
+  };
+  // slot sl: the walk search of its n samples (host copy sl.h) over the current tree (walk set k)
+  auto walk = [&](LagSlot& sl, int n, int k, const NnSetup& su, int si) -> int {
+    hipStream_t s = sides[si];
+    int r2 = ensure_walk_set(c, *W[k]);  // the configuration (budgets) for this tree size
+    if (r2 != CLRRT_OK) return r2;
+    c->nn_bf_keys += (int64_t)n * c->n_nodes;
+    c->nn_samples += n;
+    HIPC(c, hipStreamWaitEvent(s, c->ev_tree, 0));
+    HIPC(c, hipMemcpyAsync(sl.d, sl.h, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, s));
+    {
+      KTimer kt(c, 0, s);
+      HIPC(c, launch_nn_walk_search(s, sl.d, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1, su.y1,
+                                    *W[k], sl.cand, sl.ckey, sl.ncand, sl.ctie, c->work_ctr + 18, c->nnw_stateless));
+    }
+    sl.n = n;
+    sl.tree_n = c->n_nodes;
+    sl.stream = si;
+    return CLRRT_OK;
+  };
+  auto draw_to = [&](int64_t want) {
+    while ((int64_t)pending.size() < want) {
+      clrrt_sample smp;
+      clrrt_draw_samples(&c->params, &work, 1, &smp);
+      pending.push_back(smp);
+    }
+  };
+  for (int64_t k = 0;; k++) {
+    const auto tr0 = std::chrono::steady_clock::now();
+    if (n_iters > 0 && st.iterations >= n_iters) break;
+    const double ms0 = std::chrono::duration<double, std::milli>(tr0 - t0).count();
+    if (n_iters == 0 && !(ms0 < budget_ms)) break;
+    const int64_t left = n_iters > 0 ? n_iters - st.iterations : INT64_MAX;
+    const int nb = (int)std::min<int64_t>(cur, left);
+    if (c->n_nodes + 2 * (int64_t)nb > c->cap.max_nodes ||
+        c->n_rows + 2 * (int64_t)nb * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+      if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
+      st.capacity_stop = 1;
+      break;
+    }
+    const int wk = (int)(k % 3);
+    const NnSetup su = nn_setup(c);
+    const bool serve = c->n_nodes >= c->nnw_min_nodes && su.region_ok;
+    // samples of rounds r+1 (slot A, unless already searched) and r+2 (slot B) to search this round
+    int nA = 0, nB = 0;
+    if (serve) {
+      const bool more = n_iters > 0 || ms0 + 2.0 * last_round_ms < budget_ms;
+      if (A.n == 0 && (n_iters > 0 || ms0 + last_round_ms < budget_ms)) nA = (int)std::min<int64_t>(cur, left - nb);
+      const int64_t nA_eff = A.n > 0 ? A.n : nA;
+      if (more && nA_eff > 0) nB = (int)std::min<int64_t>(cur, left - nb - nA_eff);
+      nA = std::max(nA, 0);
+      nB = std::max(nB, 0);
+    }
+    draw_to(nb + (int64_t)std::max(A.n, nA) + nB);
+    // this round's lists
+    if (have_cur) {
+      HIPC(c, hipStreamWaitEvent(c->stream, cur_ev, 0));
+    } else {
+      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
+      HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
+      if (serve) {
+        // the side streams' work is done (a first pipelined round searches nothing ahead yet)
+        HIPC(c, hipStreamSynchronize(c->side));
+        HIPC(c, hipStreamSynchronize(c->side2));
+        if ((rc = build(wk, su)) != CLRRT_OK) break;
+        c->nn_bf_keys += (int64_t)nb * c->n_nodes;
+        c->nn_samples += nb;
+        KTimer kt(c, 0);
+        HIPC(c, launch_nn_walk_search(c->stream, c->d_samples, nb, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0,
+                                      su.x1, su.y1, *W[wk], c->cand, c->ckey, c->ncand, c->ctie, c->work_ctr + 18,
+                                      c->nnw_stateless));
+      } else if ((rc = run_nn(c, nb, nullptr)) != CLRRT_OK) {
+        break;
+      }
+    }
+    if (serve && (nA > 0 || nB > 0) && (rc = build(wk, su)) != CLRRT_OK) break;
+    // searches ahead, beside this round's rollouts: slot A's (bootstrap) then slot B's; B on the other
+    // side stream than A, except when both search this round's index (the walk set's sample scratch
+    // is shared: one stream)
+    auto ahead = [&]() -> int {
+      if (nA > 0) {
+        for (int j = 0; j < nA; j++) A.h[j] = pending[nb + j];
+        const int r2 = walk(A, nA, wk, su, cur_stream);
+        if (r2 != CLRRT_OK) return r2;
+      }
+      if (nB > 0) {
+        for (int j = 0; j < nB; j++) B.h[j] = pending[nb + A.n + j];
+        const int r2 = walk(B, nB, wk, su, nA > 0 ? A.stream : 1 - A.stream);
+        if (r2 != CLRRT_OK) return r2;
+      }
+      return CLRRT_OK;
+    };
+    int L = nb, nn = 0;
+    if ((rc = eval_samples(c, nb, false, &L, true, (nA > 0 || nB > 0) ? std::function<int()>(ahead) : nullptr,
+                           nullptr)) != CLRRT_OK)
+      break;
+    if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
+    if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
+    // slot A: merge the nodes appended since its walk's tree
+    if (A.n > 0) {
+      hipStream_t s = sides[A.stream];
+      HIPC(c, hipEventRecord(c->ev_commit, c->stream));
+      HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
+      const int64_t first = A.tree_n, cnt = c->n_nodes - A.tree_n;
+      if (cnt > 0) {
+        KTimer kt(c, 0, s);
+        c->nn_bf_keys += (int64_t)A.n * cnt;
+        const NnSetup su2 = nn_setup(c);
+        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
+        HIPC(c, launch_nn_delta(s, A.d, A.n, c->nn, (int)first, (int)cnt, c->dp, su2.fr, c->pk, c->pi, max_chunks,
+                                A.cand, A.ckey, A.ncand, A.ctie, c->nn_seed));
+      }
+      HIPC(c, hipEventRecord(A.ev, s));
+    }
+    // the next round's index (the walk of round r+3's samples searches it)
+    {
+      const NnSetup sn = nn_setup(c);
+      if (B.n > 0 && c->n_nodes >= c->nnw_min_nodes && sn.region_ok && (rc = build((int)((k + 1) % 3), sn)) != CLRRT_OK)
+        break;
+    }
+    for (int j = 0; j < L; j++) {
+      pending.pop_front();
+      for (int q = 0; q < 3; q++) clrrt_rng_next(&committed);
+    }
+    st.iterations += L;
+    st.goal_nodes_added += c->last_goal_nodes;
+    st.speculated += nb;
+    st.rounds++;
+    // rotate: A becomes this round's set, B slot A, this round's set slot B
+    {
+      LagSlot old;
+      old.d = c->d_samples; old.h = c->h_samples; old.cand = c->cand; old.ckey = c->ckey; old.ncand = c->ncand;
+      old.ctie = c->ctie; old.ev = cur_ev; old.stream = cur_stream;
+      have_cur = A.n > 0;
+      c->d_samples = A.d; c->h_samples = A.h; c->cand = A.cand; c->ckey = A.ckey; c->ncand = A.ncand; c->ctie = A.ctie;
+      cur_ev = A.ev;
+      cur_stream = A.stream;
+      A = B;
+      B = old;
+      B.n = 0;
+      B.stream = 1 - A.stream;
+    }
+    last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
+  }
+  HIPC(c, hipStreamSynchronize(c->side));
+  HIPC(c, hipStreamSynchronize(c->side2));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  // the buffers the context's other paths use keep their roles: (d_samples, cand, ...) and the *2 set
+  // are whichever two of the three sets, *3 the third
+  {
+    c->d_samples2 = A.d; c->h_samples2 = A.h; c->cand2 = A.cand; c->ckey2 = A.ckey; c->ncand2 = A.ncand; c->ctie2 = A.ctie;
+    c->d_samples3 = B.d; c->h_samples3 = B.h; c->cand3 = B.cand; c->ckey3 = B.ckey; c->ncand3 = B.ncand; c->ctie3 = B.ctie;
+    c->ev_lag[0] = A.ev; c->ev_lag[1] = B.ev; c->ev_lag[2] = cur_ev;
+    c->nnw_built.n = -1;
+    c->nnw.sorted_n = -1;
+    c->nnw_alt.sorted_n = -1;
+    c->nnw3.sorted_n = -1;
+  }
+  st.nodes_added = c->n_nodes - nodes_before;
+  st.elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *rng = committed;
+  if (out) *out = st;
+  return rc;
+}
+
 int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
                  clrrt_stats* out) {
   if (!c || !rng || n_iters < 0 || (mode != CLRRT_MODE_EXACT && mode != CLRRT_MODE_BATCH)) return CLRRT_EINVAL;
@@ -1620,6 +1897,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
   HIPC(c, hipSetDevice(c->device));
   batch = std::max(1, std::min<int32_t>(batch > 0 ? batch : c->cap.max_batch, c->cap.max_batch));
+  if (mode == CLRRT_MODE_BATCH && c->nn_pipeline && c->nn_lag == 2) return expand_lag2(c, rng, n_iters, budget_ms, batch, out);
   clrrt_stats st{};
   auto t0 = std::chrono::steady_clock::now();
   clrrt_rng work = *rng;       // draws ahead (speculative samples)

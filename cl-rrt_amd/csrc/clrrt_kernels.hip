@@ -932,7 +932,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   }
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && j < a.njobs)
-    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[32 + q], (unsigned long long)pclk.t[q]);
+    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.t[q]);
 #endif
 }
 
@@ -1059,7 +1059,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 #endif
   int fin = -1;  // >= 0: the lane's rollout ended with this outcome; finished in the next batch
 #ifdef CLRRT_ROLL_PROFILE
-  unsigned long long scan_sum = 0, scan_wave = 0, scan_long = 0, scan_long_pts = 0, chain_steps = 0;
+  // longest chain (a regular rollout + its goal-biased follow-up) of the lane, the steps of its current
+  // one, its steps after the wave found the queue empty, when that was
+  unsigned long long chain_steps = 0, job_steps = 0, tail_steps = 0;
+  uint64_t t_qdone = 0;
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
@@ -1134,6 +1137,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
               pass = 0;
               steps = 0;
+#ifdef CLRRT_ROLL_PROFILE
+              job_steps = 0;
+#endif
             }
           }
         }
@@ -1173,18 +1179,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (pc) pc->mark(4);
     int o = roll_step_post(r, a.p, Dobs, d2);
 #ifdef CLRRT_ROLL_PROFILE
-    {
-      unsigned it = r.scan_it, mx_ = it;
-#pragma unroll
-      for (int q = 32; q > 0; q >>= 1) mx_ = max(mx_, (unsigned)__shfl_xor((int)mx_, q, 64));
-      scan_sum += it;
-      const uint64_t actm = __ballot(true);
-      if (lane == __ffsll((unsigned long long)actm) - 1) {
-        scan_wave += mx_;
-        scan_long += __popcll(actm);  // active lanes of this wave step
-        scan_long_pts += 1;           // wave steps
-      }
-      chain_steps++;
+    job_steps++;
+    chain_steps = max(chain_steps, job_steps);
+    if (qdone) {
+      tail_steps++;
+      if (!t_qdone) t_qdone = __builtin_amdgcn_s_memtime();
     }
 #endif
     w.steps++;
@@ -1216,22 +1215,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   }
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[32 + q], (unsigned long long)pclk.t[q]);
+    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.t[q]);
   if (a.ctr) {
-    atomicAdd(&a.ctr[30], scan_sum);
-    if (scan_wave) atomicAdd(&a.ctr[31], scan_wave);
-    atomicAdd(&a.ctr[28], scan_long);
-    atomicAdd(&a.ctr[29], scan_long_pts);
-    // load balance: wave lifetimes (sum, max), steps of the busiest lane (max), waves
-    unsigned long long cmax = chain_steps;
+    // load balance: wave lifetimes (sum, max), the longest chain (max), waves; the queue drain (first
+    // step after a fetch found it empty) of the wave, the busiest lane's steps after it
+    unsigned long long cmax = chain_steps, tail = tail_steps;
 #pragma unroll
-    for (int q = 32; q > 0; q >>= 1) cmax = max(cmax, (unsigned long long)__shfl_xor((long long)cmax, q, 64));
+    for (int q = 32; q > 0; q >>= 1) {
+      cmax = max(cmax, (unsigned long long)__shfl_xor((long long)cmax, q, 64));
+      tail = max(tail, (unsigned long long)__shfl_xor((long long)tail, q, 64));
+    }
     if (lane == 0) {
       const unsigned long long life = __builtin_amdgcn_s_memtime() - t_start;
-      atomicAdd(&a.ctr[24], life);
-      atomicMax(&a.ctr[25], life);
-      atomicMax(&a.ctr[26], cmax);
-      atomicAdd(&a.ctr[27], 1ull);
+      atomicAdd(&a.ctr[48], life);
+      atomicMax(&a.ctr[49], life);
+      atomicMax(&a.ctr[50], cmax);
+      atomicAdd(&a.ctr[51], 1ull);
+      if (t_qdone) {
+        atomicAdd(&a.ctr[52], t_qdone - t_start);
+        atomicMax(&a.ctr[53], t_qdone - t_start);
+      }
+      atomicMax(&a.ctr[54], tail);
+      atomicAdd(&a.ctr[55], tail);
     }
   }
 #endif

@@ -414,9 +414,10 @@ int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[19]);
  * (samples x tree nodes of every search, plus the appended nodes merged into prefetched lists),
  * out[1] = samples searched, out[2] = walk-search tiles visited, out[3] = exact keys evaluated. */
 int clrrt_search_work(clrrt_ctx* ctx, int64_t out[4]);
-/* Diagnostics: the context's 40 raw work counters (0..2 rollout work, 8..26 search statistics,
- * 32..39 per-phase rollout clocks in a -DCLRRT_ROLL_PROFILE build). */
-int clrrt_debug_counters(clrrt_ctx* ctx, int64_t out[40]);
+/* Diagnostics: the context's 64 raw work counters (0..2 rollout work, 8..39 search statistics,
+ * 40..63 rollout profile counters of a -DCLRRT_ROLL_PROFILE build: 40..47 per-phase clocks, 48..51 wave
+ * lifetimes (sum, max), busiest lane's steps, waves, 52..55 queue-drain times and tail steps). */
+int clrrt_debug_counters(clrrt_ctx* ctx, int64_t out[64]);
 
 #ifdef __cplusplus
 }

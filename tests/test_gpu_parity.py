@@ -306,7 +306,8 @@ def test_walk_matches_brute_force_large_tree():
 
 @pytest.mark.gpu
 def test_pipelined_batch_rounds_identical():
-    """Full-size property: BATCH rounds with the next round's walk search overlapped with the current
+    """Full-size property: BATCH rounds with the walk search of the round after next (nn_lag 2, or of the
+    next round: nn_lag 1) overlapped with the current
     round's rollouts (+ the merge of the appended nodes, launch_nn_delta) grow exactly the tree of
     plain rounds (every node record and trajectory row).  So do the scheduling and search options: the
     rollout queue order (roll_priority), the persistent grid width (roll_blocks), the per-lane collision
@@ -315,8 +316,9 @@ def test_pipelined_batch_rounds_identical():
     split (budget 1)."""
     mode, obs = _scene("obb200")
     trees = []
-    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(roll_priority=0, roll_blocks=512), dict(roll_coop=0),
-                dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
+    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=1), dict(roll_priority=0, roll_blocks=512),
+                dict(roll_coop=0),
+                dict(nn_lag=1, nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
                 dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,

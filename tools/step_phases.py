@@ -44,7 +44,7 @@ for label, jl in (("1 lane, longest", [jobs[order[0]]]), ("1 lane, 2nd", [jobs[o
     steps = sum(x["nrows"] - 1 for x in r)
     lanes = len(jl)
     smax = max(x["nrows"] - 1 for x in r)
-    ph = np.array(d[32:40], dtype=np.float64) / max(1, steps)  # per lane-step (per lane clocks)
+    ph = np.array(d[40:48], dtype=np.float64) / max(1, steps)  # per lane-step (per lane clocks)
     tot = ph.sum()
     print(f"{label:28s} kernel {ms:.3f} ms, {steps // lanes} steps/lane, {tot:,.0f} clk per step "
           f"({ms * 1e-3 * 2.4e9 / max(1, steps // lanes):,.0f} wall clk/step at 2.4 GHz; longest lane {smax} steps, "
