@@ -150,10 +150,12 @@ struct clrrt_ctx {
   float* ckey2 = nullptr;
   int* ncand2 = nullptr;
   int* ctie2 = nullptr;
-  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (expand_lag2).
+  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (2: expand_lag2;
+  // default 1: on cfg3 lag 2 measured 0.931 vs 0.951 M nodes/s -- the rollouts, not the search, bound the
+  // round, and a second search in flight slows them).
   // Lag 2 keeps a third list set (*3), a third walk index set and a second side stream (allocated on
   // first use).
-  int nn_lag = 2;
+  int nn_lag = 1;
   clrrt_sample* d_samples3 = nullptr;
   clrrt_sample* h_samples3 = nullptr;
   int* cand3 = nullptr;
@@ -2127,7 +2129,7 @@ int clrrt_simulate(clrrt_ctx* c, const clrrt_sim_case* cases, int32_t n, clrrt_r
 }
 
 int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double* b, int32_t n, double* out) {
-  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 19) return CLRRT_EINVAL;
+  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 23) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
   double *da = nullptr, *db = nullptr, *dout = nullptr;

@@ -316,6 +316,75 @@ CLRRT_HD inline void sincos(double x, double& sx, double& cx) {
   cx = cos(x);
 }
 
+// The same functions with the range cases selected per lane instead of branched on (the rollout step;
+// a wave's lanes hold different headings).  Every case of glibc's sin, cos and sincos below the
+// Payne-Hanek range is one do_sin and one do_cos evaluation on per-case arguments, so computing each
+// once on the selected arguments (and the cheap Cody-Waite reduction for every lane) costs a divergent
+// wave one evaluation per function instead of one per case present.  Values are those of the branched
+// functions: the same do_sin / do_cos on the same arguments.  |x| >= 105414350 or non-finite lanes take
+// the branched functions.
+//   sincos_sel:     sincos (generic build, GCC's merged sin/cos of one argument)
+//   sin_cos_fma_sel: sin(x) and cos(x) as two separate FMA-build calls
+CLRRT_HD inline void sincos_sel(double x, double& sx, double& cx) {
+  const uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (!(k < 0x419921fbu)) {
+    sincos(x, sx, cx);
+    return;
+  }
+  const bool cA = k < 0x3feb6000u, cB = !cA && k < 0x400368fdu;
+  const double y = hp0 - fabs(x);
+  const double aB = y + hp1, daB = (y - aB) + hp1;
+  double aC, daC;
+  const int n = nofma::reduce_sincos(x, aC, daC);
+  const double a = cA ? x : (cB ? aB : aC), da = cA ? 0.0 : (cB ? daB : daC);
+  const double rs = nofma::do_sin(a, da), rc = nofma::do_cos(a, da);
+  if (k < 0x3e400000u) {
+    sx = x;
+    cx = 1.0;
+  } else if (cA) {
+    sx = rs;
+    cx = rc;
+  } else if (cB) {
+    sx = copysign_(rc, x);
+    cx = rs;
+  } else {
+    const double s0 = (n & 1) ? rc : rs, c0 = ((n + 1) & 1) ? rc : rs;
+    sx = (n & 2) ? -s0 : s0;
+    cx = ((n + 1) & 2) ? -c0 : c0;
+  }
+}
+
+CLRRT_HD inline void sin_cos_fma_sel(double x, double& sx, double& cx) {
+  const uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (!(k < 0x419921fbu)) {
+    sx = sin(x);
+    cx = cos(x);
+    return;
+  }
+  const bool cA = k < 0x3feb6000u, cB = !cA && k < 0x400368fdu;
+  const double y = hp0 - fabs(x);
+  const double aB = y + hp1, daB = (y - aB) + hp1;  // cos, case B: do_sin
+  double aC, daC;
+  const int n = reduce_sincos(x, aC, daC);
+  const double as = cA ? x : (cB ? aB : aC), das = cA ? 0.0 : (cB ? daB : daC);
+  const double ac = cA ? x : (cB ? y : aC), dac = cA ? 0.0 : (cB ? hp1 : daC);  // sin, case B: do_cos(y, hp1)
+  const double rs = do_sin(as, das), rc = do_cos(ac, dac);
+  if (k < 0x3e500000u) sx = x;
+  else if (cA) sx = rs;
+  else if (cB) sx = copysign_(rc, x);
+  else {
+    const double s0 = (n & 1) ? rc : rs;
+    sx = (n & 2) ? -s0 : s0;
+  }
+  if (k < 0x3e400000u) cx = 1.0;
+  else if (cA) cx = rc;
+  else if (cB) cx = rs;
+  else {
+    const double c0 = ((n + 1) & 1) ? rc : rs;
+    cx = ((n + 1) & 2) ? -c0 : c0;
+  }
+}
+
 // ------------------------------------------------------------------------------- float sincosf
 // glibc 2.35 sincosf (sysdeps/ieee754/flt-32/s_sincosf.c + sincosf.h; the FMA variant libm's ifunc
 // selects on FMA+AVX2 hosts): the float argument is widened to double, reduced by a Cody-Waite step

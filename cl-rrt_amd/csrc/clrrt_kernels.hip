@@ -538,10 +538,9 @@ __device__ __forceinline__ double roll_step_pre(Roll& r, const DevParams& p, dou
   // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
   const double d2 = ode_euler(r, p, dc, ac);
   if (pc) pc->mark(2);
-  glibc::sincos(r.x2, r.s2, r.c2);
+  glibc::sincos_sel(r.x2, r.s2, r.c2);
   r.t3 = glibc::tan(r.x3);
-  r.cwp = glibc::cos(r.x2);  // independent of sincos / tan: their latencies overlap
-  r.swp = glibc::sin(r.x2);
+  glibc::sin_cos_fma_sel(r.x2, r.swp, r.cwp);  // independent of sincos / tan: their latencies overlap
   if (pc) pc->mark(3);
   col7 = (double)r.wp;
   col8 = vref;
@@ -1756,6 +1755,10 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 15: r = round(x); break;
     case 16: { double sx, cx; glibc::sincos(x, sx, cx); r = sx; } break;
     case 17: { double sx, cx; glibc::sincos(x, sx, cx); r = cx; } break;
+    case 20: { double sx, cx; glibc::sincos_sel(x, sx, cx); r = sx; } break;
+    case 21: { double sx, cx; glibc::sincos_sel(x, sx, cx); r = cx; } break;
+    case 22: { double sx, cx; glibc::sin_cos_fma_sel(x, sx, cx); r = sx; } break;
+    case 23: { double sx, cx; glibc::sin_cos_fma_sel(x, sx, cx); r = cx; } break;
     case 18: {  // diagnostics: latency of a rollout step's trig (sincos, cos, sin, tan), y[0] iterations
       double z = x;
       for (int it = 0; it < (int)y; it++) {

@@ -48,15 +48,22 @@ HOST = {
     12: lambda a, b: float(_libm.asinf(_f32(a))), 13: lambda a, b: float(_libm.sqrtf(_f32(a))),
     14: lambda a, b: float(np.float32(_f32(a)) / np.float32(_f32(b))), 15: lambda a, b: float(_libm.round(a)),
     16: lambda a, b: _sincos(a, 0), 17: lambda a, b: _sincos(a, 1),
+    # the rollout step's case-selected forms (glibc::sincos_sel, glibc::sin_cos_fma_sel)
+    20: lambda a, b: _sincos(a, 0), 21: lambda a, b: _sincos(a, 1),
+    22: lambda a, b: math.sin(a), 23: lambda a, b: math.cos(a),
 }
 NAMES = ["sin", "cos", "tan", "sqrt", "fmod", "atan2", "exp", "div", "cosf", "sinf", "atan2f", "acosf",
-         "asinf", "sqrtf", "fdiv", "round", "sincos.sin", "sincos.cos"]
-EXACT = {0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17}
+         "asinf", "sqrtf", "fdiv", "round", "sincos.sin", "sincos.cos", None, None, "sincos_sel.sin",
+         "sincos_sel.cos", "sin_cos_fma_sel.sin", "sin_cos_fma_sel.cos"]
+FNS = [f for f in range(24) if f not in (18, 19)]  # 18, 19: latency diagnostics
+EXACT = {0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 20, 21, 22, 23}
 
 
 def _inputs(fn, n, rng):
-    if fn in (0, 1, 8, 9, 16, 17):
+    if fn in (0, 1, 8, 9, 16, 17, 20, 21, 22, 23):
         a = rng.uniform(-7, 7, n)
+        a[: n // 8] = rng.uniform(-1e-8, 1e-8, n // 8)  # the tiny-argument cases
+        a[n // 8: n // 4] = rng.uniform(-3e4, 3e4, n // 8)
     elif fn == 2:
         a = rng.uniform(-0.52, 0.52, n)
     elif fn in (3, 13):
@@ -80,7 +87,7 @@ def test_device_math_vs_glibc():
     rng = np.random.default_rng(5)
     n = 20000
     report = {}
-    for fn in range(18):
+    for fn in FNS:
         a, b = _inputs(fn, n, rng)
         g = pl.selftest_math(fn, a, b)
         h = np.array([HOST[fn](x, y) for x, y in zip(a, b)])

@@ -316,9 +316,9 @@ def test_pipelined_batch_rounds_identical():
     split (budget 1)."""
     mode, obs = _scene("obb200")
     trees = []
-    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=1), dict(roll_priority=0, roll_blocks=512),
+    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=2), dict(roll_priority=0, roll_blocks=512),
                 dict(roll_coop=0),
-                dict(nn_lag=1, nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
+                dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
                 dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,

@@ -90,7 +90,7 @@ def test_native_full_reference_nodes_match_oracle():
     goal = (40.0, 0.0, 0.0, 0.0)
     obs = T.scene(200, 0)
     root = np.array([0.0, 0.0, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0, 0.0, 0.0])
-    trees = [(5, 120, 0), (6, 512, 128)]
+    trees = [(5, 120, 0), (6, 512, 64)]  # BATCH rounds of the engine's max_batch (64)
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
         tin, tout = os.path.join(td, "t.bin"), os.path.join(td, "tout.bin")
