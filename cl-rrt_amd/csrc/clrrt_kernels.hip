@@ -368,6 +368,74 @@ __global__ void k_nn_exact(const clrrt_sample* __restrict__ S, int B, const NnRe
   ncand[s] = cnt;
 }
 
+// The same for trees whose (id, key) sequence fits in LDS: one workgroup (one wave) per sample; the 64
+// lanes build the keys, one lane replays std::sort on the LDS copy (its long chain of dependent
+// accesses then waits on LDS instead of global-memory latency), and the lanes test feasibleNode on 64
+// sorted entries at a time, the first `sort_limit` feasible ones in sorted order forming the list.
+#define NN_EXACT_LDS_MAX 18432  /* entries: 144 KB of dynamic LDS */
+__global__ void __launch_bounds__(64) k_nn_exact_lds(const clrrt_sample* __restrict__ S, int B,
+                                                     const NnRec* __restrict__ nodes, int N, DevParams p,
+                                                     const int* __restrict__ ctie, int* __restrict__ cand,
+                                                     float* __restrict__ ckey, int* __restrict__ ncand) {
+  extern __shared__ KeyId s_kv[];
+  const int s = blockIdx.x;
+  if (s >= B || !ctie[s]) return;
+  const int lane = threadIdx.x;
+  const double sx = S[s].x, sy = S[s].y;
+  const int ex = S[s].explore;
+  for (int n = lane; n < N; n += 64) {
+    const NnRec& rec = nodes[n];
+    float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+    if (!ex) k = rec.costE + k;
+    s_kv[n].id = n;
+    s_kv[n].key = k;
+  }
+  __syncthreads();
+  if (lane == 0) std_sort(s_kv, N);
+  __syncthreads();
+  int cnt = 0;
+  for (int i0 = 0; i0 < N && cnt < p.sort_limit; i0 += 64) {
+    const int i = i0 + lane;
+    bool f = false;
+    KeyId e{0, 0.f};
+    if (i < N) {
+      e = s_kv[i];
+      const NnRec& rec = nodes[e.id];
+      f = feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len);
+    }
+    const uint64_t m = __ballot(f);
+    // the first (sort_limit - cnt) feasible entries of this chunk, in sorted order
+    const int rank = cnt + __popcll(m & ((1ull << lane) - 1));
+    if (f && rank < p.sort_limit) {
+      cand[s * CAND_K + rank] = e.id;
+      ckey[s * CAND_K + rank] = e.key;
+    }
+    cnt = min(p.sort_limit, cnt + __popcll(m));
+  }
+  for (int j = cnt + lane; j < CAND_K; j += 64) cand[s * CAND_K + j] = -1;
+  if (lane == 0) ncand[s] = cnt;
+}
+
+// EXACT-mode tie replay for the samples with ctie set: in LDS when the tree fits, else one lane per
+// sample over the global scratch.
+static hipError_t launch_nn_exact_any(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                      const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
+                                      int* ncand) {
+  if (N <= NN_EXACT_LDS_MAX) {
+    const size_t lds = sizeof(KeyId) * (size_t)N;
+    if (lds > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute((const void*)&k_nn_exact_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_nn_exact_lds, dim3(B), dim3(64), lds, st, S, B, nodes, N, p, ctie, cand, ckey, ncand);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, scratch, cand, ckey,
+                     ncand);
+  return hipGetLastError();
+}
+
 // --------------------------------------------------------------------------------------------
 // rollouts
 // --------------------------------------------------------------------------------------------
@@ -1972,11 +2040,7 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
                         stats ? stats + 5 : nullptr);
     if (e != hipSuccess) return e;
   }
-  if (exact_scratch) {
-    hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, exact_scratch,
-                       cand, ckey, ncand);
-    LAUNCH_CHECK();
-  }
+  if (exact_scratch) return launch_nn_exact_any(st, S, B, nodes, N, p, ctie, exact_scratch, cand, ckey, ncand);
   return hipSuccess;
 }
 
@@ -2005,10 +2069,7 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
 hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                 int* ncand) {
-  hipLaunchKernelGGL(k_nn_exact, dim3((B + 63) / 64), dim3(64), 0, st, S, B, nodes, N, p, ctie, scratch, cand, ckey,
-                     ncand);
-  LAUNCH_CHECK();
-  return hipSuccess;
+  return launch_nn_exact_any(st, S, B, nodes, N, p, ctie, scratch, cand, ckey, ncand);
 }
 
 static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
