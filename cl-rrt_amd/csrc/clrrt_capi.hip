@@ -115,6 +115,7 @@ struct clrrt_ctx {
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
   int roll_coop = 1;          // option "roll_coop": wave-cooperative collision checks in k_roll_run
+  int exact_min_width = 8;    // option "exact_min_width": EXACT rounds speculate at least this many samples
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
@@ -1138,6 +1139,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_coop") c->roll_coop = value != 0;
+  else if (k == "exact_min_width" && value >= 1 && value <= 1 << 20) c->exact_min_width = (int)value;
   else if (k == "cu_split" && value >= 0 && value <= 7) {
     HIPC(c, hipStreamSynchronize(c->side));
     if (c->roll_st) HIPC(c, hipStreamSynchronize(c->roll_st));
@@ -1906,7 +1908,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   clrrt_rng committed = *rng;  // state after exactly `iterations` iterations
   std::deque<clrrt_sample> pending;
   const bool exact = mode == CLRRT_MODE_EXACT;
-  int cur = exact ? std::min(batch, 16) : batch;
+  int cur = exact ? std::min(batch, std::max(16, c->exact_min_width)) : batch;
   int64_t nodes_before = c->n_nodes;
   int rc = CLRRT_OK;
   bool have_next = false;  // this round's samples and lists were prepared by the previous round
@@ -1998,7 +2000,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     st.goal_nodes_added += c->last_goal_nodes;
     st.speculated += nb;
     st.rounds++;
-    if (exact) cur = std::max(8, std::min(batch, L == nb ? 2 * nb : 2 * L));
+    if (exact) cur = std::max(c->exact_min_width, std::min(batch, L == nb ? 2 * nb : 2 * L));
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
   HIPC(c, hipStreamSynchronize(c->side));

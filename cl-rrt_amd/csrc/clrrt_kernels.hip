@@ -368,16 +368,137 @@ __global__ void k_nn_exact(const clrrt_sample* __restrict__ S, int B, const NnRe
   ncand[s] = cnt;
 }
 
+// std_sort (clrrt_stdsort.hpp: libstdc++'s introsort) replayed by one 64-lane wave (a workgroup of 64)
+// on an LDS array, the same permutation.  The introsort's control (median-of-three, the explicit range
+// stack, the depth limit's heapsort, the final insertion sort) runs as in std_sort (the data moves of
+// the pivot choice, the heapsort and the insertion sort on lane 0); the partition is parallel.
+// __unguarded_partition's left scan stops at the positions L_0 < L_1 < ... with !(a < pivot) and its
+// right scan at R_0 > R_1 > ... with !(pivot < a), both on the range as it was (a swap only changes
+// positions the scans have passed); it swaps (L_k, R_k) while L_k < R_k and returns, at the first k
+// with L_k >= R_k, L_k if L_k < R_{k-1} (else the left scan stops at the swapped R_{k-1}).  The wave
+// finds the stops 64 positions at a time from both ends, pairs them, and swaps the pairs (disjoint) once
+// the crossing is known.  pairs: LDS scratch of n / 2 + 64 int2.
+__device__ __forceinline__ void wave_std_sort(KeyId* a, int n, int2* pairs) {
+  const int lane = threadIdx.x & 63;
+  if (n <= 1) return;
+  struct Rg { int lo, hi, depth; };
+  Rg stack[64];
+  int sp = 0;
+  int lo = 0, hi = n;
+  int depth = 2 * ilog2(n);
+  __shared__ int s_l[64], s_r[64];  // pending stop positions of the two scans
+  for (;;) {
+    while (hi - lo > 16) {
+      if (depth == 0) {
+        if (lane == 0) heap_sort_(a + lo, hi - lo);
+        __syncthreads();
+        break;
+      }
+      --depth;
+      if (lane == 0) {
+        KeyId* first = a + lo;
+        KeyId* last = a + hi;
+        median_to_first_(first, first + 1, first + (last - first) / 2, last - 1);
+      }
+      __syncthreads();
+      const float P = a[lo].key;
+      const int f = lo + 1, l = hi;
+      int lpos = f, rpos = l - 1;  // next positions the scans examine
+      int nl = 0, hl = 0, nr = 0, hr = 0;  // pending stops (count, head) of each scan
+      int np = 0;                  // pairs recorded
+      int prevR = INT_MAX;         // R_{k-1}
+      int cut = -1;
+      while (cut < 0) {
+        if (nl == 0) {  // the next 64 positions of the left scan
+          const int i = lpos + lane;
+          const bool st = i < l && !(a[i].key < P);
+          const uint64_t m = __ballot(st);
+          if (st) s_l[__popcll(m & ((1ull << lane) - 1))] = i;
+          nl = __popcll(m);
+          hl = 0;
+          lpos += 64;
+        }
+        if (nr == 0) {  // the next 64 positions of the right scan, downwards
+          const int i = rpos - lane;
+          const bool st = i >= f && !(P < a[i].key);
+          const uint64_t m = __ballot(st);
+          if (st) s_r[__popcll(m & ((1ull << lane) - 1))] = i;
+          nr = __popcll(m);
+          hr = 0;
+          rpos -= 64;
+        }
+        __syncthreads();
+        const bool lend = nl == 0 && lpos >= l, rend = nr == 0 && rpos < f;  // a scan ran out of range
+        const int m = min(nl, nr);
+        int Lk = INT_MAX, Rk = INT_MIN;
+        bool cross = false;
+        if (lane < m) {
+          Lk = s_l[hl + lane];
+          Rk = s_r[hr + lane];
+          cross = Lk >= Rk;
+        }
+        const uint64_t cm = __ballot(cross);
+        const int kx = cm ? __ffsll((unsigned long long)cm) - 1 : m;  // pairs before the crossing
+        if (lane < kx) pairs[np + lane] = make_int2(Lk, Rk);
+        const int prev = kx > 0 ? __shfl(Rk, kx - 1, 64) : prevR;
+        if (cm) {
+          const int Lx = __shfl(Lk, kx, 64);
+          cut = Lx < prev ? Lx : prev;
+        } else if ((nl - m == 0 && lend) || (nr - m == 0 && rend)) {
+          // a scan has no further stop in range: the sequential scans would meet the last swap
+          // (a missing L_k: the left scan stops at R_{k-1}; a missing R_k: the right scan stops at L_{k-1}
+          // and the left scan's next stop L_k, if any, is returned unless past R_{k-1})
+          if (nl - m > 0) {
+            const int Lx = s_l[hl + m];
+            cut = Lx < prev ? Lx : prev;
+          } else {
+            cut = prev == INT_MAX ? l : prev;
+          }
+        }
+        np += kx;
+        prevR = prev;
+        nl -= m; hl += m;
+        nr -= m; hr += m;
+        __syncthreads();
+      }
+      for (int k = lane; k < np; k += 64) {  // the swaps (disjoint positions)
+        const int2 pr = pairs[k];
+        const KeyId t = a[pr.x];
+        a[pr.x] = a[pr.y];
+        a[pr.y] = t;
+      }
+      __syncthreads();
+      stack[sp++] = Rg{cut, hi, depth};
+      hi = cut;
+    }
+    if (sp == 0) break;
+    --sp;
+    lo = stack[sp].lo;
+    hi = stack[sp].hi;
+    depth = stack[sp].depth;
+  }
+  // __final_insertion_sort (elements only move within the final partitions: lane 0)
+  if (lane == 0) {
+    if (n > 16) {
+      insertion_sort_(a, a + 16);
+      for (KeyId* i = a + 16; i != a + n; ++i) unguarded_linear_insert_(i);
+    } else {
+      insertion_sort_(a, a + n);
+    }
+  }
+  __syncthreads();
+}
+
 // The same for trees whose (id, key) sequence fits in LDS: one workgroup (one wave) per sample; the 64
-// lanes build the keys, one lane replays std::sort on the LDS copy (its long chain of dependent
-// accesses then waits on LDS instead of global-memory latency), and the lanes test feasibleNode on 64
+// lanes build the keys, replay std::sort on the LDS copy (wave_std_sort), and test feasibleNode on 64
 // sorted entries at a time, the first `sort_limit` feasible ones in sorted order forming the list.
-#define NN_EXACT_LDS_MAX 18432  /* entries: 144 KB of dynamic LDS */
+#define NN_EXACT_LDS_MAX 12000  /* entries: 8 B each + 4 B of partition pairs: 144 KB of dynamic LDS */
 __global__ void __launch_bounds__(64) k_nn_exact_lds(const clrrt_sample* __restrict__ S, int B,
                                                      const NnRec* __restrict__ nodes, int N, DevParams p,
                                                      const int* __restrict__ ctie, int* __restrict__ cand,
                                                      float* __restrict__ ckey, int* __restrict__ ncand) {
   extern __shared__ KeyId s_kv[];
+  int2* s_pairs = (int2*)(s_kv + N);  // [N / 2 + 64]
   const int s = blockIdx.x;
   if (s >= B || !ctie[s]) return;
   const int lane = threadIdx.x;
@@ -391,8 +512,7 @@ __global__ void __launch_bounds__(64) k_nn_exact_lds(const clrrt_sample* __restr
     s_kv[n].key = k;
   }
   __syncthreads();
-  if (lane == 0) std_sort(s_kv, N);
-  __syncthreads();
+  wave_std_sort(s_kv, N, s_pairs);
   int cnt = 0;
   for (int i0 = 0; i0 < N && cnt < p.sort_limit; i0 += 64) {
     const int i = i0 + lane;
@@ -422,7 +542,7 @@ static hipError_t launch_nn_exact_any(hipStream_t st, const clrrt_sample* S, int
                                       const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                       int* ncand) {
   if (N <= NN_EXACT_LDS_MAX) {
-    const size_t lds = sizeof(KeyId) * (size_t)N;
+    const size_t lds = sizeof(KeyId) * (size_t)N + sizeof(int2) * (size_t)(N / 2 + 64);
     if (lds > 64 * 1024) {
       const hipError_t e = hipFuncSetAttribute((const void*)&k_nn_exact_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)lds);

@@ -15,3 +15,15 @@ def test_stdsort_replay_matches_libstdcxx():
         out = subprocess.run([exe], capture_output=True, text=True)
         assert out.returncode == 0, out.stdout + out.stderr
         assert "mismatching 0" in out.stdout
+
+
+def test_wave_partition_argument_matches_replay():
+    """wave_std_sort's parallel partition (both scans' stops paired, swaps after the crossing) gives the
+    sequential replay's permutation (tests/native/wave_sort_check.cpp)."""
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "wave_sort_check")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(HERE, "native", "wave_sort_check.cpp")],
+                       check=True)
+        out = subprocess.run([exe], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "mismatches 0" in out.stdout

@@ -10,10 +10,13 @@ from clrrt import abi, scenes
 
 budget = float(sys.argv[1]) if len(sys.argv) > 1 else 2000.0
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+widths = [int(w) for w in sys.argv[3].split(",")] if len(sys.argv) > 3 else [8]
 pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 20,
                    max_rows=1 << 25, max_batch=max(batch, 256))
 pl.set_obstacles(scenes.urban_scene(200))
-for label in ("warm-up", "timed"):
+for label in ["warm-up"] + [f"min width {w}" for w in widths]:
+    if label != "warm-up":
+        pl.set_option("exact_min_width", int(label.split()[-1]))
     pl.tree_init()
     pl.reset_counters()
     pl.enable_timing(True)
