@@ -77,8 +77,16 @@ struct clrrt_ctx {
   RollRes* res_spec = nullptr;
   clrrt_node* regnodes = nullptr;
   RollRes* res_gb = nullptr;
-  double* slots = nullptr;  // rollout rows of one round, [2][max_batch * CAND_K][slot_rows][10]
+  double* slots = nullptr;  // rollout rows of one round, [2][max_batch * CAND_K][slot_rows][10] (allocated
+                            // only when rows are not deferred: option "rows_deferred" 0 or the non-persistent path)
   int slot_rows = 0;
+  // deferred rows (option "rows_deferred", default 1): the persistent rollouts store no rows; each commit
+  // gathers its accepted rollouts' start states into rep_buf and the next persistent launch replays them
+  // into the arena (flush_replays runs them alone when rows are needed before that)
+  int rows_deferred = 1;
+  void* rep_buf = nullptr;  // [2 max_batch] Replay
+  int rep_n = 0;            // pending replays
+  bool eval_deferred = false;  // the last eval_samples ran with deferred rows
   clrrt_node* gbnodes = nullptr;
   SampleOut* so = nullptr;
   int* first_conflict = nullptr;
@@ -190,6 +198,8 @@ struct clrrt_ctx {
 
 // ------------------------------------------------------------------------------------------ util
 static void pf_reset(clrrt_ctx* c);
+static int flush_replays(clrrt_ctx* c);
+static int ensure_slots(clrrt_ctx* c);
 
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -411,7 +421,7 @@ static void free_all(clrrt_ctx* c) {
   if (c->side) hipStreamSynchronize(c->side);  // side-stream work (prefetched search) uses the *2 buffers
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
-                  c->out_nodes, c->jobs, c->slots, c->totals, c->work_ctr, c->grid_buf,
+                  c->out_nodes, c->jobs, c->slots, c->rep_buf, c->totals, c->work_ctr, c->grid_buf,
                   c->nn_seed, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
@@ -497,8 +507,8 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   chk(dalloc(&c->res_spec, B * CAND_K));
   chk(dalloc(&c->regnodes, B));
   chk(dalloc(&c->res_gb, B * CAND_K));
-  c->slot_rows = c->dp.n_steps_max + 1;
-  chk(dalloc(&c->slots, (size_t)2 * c->slot_rows * 10 * B * CAND_K));
+  c->slot_rows = 0;  // slots allocated on first use (ensure_slots)
+  chk(hipMalloc(&c->rep_buf, replay_bytes() * (size_t)2 * B));
   chk(dalloc(&c->gbnodes, B));
   chk(dalloc(&c->so, B));
   chk(dalloc(&c->first_conflict, 1));
@@ -571,7 +581,9 @@ int clrrt_set_params(clrrt_ctx* c, const clrrt_params* p) {
   pf_reset(c);
   DevParams d;
   derive(*p, d, c->n_obs);
-  if (d.n_steps_max + 1 > c->slot_rows) {  // a smaller sim_dt needs longer rollout slots
+  int rc = flush_replays(c);  // pending replays run under the parameters they were committed with
+  if (rc != CLRRT_OK) return rc;
+  if (c->slots && d.n_steps_max + 1 > c->slot_rows) {  // a smaller sim_dt needs longer rollout slots
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipFree(c->slots));
@@ -734,6 +746,8 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
   std::vector<BakedObs> b(m);
   for (int i = 0; i < m; i++) bake_obstacle(o[i], b[i]);
   HIPC(c, hipSetDevice(c->device));
+  int frc = flush_replays(c);  // pending replays collide against the obstacles they were committed with
+  if (frc != CLRRT_OK) return frc;
   if (m > 0) {
     HIPC(c, hipMemcpyAsync(c->obs, b.data(), sizeof(BakedObs) * m, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -746,6 +760,7 @@ int clrrt_set_obstacles(clrrt_ctx* c, const clrrt_obstacle* o, int32_t m) {
 int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
   if (!c || !root_state) return CLRRT_EINVAL;
   pf_reset(c);
+  c->rep_n = 0;  // replays pending for the old tree's rows: the tree is replaced
   HIPC(c, hipSetDevice(c->device));
   double* d_state = nullptr;
   HIPC(c, hipMalloc((void**)&d_state, 10 * sizeof(double)));
@@ -765,6 +780,7 @@ int clrrt_tree_init(clrrt_ctx* c, const double root_state[10]) {
 int clrrt_tree_load(clrrt_ctx* c, const clrrt_node* nodes, int64_t n) {
   if (!c || n < 0 || (n > 0 && !nodes)) return CLRRT_EINVAL;
   pf_reset(c);
+  c->rep_n = 0;  // the tree is replaced
   if (n > c->cap.max_nodes) return fail(c, CLRRT_ECAPACITY, "tree_load: too many nodes");
   HIPC(c, hipSetDevice(c->device));
   if (n > 0) {
@@ -806,6 +822,8 @@ int clrrt_tree_rows(clrrt_ctx* c, int64_t row_offset, int64_t nrows, double* out
     return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   if (nrows == 0) return CLRRT_OK;
+  int rc = flush_replays(c);
+  if (rc != CLRRT_OK) return rc;
   HIPC(c, hipMemcpyAsync(out, c->arena + row_offset * 10, sizeof(double) * 10 * nrows, hipMemcpyDeviceToHost,
                          c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
@@ -894,6 +912,8 @@ int clrrt_path_commit(clrrt_ctx* c, const int32_t* ids, int32_t n, int32_t* n_re
   for (int i = 0; i < n; i++)
     if (ids[i] < 0 || ids[i] >= c->n_nodes) return fail(c, CLRRT_EINVAL, "path_commit: node id outside the tree");
   HIPC(c, hipSetDevice(c->device));
+  int frc = flush_replays(c);  // the path's rows are copied from the arena
+  if (frc != CLRRT_OK) return frc;
   if (n_remote) *n_remote = 0;
   c->path_n = 0;
   c->path_nrows = 0;
@@ -985,6 +1005,7 @@ int clrrt_path_transform(clrrt_ctx* c, int32_t dir, const double pose[3]) {
 int clrrt_tree_init_from_path(clrrt_ctx* c, const double car_state[6], int32_t* outcome) {
   if (!c || !car_state) return CLRRT_EINVAL;
   pf_reset(c);
+  c->rep_n = 0;  // the tree is replaced by the committed path's survivors (their rows: the path buffer)
   HIPC(c, hipSetDevice(c->device));
   int rc = path_reserve(c, std::max(1, c->path_n), std::max<int64_t>(1, c->path_nrows));
   if (rc != CLRRT_OK) return rc;
@@ -1139,6 +1160,11 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_coop") c->roll_coop = value != 0;
+  else if (k == "rows_deferred") {
+    int rc = flush_replays(c);
+    if (rc != CLRRT_OK) return rc;
+    c->rows_deferred = value != 0;
+  }
   else if (k == "exact_min_width" && value >= 1 && value <= 1 << 20) c->exact_min_width = (int)value;
   else if (k == "cu_split" && value >= 0 && value <= 7) {
     HIPC(c, hipStreamSynchronize(c->side));
@@ -1457,14 +1483,25 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     HIPC(c, hipEventRecord(c->ev_rs0, st));
     HIPC(c, hipStreamWaitEvent(rst, c->ev_rs0, 0));
   }
+  const bool persistent = c->roll_persistent && c->dp.n_steps_max > 0;
+  const bool deferred = persistent && c->rows_deferred;
+  if (!deferred) {  // rows into job slots: replays pending from a deferred round run first
+    int rc = flush_replays(c);
+    if (rc == CLRRT_OK) rc = ensure_slots(c);
+    if (rc != CLRRT_OK) return rc;
+  }
   {
     KTimer kt(c, 1, rst);
     RollArgs a = roll_args(c, n * CAND_K);
     a.res = c->res_spec;
     a.res_gb = c->res_gb;
-    a.slots = c->slots;
+    a.slots = deferred ? nullptr : c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
+    if (deferred) {  // this launch also replays the previous commit's accepted rollouts
+      a.rep = c->rep_buf;
+      a.nrep = c->rep_n;
+    }
     // persistent blocks (1 resident per CU: the step loop fills the register file).  The rollout kernel's
     // makespan is its longest chains, not its width, while the side stream's search of the next round
     // grows with the tree and takes the CUs the rollouts leave; so the grid narrows as the tree grows:
@@ -1481,10 +1518,12 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
     }
-    if (c->roll_persistent && c->dp.n_steps_max > 0)
+    if (persistent)
       HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
+    if (deferred) c->rep_n = 0;
+    c->eval_deferred = deferred;
   }
   if (c->roll_st) {
     HIPC(c, hipEventRecord(c->ev_rs1, rst));
@@ -1540,7 +1579,15 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   c->counters.fail_iterlimit += c->h_totals[5];
   c->counters.rollouts += c->h_totals[6];
   c->last_goal_nodes = c->h_totals[7];
-  {
+  if (c->eval_deferred) {  // the accepted rollouts are replayed into the arena by the next persistent launch
+    if (c->rep_n > 0) {
+      int rc = flush_replays(c);
+      if (rc != CLRRT_OK) return rc;
+    }
+    KTimer kt(c, 2);
+    HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->roll_prep, c->res_spec, c->rep_buf));
+    c->rep_n = (int)nn;
+  } else {
     KTimer kt(c, 2);
     HIPC(c, launch_copy_rows(st, c->jobs, c->out_nodes, (int)nn, c->slots, c->slot_rows,
                              (int)(c->cap.max_batch * CAND_K), c->arena));
@@ -1548,6 +1595,38 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   c->n_rows += nr;
   c->last_eval_rows = nr;
   *n_out = (int)nn;
+  return CLRRT_OK;
+}
+
+// Row slots for the paths that store speculative rows (option "rows_deferred" 0, non-persistent rollouts).
+static int ensure_slots(clrrt_ctx* c) {
+  const int need = c->dp.n_steps_max + 1;
+  if (c->slots && c->slot_rows >= need) return CLRRT_OK;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->slots) HIPC(c, hipFree(c->slots));
+  c->slots = nullptr;
+  c->slot_rows = 0;
+  HIPC(c, dalloc(&c->slots, (size_t)2 * need * 10 * c->cap.max_batch * CAND_K));
+  c->slot_rows = need;
+  return CLRRT_OK;
+}
+
+// Run the pending replays (the last commit's accepted rollouts, deferred rows) on their own: before
+// anything reads the arena, changes what a replay depends on (parameters, obstacles), or at the end of
+// an expansion.  Same kernel, no jobs of a round.
+static int flush_replays(clrrt_ctx* c) {
+  if (c->rep_n <= 0) return CLRRT_OK;
+  HIPC(c, hipSetDevice(c->device));
+  KTimer kt(c, 1);
+  RollArgs a = roll_args(c, 0);
+  a.res = c->res_spec;
+  a.res_gb = c->res_gb;
+  a.rep = c->rep_buf;
+  a.nrep = c->rep_n;
+  a.coop_enable = c->roll_coop;
+  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_prep, c->roll_q, c->roll_best, 4 * c->n_cu));
+  c->rep_n = 0;
   return CLRRT_OK;
 }
 
@@ -1872,6 +1951,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     }
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
+  // the last round's accepted rows (part of the query's output tree, so inside its time)
+  if (rc == CLRRT_OK) rc = flush_replays(c);
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->side2));
   HIPC(c, hipStreamSynchronize(c->stream));
@@ -2003,6 +2084,8 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if (exact) cur = std::max(c->exact_min_width, std::min(batch, L == nb ? 2 * nb : 2 * L));
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
+  // the last round's accepted rows (part of the query's output tree, so inside its time)
+  if (rc == CLRRT_OK) rc = flush_replays(c);
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->stream));
   st.nodes_added = c->n_nodes - nodes_before;

@@ -107,6 +107,10 @@ struct RollArgs {
   int B;
   int coop_off;     // k_roll_run's cooperative collision scratch: byte offset in the dynamic LDS
   int coop_enable;  // option "roll_coop": use it where it applies (launch_rollout_persistent)
+  // k_roll_run: replays of committed rollouts (deferred rows, see Replay in clrrt_kernels.hip), served
+  // before the round's jobs; slots == nullptr: the speculative rollouts store no rows
+  const void* rep;
+  int nrep;
 };
 
 struct SelArgs {
@@ -209,6 +213,11 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, v
                                      int blocks);
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t rollout_prep_bytes();
+size_t replay_bytes();
+// deferred rows: the committed rollouts' start states (jobs/recs from launch_compact, prep and res of the
+// round's k_roll_prep / k_roll_run) into out[0..n) for the next persistent launch's replays
+hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const void* prep,
+                                const RollRes* res, void* out);
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);

@@ -1144,6 +1144,21 @@ struct RollInit {
   int32_t valid, pad;
 };
 
+// Deferred trajectory rows.  k_roll_run stores no rows for the speculative rollouts (most of them fail or
+// are abandoned, and their rows would never be read); a commit records the accepted ones (k_replay_gather)
+// and the next k_roll_run launch replays them from the same start state, writing their rows straight into
+// the arena (rollouts are deterministic: same init, same steps, same rows).  A replay of a regular rollout
+// starts from k_roll_prep's Simulation state, a replay of a goal-biased one from the end of the regular
+// rollout it followed (as the gb follow-up itself did).  Replays take the queue's first positions.
+struct Replay {
+  RollInit ini;        // regular: the Simulation state after its ctor
+  double gst[10];      // goal-biased: the regular rollout's stateArray.back(), ref.back(), ref.v.back()
+  double gbx, gby, gvb;
+  int64_t row_off;     // arena row of stateArray[0]
+  int32_t nrows;       // rows the committed node holds
+  int32_t gb;
+};
+
 // Scheduling only: a rollout toward a sample 8-20 m away (1.7-4.2 turning radii) at 30-90 degrees off
 // the heading is the kind that ends in the iteration limit after the full horizon (the vehicle
 // circles without reaching the reference: tools/orbit_predict.py, cfg3 round 40: this class is 3% of
@@ -1195,10 +1210,12 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
   ini.valid = 1;
   ini.pad = 0;
   prep[j] = ini;
-  double* rows = a.slots + (int64_t)j * a.slot_rows * 10;
+  if (a.slots) {  // rows in job slots (rows not deferred)
+    double* rows = a.slots + (int64_t)j * a.slot_rows * 10;
 #pragma unroll
-  for (int k = 0; k < 10; k++) rows[k] = ps.v[k];
-  rows[7] = ini.c7;
+    for (int k = 0; k < 10; k++) rows[k] = ps.v[k];
+    rows[7] = ini.c7;
+  }
 }
 
 #ifndef REFILL_MIN
@@ -1237,6 +1254,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   double c7 = 0, c8 = 0, c9 = 0;
   int j = -1, k = 0, s = 0, pass = 0, steps = 0;
   bool exhausted = false;
+  // rows: where this lane's rollout writes stateArray (a replay's arena rows; nullptr for the speculative
+  // rollouts when rows are deferred, else their job slots); rp: the lane replays a committed rollout of
+  // nrows_rp rows
+  const Replay* __restrict__ reps = (const Replay*)a.rep;
+  const int nq = a.nrep + a.njobs;  // queue: the replays, then the round's jobs
+  double* rows = nullptr;
+  bool rp = false;
+  int nrows_rp = 0;
+  unsigned long long n_rep = 0, n_rep_bad = 0;
+  // a pending goal-biased rollout init (a successful rollout's gb follow-up, or a goal-biased replay):
+  // the regular rollout's end state, ref.back() and ref.v.back()
+  bool gbq = false;
+  double gst[10], gbx = 0, gby = 0, gvb = 0;
   PhaseClk pclk{};
 #ifdef CLRRT_ROLL_PROFILE
   PhaseClk* pc = &pclk;
@@ -1260,32 +1290,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   // every step for one or two lanes.
   auto finish_parked = [&]() {
     if (fin >= 0) {
-      RollRes out;
-      finish_rollout(r, c7, c8, c9, fin, steps, out);
-      if (pass == 1) {
-        a.res_gb[j] = out;
+      if (rp) {  // a replay: its rows are written; check it ran as long as the committed rollout
+        n_rep++;
+        n_rep_bad += (steps + 1 != nrows_rp);
+        rp = false;
+        rows = nullptr;
         j = -1;
       } else {
-        a.res[j] = out;
-        const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
-        if (ok) atomicMin(&best[s], k);
-        if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
-          // goal-biased rollout from the node this rollout would append (expandTree :163-173)
-          const RefD R = make_goal_ref(out.bx, out.by, a.p);
-          roll_init(r, out.st, R, out.vback, true, a.p);
-          c7 = (double)r.wp; c8 = out.st[8]; c9 = out.st[9];
-          pass = 1;
-          steps = 0;
-          double* rows = a.slots + pass_stride + j * slot;
-#pragma unroll
-          for (int q = 0; q < 10; q++) rows[q] = out.st[q];
-          rows[7] = c7;
-        } else {
-          a.res_gb[j].outcome = -1;
+        RollRes out;
+        finish_rollout(r, c7, c8, c9, fin, steps, out);
+        if (pass == 1) {
+          a.res_gb[j] = out;
           j = -1;
+        } else {
+          a.res[j] = out;
+          const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
+          if (ok) atomicMin(&best[s], k);
+          if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
+            // goal-biased rollout from the node this rollout would append (expandTree :163-173)
+#pragma unroll
+            for (int q = 0; q < 10; q++) gst[q] = out.st[q];
+            gbx = out.bx; gby = out.by; gvb = out.vback;
+            gbq = true;
+            pass = 1;
+            rows = a.slots ? a.slots + pass_stride + j * slot : nullptr;
+          } else {
+            a.res_gb[j].outcome = -1;
+            j = -1;
+          }
         }
       }
       fin = -1;
+    }
+  };
+  // the pending goal-biased init (one code site for the follow-ups and the goal-biased replays)
+  auto gb_init = [&]() {
+    if (gbq) {
+      const RefD R = make_goal_ref(gbx, gby, a.p);
+      roll_init(r, gst, R, gvb, true, a.p);
+      c7 = (double)r.wp; c8 = gst[8]; c9 = gst[9];
+      steps = 0;
+      if (rows) {
+#pragma unroll
+        for (int q = 0; q < 10; q++) rows[q] = gst[q];
+        rows[7] = c7;
+      }
+      gbq = false;
     }
   };
   for (;;) {
@@ -1308,10 +1358,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         base = __shfl(base, leader, 64);
         if (idle) {
           const int q0 = base + __popcll(m & ((1ull << lane) - 1));
-          if (q0 >= a.njobs) {
+          if (q0 >= nq) {
             exhausted = true;
+          } else if (q0 < a.nrep) {  // replay of a committed rollout: rows into the arena
+            const Replay& rq = reps[q0];
+            rp = true;
+            nrows_rp = rq.nrows;
+            rows = a.arena + rq.row_off * 10;
+            j = 0;  // busy (replays touch no per-job result)
+            k = 0; s = 0; pass = 0; steps = 0;
+            if (rq.gb) {
+#pragma unroll
+              for (int q = 0; q < 10; q++) gst[q] = rq.gst[q];
+              gbx = rq.gbx; gby = rq.gby; gvb = rq.gvb;
+              gbq = true;
+            } else {
+              r = rq.ini.r;
+              c7 = rq.ini.c7; c8 = rq.ini.c8; c9 = rq.ini.c9;
+              store_row(rows, 1, r, c7, c8, c9);
+            }
           } else {
-            const int q = a.perm ? a.perm[q0] : q0;
+            const int qj = q0 - a.nrep;
+            const int q = a.perm ? a.perm[qj] : qj;
             k = q / B;
             s = q - k * B;
             j = s * CAND_K + k;
@@ -1324,6 +1392,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
               pass = 0;
               steps = 0;
+              rows = a.slots ? a.slots + j * slot : nullptr;
 #ifdef CLRRT_ROLL_PROFILE
               job_steps = 0;
 #endif
@@ -1332,6 +1401,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         }
         qdone = qdone || __ballot(exhausted) != 0;
       }
+      gb_init();
       if (pc) pc->mark(6);
       continue;
     }
@@ -1351,7 +1421,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       // and stores in issue order, so a load issued after the stores would wait for all ten of them to
       // complete (measured: ~60% of the kernel's wave time); issued here it only waits for the previous
       // step's stores, long retired.
-      const bool check = (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
+      const bool check = !rp && (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
       best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
       if (pc) pc->mark(6);
       d2 = roll_step_pre(r, a.p, c7, c8, c9, w, pc);
@@ -1374,7 +1444,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     }
 #endif
     w.steps++;
-    store_row(a.slots + pass * pass_stride + j * slot + (int64_t)steps * 10, 1, r, c7, c8, c9);
+    if (rows) store_row(rows + (int64_t)steps * 10, 1, r, c7, c8, c9);
     if (pc) pc->mark(5);
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
@@ -1398,6 +1468,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       atomicAdd(&a.ctr[0], v0);
       atomicAdd(&a.ctr[1], v1);
       atomicAdd(&a.ctr[2], v2);
+    }
+    if (n_rep) {  // replays run, replays whose row count differs from the committed node's (must stay 0)
+      atomicAdd(&a.ctr[60], n_rep);
+      if (n_rep_bad) atomicAdd(&a.ctr[61], n_rep_bad);
     }
   }
 #ifdef CLRRT_ROLL_PROFILE
@@ -1623,6 +1697,38 @@ __global__ void __launch_bounds__(256) k_copy_rows(const Job* __restrict__ jobs,
   const double* src = slots + ((int64_t)jb.gb * slot_jobs + jb.parent) * slot_rows * 10;
   double* dst = arena + jb.row_off * 10;
   for (int t = threadIdx.x; t < n; t += blockDim.x) dst[t] = src[t];
+}
+
+// Commit with deferred rows: the accepted rollouts' start states for the next k_roll_run's replays (one
+// lane per committed node; jobs[] from k_compact_scatter: parent = the job, gb = pass).
+__global__ void __launch_bounds__(256) k_replay_gather(const Job* __restrict__ jobs, const clrrt_node* __restrict__ recs,
+                                                       int n, const RollInit* __restrict__ prep,
+                                                       const RollRes* __restrict__ res, Replay* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Job jb = jobs[i];
+  Replay& o = out[i];
+  o.row_off = jb.row_off;
+  o.nrows = recs[i].nrows;
+  o.gb = jb.gb;
+  if (jb.gb) {
+    const RollRes& g = res[jb.parent];
+#pragma unroll
+    for (int q = 0; q < 10; q++) o.gst[q] = g.st[q];
+    o.gbx = g.bx; o.gby = g.by; o.gvb = g.vback;
+  } else {
+    o.ini = prep[jb.parent];
+  }
+}
+
+size_t replay_bytes() { return sizeof(Replay); }
+
+hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const void* prep,
+                                const RollRes* res, void* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_replay_gather, dim3((n + 255) / 256), dim3(256), 0, st, jobs, recs, n, (const RollInit*)prep, res,
+                     (Replay*)out);
+  return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256) k_bbox(const clrrt_node* __restrict__ recs, const int64_t* n_dev, int n_host,
@@ -2265,7 +2371,7 @@ static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
 
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, void* prep, int* qnext, int* best,
                                      int blocks) {
-  if (a0.njobs <= 0) return hipSuccess;
+  if (a0.njobs <= 0 && a0.nrep <= 0) return hipSuccess;
   hipError_t e;
   if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
@@ -2285,16 +2391,21 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
                                 : (const void*)&k_roll_run<false, false>;
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
-  const int nb = blocks < (a0.njobs + 255) / 256 ? blocks : (a0.njobs + 255) / 256;
+  const int nqueue = a0.njobs + a0.nrep;
+  const int nb = blocks < (nqueue + 255) / 256 ? blocks : (nqueue + 255) / 256;
   if (a.p.need_gap) {
-    hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
-    LAUNCH_CHECK();
-    if ((e = roll_order(st, a)) != hipSuccess) return e;
+    if (a.njobs > 0) {
+      hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
+      LAUNCH_CHECK();
+      if ((e = roll_order(st, a)) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
   } else {
-    hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
-    LAUNCH_CHECK();
-    if ((e = roll_order(st, a)) != hipSuccess) return e;
+    if (a.njobs > 0) {
+      hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
+      LAUNCH_CHECK();
+      if ((e = roll_order(st, a)) != hipSuccess) return e;
+    }
     if (coop)
       hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
     else

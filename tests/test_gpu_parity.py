@@ -313,11 +313,12 @@ def test_pipelined_batch_rounds_identical():
     rollout queue order (roll_priority), the persistent grid width (roll_blocks), the per-lane collision
     checks instead of the wave-cooperative ones (roll_coop), the single-buffered
     walk index (nn_walk_double) and the walk without overflow split (budget 0) or with every sample
-    split (budget 1)."""
+    split (budget 1); and the trajectory rows stored by every speculative rollout (rows_deferred 0) instead of
+    replayed for the accepted ones only (the default: each replay must run exactly its node's row count)."""
     mode, obs = _scene("obb200")
     trees = []
     variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=2), dict(roll_priority=0, roll_blocks=512),
-                dict(roll_coop=0),
+                dict(roll_coop=0), dict(rows_deferred=0),
                 dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
                 dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
     for opts in variants:
@@ -331,6 +332,9 @@ def test_pipelined_batch_rounds_identical():
         assert st["rounds"] == 6
         n, nr = pl.size()
         trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n))
+        d = pl.debug_counters()
+        assert d[61] == 0, f"{d[61]} replays ran a different row count ({opts})"
+        assert (d[60] > 0) == (opts.get("rows_deferred", 1) != 0), (d[60], opts)
         pl.close()
     print(f"pipelined rounds: {trees[1][2]} nodes")
     assert trees[0][2] > 20000
@@ -362,6 +366,7 @@ def test_round_prefetch_identical():
             pl.round_commit(out.data_ptr(), n, 0, n)
         n_nodes, nr = pl.size()
         trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n_nodes))
+        assert pl.debug_counters()[61] == 0
         pl.close()
     print(f"round prefetch: {trees[1][2]} nodes")
     assert trees[0][2] > 20000
