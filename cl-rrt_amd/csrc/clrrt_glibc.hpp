@@ -14,6 +14,9 @@
 // Domain restated: |x| < 105414350 for sin/cos (beyond that glibc switches to __branred: we fall
 // back to the GPU libm, outside anything the planner evaluates); |x| <= 0.787 for tan (steering
 // angles are clamped to +-0.52 rad; larger arguments fall back likewise).  NaN/Inf propagate.
+// Provenance: the algorithms, constants and tables restated here are glibc's (GNU C Library 2.35, libm;
+// the IBM Accurate Mathematical Library sources, (C) IBM Corp. and the Free Software Foundation), which
+// glibc distributes under the GNU Lesser General Public License v2.1 or later.
 #pragma once
 #include <stdint.h>
 #include <string.h>

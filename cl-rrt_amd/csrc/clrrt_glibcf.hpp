@@ -8,6 +8,10 @@
 // rounds ~35% of their results differently, which reorders near-tied keys; these restatements make the
 // device keys the reference's keys bit for bit.  Checked against the host libm on every float argument
 // (atanf, acosf, asinf) and on 10^8 random and edge-case pairs (atan2f): tests/native/glibcf_check.cpp.
+// Provenance: glibc 2.35's float atan/atan2/acos/asin derive from Sun Microsystems' fdlibm ("Copyright (C)
+// 1993 by Sun Microsystems, Inc. ... Permission to use, copy, modify, and distribute this software is
+// freely granted, provided that this notice is preserved"); glibc distributes them under the GNU Lesser
+// General Public License v2.1 or later.
 #pragma once
 #include <stdint.h>
 #include <string.h>

@@ -8,6 +8,8 @@
 // to its algorithm — decides which parent is expanded.  EXACT mode therefore replays the same
 // algorithm on samples whose candidate list contains such a tie.  Usable on host (tests) and
 // device (one lane per sample).
+// Provenance: the algorithm restated is libstdc++'s std::sort (GCC 11, (C) the Free Software Foundation),
+// distributed under the GNU General Public License v3 with the GCC Runtime Library Exception.
 #pragma once
 #include <stdint.h>
 

@@ -185,6 +185,8 @@ def main():
             sys.exit(f"atan2 cij row {i}: {cij[7 * i:7 * i + 7]}")
     lines = [
         "// clrrt_glibc_data.hpp — GENERATED by tools/gen_glibc_libm.py; do not edit.",
+        "// Provenance: glibc 2.35 libm's data (the IBM Accurate Mathematical Library, (C) IBM Corp. and the Free",
+        "// Software Foundation), distributed by glibc under the GNU Lesser General Public License v2.1 or later.",
         "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c), tan (s_tan.c) and atan2 (e_atan2.c)",
         "// as loaded by its FMA variants, read from the libm image the CPU oracle links (hash-checked);",
         "// __sincostab cross-checked against 60-digit sin/cos(k/128).",
