@@ -113,12 +113,11 @@ struct clrrt_ctx {
   WalkBufs nnw_alt{};
   struct { int64_t n = -1; double ox, oy, x0, y0, x1, y1; float delta; } nnw_built;
   CompactBufs cmp{};                   // round compaction scratch
-  // persistent rollouts (k_roll_prep + k_roll_run)
+  // persistent rollouts (k_roll_run; k_roll_flag + k_roll_order for the queue order)
   int roll_persistent = 1;
   int nn_debug = 0;
   int roll_blocks = 0;       // persistent blocks (0: 5/8 of the CUs)
   int n_cu = 256;
-  void* roll_prep = nullptr;  // [max_batch * CAND_K] RollInit
   int* roll_q = nullptr;      // [1] queue head
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
@@ -422,7 +421,7 @@ static void free_all(clrrt_ctx* c) {
   void* ptrs[] = {c->tree, c->nn, c->arena, c->obs, c->d_samples, c->pk, c->pi, c->cand, c->ckey, c->ncand,
                   c->ctie, c->sort_scratch, c->res_spec, c->regnodes, c->res_gb, c->gbnodes, c->so, c->first_conflict,
                   c->out_nodes, c->jobs, c->slots, c->rep_buf, c->totals, c->work_ctr, c->grid_buf,
-                  c->nn_seed, c->d_bbox, c->roll_prep, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag,
+                  c->nn_seed, c->d_bbox, c->roll_q, c->roll_best, c->roll_perm, c->roll_pflag,
                   c->goal_recs, c->bp_path, c->path_nodes, c->path_rows, c->ri_int, c->ri_off, c->ri_cost,
                   c->ri_terms, c->nnw.keys, c->nnw.keys2, c->nnw.vals, c->nnw.vals2, c->nnw.tmp, c->nnw.P, c->nnw.Q,
                   c->nnw.CE, c->nnw.ID, c->nnw.tiles, c->nnw.supers, c->nnw.sorder, c->nnw.HEAD, c->nnw.ovf_n, c->nnw.ovf, c->nnw.pk, c->nnw.pi, c->nnw_alt.keys, c->nnw_alt.keys2, c->nnw_alt.vals, c->nnw_alt.vals2, c->nnw_alt.tmp, c->nnw_alt.P, c->nnw_alt.Q, c->nnw_alt.CE, c->nnw_alt.ID, c->nnw_alt.tiles, c->nnw_alt.supers, c->nnw_alt.sorder, c->nnw_alt.HEAD, c->nnw_alt.ovf_n, c->nnw_alt.ovf, c->nnw_alt.pk, c->nnw_alt.pi, c->nnw.skeys, c->nnw.sids, c->nnw_alt.skeys, c->nnw_alt.sids, c->cmp.packed, c->cmp.scanned,
@@ -520,7 +519,6 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   c->cmp.tmp_bytes = compact_scan_bytes((int)B);
   chk(hipMalloc(&c->cmp.tmp, std::max<size_t>(c->cmp.tmp_bytes, 256)));
   chk(dalloc(&c->nn_seed, B));
-  chk(hipMalloc(&c->roll_prep, rollout_prep_bytes() * (size_t)B * CAND_K));
   chk(dalloc(&c->roll_q, 1));
   chk(dalloc(&c->roll_best, B));
   chk(dalloc(&c->roll_perm, (int64_t)B * CAND_K));
@@ -1519,7 +1517,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.pflag = c->roll_pflag;
     }
     if (persistent)
-      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_prep, c->roll_q, c->roll_best, blocks));
+      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
     if (deferred) c->rep_n = 0;
@@ -1585,7 +1583,8 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
       if (rc != CLRRT_OK) return rc;
     }
     KTimer kt(c, 2);
-    HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->roll_prep, c->res_spec, c->rep_buf));
+    HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->tree, c->cand, c->d_samples, c->res_spec,
+                                 c->rep_buf));
     c->rep_n = (int)nn;
   } else {
     KTimer kt(c, 2);
@@ -1625,7 +1624,7 @@ static int flush_replays(clrrt_ctx* c) {
   a.rep = c->rep_buf;
   a.nrep = c->rep_n;
   a.coop_enable = c->roll_coop;
-  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_prep, c->roll_q, c->roll_best, 4 * c->n_cu));
+  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, 4 * c->n_cu));
   c->rep_n = 0;
   return CLRRT_OK;
 }

@@ -99,7 +99,7 @@ struct RollArgs {
   RollRes* __restrict__ res_gb;            // SPEC: goal-biased rollout (outcome -1 = not run)
   unsigned long long* ctr;  // [3] steps, scan points, box tests (nullable)
   int njobs;
-  // persistent rollouts: queue order (nullable).  k_roll_prep flags the jobs likely to run long
+  // persistent rollouts: queue order (nullable).  k_roll_flag flags the jobs likely to run long
   // (pflag[q], q = k B + s), the queue serves them first (perm[position] = q); results do not depend
   // on the order
   int* perm;
@@ -207,17 +207,15 @@ hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, co
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                 int* ncand);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
-// Round rollouts as k_roll_prep + persistent k_roll_run (see clrrt_kernels.hip); prep holds
-// njobs * rollout_prep_bytes(), best B ints, qnext one int.
-hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, void* prep, int* qnext, int* best,
-                                     int blocks);
+// Round rollouts (and the pending replays a.rep[0..nrep)) as the persistent k_roll_run, behind k_roll_flag +
+// k_roll_order when a.perm / a.pflag are set (see clrrt_kernels.hip); best B ints, qnext one int.
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, int* qnext, int* best, int blocks);
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
-size_t rollout_prep_bytes();
 size_t replay_bytes();
 // deferred rows: the committed rollouts' start states (jobs/recs from launch_compact, prep and res of the
 // round's k_roll_prep / k_roll_run) into out[0..n) for the next persistent launch's replays
-hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const void* prep,
-                                const RollRes* res, void* out);
+hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const clrrt_node* tree,
+                                const int* cand, const clrrt_sample* S, const RollRes* res, void* out);
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);

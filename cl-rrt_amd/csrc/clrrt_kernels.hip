@@ -1138,25 +1138,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 //                 running) -- expandTree never looks past the first success (:150-160), so the
 //                 round's result is unchanged.  A successful regular rollout that passes the
 //                 goal-bias gate continues in the same lane with the goal-biased rollout.
-struct RollInit {
-  Roll r;
-  double c7, c8, c9;
-  int32_t valid, pad;
+// What a rollout starts from (getReference / getGoalReference + the Simulation ctor): the parent state,
+// the parent's ref.back() and ref.v.back(), the sample (regular rollouts) and the goal-bias flag.
+struct RollSrc {
+  double st[10];
+  double bx, by, vb;   // parent ref.back(), ref.v.back()
+  double sx, sy;       // sample (regular)
+  int32_t gb, pad;
 };
 
 // Deferred trajectory rows.  k_roll_run stores no rows for the speculative rollouts (most of them fail or
 // are abandoned, and their rows would never be read); a commit records the accepted ones (k_replay_gather)
-// and the next k_roll_run launch replays them from the same start state, writing their rows straight into
-// the arena (rollouts are deterministic: same init, same steps, same rows).  A replay of a regular rollout
-// starts from k_roll_prep's Simulation state, a replay of a goal-biased one from the end of the regular
-// rollout it followed (as the gb follow-up itself did).  Replays take the queue's first positions.
+// and the next k_roll_run launch replays them from the same start, writing their rows straight into the
+// arena (rollouts are deterministic: same start, same steps, same rows).  A regular rollout starts from its
+// parent node and sample, a goal-biased one from the end of the regular rollout it followed.  Replays
+// take the queue's first positions.
 struct Replay {
-  RollInit ini;        // regular: the Simulation state after its ctor
-  double gst[10];      // goal-biased: the regular rollout's stateArray.back(), ref.back(), ref.v.back()
-  double gbx, gby, gvb;
+  RollSrc src;
   int64_t row_off;     // arena row of stateArray[0]
   int32_t nrows;       // rows the committed node holds
-  int32_t gb;
+  int32_t pad;
 };
 
 // Scheduling only: a rollout toward a sample 8-20 m away (1.7-4.2 turning radii) at 30-90 degrees off
@@ -1184,38 +1185,14 @@ __global__ void __launch_bounds__(256) k_roll_order(const int* __restrict__ pfla
   perm[pos] = q;
 }
 
-template <bool NEED_GAP>
-__global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restrict__ prep) {
-  glibc::stage_tables();
+// Queue order flags (roll_priority): pflag[q] for queue position q = k B + s, 1 for the jobs likely to run
+// the whole horizon (roll_likely_long); k_roll_order then serves them first.
+__global__ void __launch_bounds__(256) k_roll_flag(RollArgs a) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= a.njobs) return;
   const int id = a.cand[j];
-  int* pflag = a.pflag ? a.pflag + (j % CAND_K) * a.B + j / CAND_K : nullptr;  // queue position q = k B + s
-  if (id < 0) {
-    prep[j].valid = 0;
-    if (pflag) *pflag = 0;
-    return;
-  }
-  const clrrt_node& n = a.tree[id];
-  St10 ps;
-#pragma unroll
-  for (int k = 0; k < 10; k++) ps.v[k] = n.state[k];
-  if (pflag) *pflag = roll_likely_long(ps.v, a.samples[j / CAND_K].x, a.samples[j / CAND_K].y);
-  const RefD R = make_ref(n.ref_back[0], n.ref_back[1], a.samples[j / CAND_K].x, a.samples[j / CAND_K].y, a.p);
-  RollInit ini;
-  roll_init(ini.r, ps.v, R, n.ref_vback, false, a.p);
-  ini.c7 = (double)ini.r.wp;
-  ini.c8 = ps.v[8];
-  ini.c9 = ps.v[9];
-  ini.valid = 1;
-  ini.pad = 0;
-  prep[j] = ini;
-  if (a.slots) {  // rows in job slots (rows not deferred)
-    double* rows = a.slots + (int64_t)j * a.slot_rows * 10;
-#pragma unroll
-    for (int k = 0; k < 10; k++) rows[k] = ps.v[k];
-    rows[7] = ini.c7;
-  }
+  a.pflag[(j % CAND_K) * a.B + j / CAND_K] =
+      id < 0 ? 0 : roll_likely_long(a.tree[id].state, a.samples[j / CAND_K].x, a.samples[j / CAND_K].y);
 }
 
 #ifndef REFILL_MIN
@@ -1232,7 +1209,7 @@ __global__ void __launch_bounds__(256) k_roll_prep(RollArgs a, RollInit* __restr
 // COOP: the collision check is obs_distance_coop (OBB collision without the gap value, static grid built,
 // the per-wave LDS scratch after the obstacle tables at a.coop_off)
 template <bool NEED_GAP, bool COOP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLL_WAVES))) k_roll_run(RollArgs a, const RollInit* __restrict__ prep,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLL_WAVES))) k_roll_run(RollArgs a,
                                                   int* __restrict__ qnext, int* __restrict__ best, int B) {
   extern __shared__ float4 lds[];
   glibc::stage_tables();
@@ -1263,10 +1240,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   bool rp = false;
   int nrows_rp = 0;
   unsigned long long n_rep = 0, n_rep_bad = 0;
-  // a pending goal-biased rollout init (a successful rollout's gb follow-up, or a goal-biased replay):
-  // the regular rollout's end state, ref.back() and ref.v.back()
-  bool gbq = false;
-  double gst[10], gbx = 0, gby = 0, gvb = 0;
+  // a pending rollout start (a fetched job or replay, a successful rollout's goal-biased follow-up): the
+  // Simulation is constructed for all of them at one code site (init_pending) after the fetch
+  bool iq = false;
+  RollSrc src;
   PhaseClk pclk{};
 #ifdef CLRRT_ROLL_PROFILE
   PhaseClk* pc = &pclk;
@@ -1309,9 +1286,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
             // goal-biased rollout from the node this rollout would append (expandTree :163-173)
 #pragma unroll
-            for (int q = 0; q < 10; q++) gst[q] = out.st[q];
-            gbx = out.bx; gby = out.by; gvb = out.vback;
-            gbq = true;
+            for (int q = 0; q < 10; q++) src.st[q] = out.st[q];
+            src.bx = out.bx; src.by = out.by; src.vb = out.vback;
+            src.gb = 1;
+            iq = true;
             pass = 1;
             rows = a.slots ? a.slots + pass_stride + j * slot : nullptr;
           } else {
@@ -1323,19 +1301,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       fin = -1;
     }
   };
-  // the pending goal-biased init (one code site for the follow-ups and the goal-biased replays)
-  auto gb_init = [&]() {
-    if (gbq) {
-      const RefD R = make_goal_ref(gbx, gby, a.p);
-      roll_init(r, gst, R, gvb, true, a.p);
-      c7 = (double)r.wp; c8 = gst[8]; c9 = gst[9];
+  // getReference / getGoalReference + Simulation ctor of the pending starts (rrtplanner.cpp:146-149,
+  // :165-168; simulation.cpp:36-47), and stateArray[0] when the lane writes rows
+  auto init_pending = [&]() {
+    if (iq) {
+      const RefD R = src.gb ? make_goal_ref(src.bx, src.by, a.p) : make_ref(src.bx, src.by, src.sx, src.sy, a.p);
+      roll_init(r, src.st, R, src.vb, src.gb != 0, a.p);
+      c7 = (double)r.wp; c8 = src.st[8]; c9 = src.st[9];
       steps = 0;
       if (rows) {
 #pragma unroll
-        for (int q = 0; q < 10; q++) rows[q] = gst[q];
+        for (int q = 0; q < 10; q++) rows[q] = src.st[q];
         rows[7] = c7;
       }
-      gbq = false;
+      iq = false;
     }
   };
   for (;;) {
@@ -1367,29 +1346,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
             rows = a.arena + rq.row_off * 10;
             j = 0;  // busy (replays touch no per-job result)
             k = 0; s = 0; pass = 0; steps = 0;
-            if (rq.gb) {
-#pragma unroll
-              for (int q = 0; q < 10; q++) gst[q] = rq.gst[q];
-              gbx = rq.gbx; gby = rq.gby; gvb = rq.gvb;
-              gbq = true;
-            } else {
-              r = rq.ini.r;
-              c7 = rq.ini.c7; c8 = rq.ini.c8; c9 = rq.ini.c9;
-              store_row(rows, 1, r, c7, c8, c9);
-            }
+            src = rq.src;
+            iq = true;
           } else {
             const int qj = q0 - a.nrep;
             const int q = a.perm ? a.perm[qj] : qj;
             k = q / B;
             s = q - k * B;
             j = s * CAND_K + k;
-            if (!prep[j].valid || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+            const int id = a.cand[j];
+            if (id < 0 || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
               a.res[j].outcome = -1;
               a.res_gb[j].outcome = -1;
               j = -1;
             } else {
-              r = prep[j].r;
-              c7 = prep[j].c7; c8 = prep[j].c8; c9 = prep[j].c9;
+              const clrrt_node& n = a.tree[id];
+#pragma unroll
+              for (int q = 0; q < 10; q++) src.st[q] = n.state[q];
+              src.bx = n.ref_back[0]; src.by = n.ref_back[1]; src.vb = n.ref_vback;
+              src.sx = a.samples[s].x; src.sy = a.samples[s].y;
+              src.gb = 0;
+              iq = true;
               pass = 0;
               steps = 0;
               rows = a.slots ? a.slots + j * slot : nullptr;
@@ -1401,7 +1378,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         }
         qdone = qdone || __ballot(exhausted) != 0;
       }
-      gb_init();
+      init_pending();
       if (pc) pc->mark(6);
       continue;
     }
@@ -1702,31 +1679,40 @@ __global__ void __launch_bounds__(256) k_copy_rows(const Job* __restrict__ jobs,
 // Commit with deferred rows: the accepted rollouts' start states for the next k_roll_run's replays (one
 // lane per committed node; jobs[] from k_compact_scatter: parent = the job, gb = pass).
 __global__ void __launch_bounds__(256) k_replay_gather(const Job* __restrict__ jobs, const clrrt_node* __restrict__ recs,
-                                                       int n, const RollInit* __restrict__ prep,
+                                                       int n, const clrrt_node* __restrict__ tree,
+                                                       const int* __restrict__ cand, const clrrt_sample* __restrict__ S,
                                                        const RollRes* __restrict__ res, Replay* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Job jb = jobs[i];
-  Replay& o = out[i];
+  Replay o;
   o.row_off = jb.row_off;
   o.nrows = recs[i].nrows;
-  o.gb = jb.gb;
-  if (jb.gb) {
+  o.pad = 0;
+  o.src.gb = jb.gb;
+  o.src.pad = 0;
+  if (jb.gb) {  // from the end of the regular rollout of the same job
     const RollRes& g = res[jb.parent];
 #pragma unroll
-    for (int q = 0; q < 10; q++) o.gst[q] = g.st[q];
-    o.gbx = g.bx; o.gby = g.by; o.gvb = g.vback;
-  } else {
-    o.ini = prep[jb.parent];
+    for (int q = 0; q < 10; q++) o.src.st[q] = g.st[q];
+    o.src.bx = g.bx; o.src.by = g.by; o.src.vb = g.vback;
+    o.src.sx = o.src.sy = 0.0;
+  } else {  // from the job's parent node toward its sample
+    const clrrt_node& p = tree[cand[jb.parent]];
+#pragma unroll
+    for (int q = 0; q < 10; q++) o.src.st[q] = p.state[q];
+    o.src.bx = p.ref_back[0]; o.src.by = p.ref_back[1]; o.src.vb = p.ref_vback;
+    o.src.sx = S[jb.parent / CAND_K].x; o.src.sy = S[jb.parent / CAND_K].y;
   }
+  out[i] = o;
 }
 
 size_t replay_bytes() { return sizeof(Replay); }
 
-hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const void* prep,
-                                const RollRes* res, void* out) {
+hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const clrrt_node* tree,
+                                const int* cand, const clrrt_sample* S, const RollRes* res, void* out) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_replay_gather, dim3((n + 255) / 256), dim3(256), 0, st, jobs, recs, n, (const RollInit*)prep, res,
+  hipLaunchKernelGGL(k_replay_gather, dim3((n + 255) / 256), dim3(256), 0, st, jobs, recs, n, tree, cand, S, res,
                      (Replay*)out);
   return hipGetLastError();
 }
@@ -2369,13 +2355,11 @@ static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, void* prep, int* qnext, int* best,
-                                     int blocks) {
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, int* qnext, int* best, int blocks) {
   if (a0.njobs <= 0 && a0.nrep <= 0) return hipSuccess;
   hipError_t e;
   if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
-  RollInit* pr = (RollInit*)prep;
   RollArgs a = a0;
   a.B = B;
   // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then (COOP) the cooperative
@@ -2393,29 +2377,23 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
     return e;
   const int nqueue = a0.njobs + a0.nrep;
   const int nb = blocks < (nqueue + 255) / 256 ? blocks : (nqueue + 255) / 256;
-  if (a.p.need_gap) {
-    if (a.njobs > 0) {
-      hipLaunchKernelGGL((k_roll_prep<true>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
-      LAUNCH_CHECK();
-      if ((e = roll_order(st, a)) != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+  if (a.njobs > 0 && a.perm && a.pflag) {  // queue order: the likely-long jobs first
+    hipLaunchKernelGGL(k_roll_flag, dim3((a.njobs + 255) / 256), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    if ((e = roll_order(st, a)) != hipSuccess) return e;
   } else {
-    if (a.njobs > 0) {
-      hipLaunchKernelGGL((k_roll_prep<false>), dim3((a.njobs + 255) / 256), dim3(256), 0, st, a, pr);
-      LAUNCH_CHECK();
-      if ((e = roll_order(st, a)) != hipSuccess) return e;
-    }
-    if (coop)
-      hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
-    else
-      hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, pr, qnext, best, B);
+    a.perm = nullptr;
   }
+  if (a.p.need_gap)
+    hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  else if (coop)
+    hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  else
+    hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
   LAUNCH_CHECK();
   return hipSuccess;
 }
 
-size_t rollout_prep_bytes() { return sizeof(RollInit); }
 
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
   if (src == SRC_SPEC) return launch_roll_t<SRC_SPEC>(st, a);
