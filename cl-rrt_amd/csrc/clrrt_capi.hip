@@ -122,6 +122,7 @@ struct clrrt_ctx {
   int* roll_best = nullptr;   // [max_batch] first successful candidate per sample
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
   int roll_coop = 1;          // option "roll_coop": wave-cooperative collision checks in k_roll_run
+  int roll_spread = 1;        // option "roll_spread": a short queue is spread over the persistent waves
   int exact_min_width = 8;    // option "exact_min_width": EXACT rounds speculate at least this many samples
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
@@ -1158,6 +1159,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_coop") c->roll_coop = value != 0;
+  else if (k == "roll_spread") c->roll_spread = value != 0;
   else if (k == "rows_deferred") {
     int rc = flush_replays(c);
     if (rc != CLRRT_OK) return rc;
@@ -1512,6 +1514,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
                        : c->cu_split > 0  ? std::max(1, (c->cu_split * c->n_cu) / 8)
                                           : std::max(1, (eighths * c->n_cu) / 8);
     a.coop_enable = c->roll_coop;
+    a.lanes_per_wave = c->roll_spread ? 0 : 64;
     if (c->roll_priority) {
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
@@ -1624,7 +1627,8 @@ static int flush_replays(clrrt_ctx* c) {
   a.rep = c->rep_buf;
   a.nrep = c->rep_n;
   a.coop_enable = c->roll_coop;
-  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, 4 * c->n_cu));
+  a.lanes_per_wave = c->roll_spread ? 0 : 64;
+  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, c->n_cu));
   c->rep_n = 0;
   return CLRRT_OK;
 }

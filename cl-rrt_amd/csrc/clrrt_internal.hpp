@@ -111,6 +111,9 @@ struct RollArgs {
   // before the round's jobs; slots == nullptr: the speculative rollouts store no rows
   const void* rep;
   int nrep;
+  // k_roll_run lanes per wave that take jobs: <= 0 spreads the queue over the grid's waves (set by
+  // launch_rollout_persistent), 64 fills every lane (option "roll_spread" 0)
+  int lanes_per_wave;
 };
 
 struct SelArgs {

@@ -1260,6 +1260,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
+  // lanes that take jobs (a.lanes_per_wave: a short queue is spread over the grid's waves, so a rollout
+  // shares its wave with few others -- each step of a wave runs the union of its lanes' paths -- and the
+  // idle lanes still serve the cooperative collision checks)
+  const bool lane_on = lane < a.lanes_per_wave;
+  const int refill_min = min(REFILL_MIN, max(1, a.lanes_per_wave / 4));  // parked/idle lanes that trigger a batch
 
   // Rollouts that ended wait (parked) until enough lanes are parked or idle; then the wave finishes
   // them together (result store, best[], goal-bias gate + goal-biased rollout init) and refills the
@@ -1321,13 +1326,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (pc) pc->mark(0);
     const uint64_t parked = __ballot(fin >= 0);
     const uint64_t busy0 = __ballot(j >= 0 && fin < 0);
-    const uint64_t m0 = __ballot(j < 0 && !qdone);
+    const uint64_t m0 = __ballot(j < 0 && !qdone && lane_on);
     // once the queue is empty, finish parked rollouts at once: a goal-biased follow-up (up to the whole
     // horizon) must not wait for other lanes to end
-    if ((parked | m0) && (__popcll(parked | m0) >= REFILL_MIN || busy0 == 0 || (qdone && parked))) {
+    if ((parked | m0) && (__popcll(parked | m0) >= refill_min || busy0 == 0 || (qdone && parked))) {
       finish_parked();
       if (pc) pc->mark(7);
-      const bool idle = j < 0 && !qdone;
+      const bool idle = j < 0 && !qdone && lane_on;
       const uint64_t m = __ballot(idle);
       if (m) {
         // wave-aggregated fetch: the idle lanes take consecutive queue positions
@@ -2376,7 +2381,15 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
   const int nqueue = a0.njobs + a0.nrep;
-  const int nb = blocks < (nqueue + 255) / 256 ? blocks : (nqueue + 255) / 256;
+  // a queue shorter than the grid's lanes is spread over its waves (lanes per wave = ceil(queue / waves))
+  int lpw = 64;
+  if (a0.lanes_per_wave <= 0) {
+    const int waves = 4 * blocks;
+    lpw = (nqueue + waves - 1) / waves;
+    lpw = lpw < 1 ? 1 : (lpw > 64 ? 64 : lpw);
+  }
+  a.lanes_per_wave = lpw;
+  const int nb = blocks < (nqueue + 4 * lpw - 1) / (4 * lpw) ? blocks : (nqueue + 4 * lpw - 1) / (4 * lpw);
   if (a.njobs > 0 && a.perm && a.pflag) {  // queue order: the likely-long jobs first
     hipLaunchKernelGGL(k_roll_flag, dim3((a.njobs + 255) / 256), dim3(256), 0, st, a);
     LAUNCH_CHECK();
