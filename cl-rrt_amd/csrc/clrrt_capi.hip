@@ -123,6 +123,7 @@ struct clrrt_ctx {
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
   int roll_coop = 1;          // option "roll_coop": wave-cooperative collision checks in k_roll_run
   int roll_spread = 1;        // option "roll_spread": a short queue is spread over the persistent waves
+  int nn_exact_fused = 1;     // option "nn_exact_fused": EXACT lists of small trees by k_nn_exact_fused
   int exact_min_width = 8;    // option "exact_min_width": EXACT rounds speculate at least this many samples
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
@@ -1160,6 +1161,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_coop") c->roll_coop = value != 0;
   else if (k == "roll_spread") c->roll_spread = value != 0;
+  else if (k == "nn_exact_fused") c->nn_exact_fused = value != 0;
   else if (k == "rows_deferred") {
     int rc = flush_replays(c);
     if (rc != CLRRT_OK) return rc;
@@ -1435,6 +1437,11 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   c->nn_bf_keys += (int64_t)n * c->n_nodes;
   c->nn_samples += n;
   int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)n * NN_K));
+  if (scratch && c->nn_exact_fused && c->n_nodes <= nn_exact_small_max()) {  // EXACT rounds on small trees
+    HIPC(c, launch_nn_exact_small(st, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, c->cand, c->ckey, c->ncand,
+                                  c->ctie));
+    return CLRRT_OK;
+  }
   const NnSetup su = nn_setup(c);
   if (walk_serves(c, su)) {
     int rc = ensure_walk(c);

@@ -210,6 +210,11 @@ hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, co
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                 int* ncand);
 hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a);
+// EXACT-mode lists of a tree of at most nn_exact_small_max() nodes, one wave per sample (k_nn_exact_fused:
+// keys, list, tie flag and the std::sort replay of tied samples in one kernel)
+hipError_t launch_nn_exact_small(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                 const DevParams& p, int* cand, float* ckey, int* ncand, int* ctie);
+int nn_exact_small_max();
 // Round rollouts (and the pending replays a.rep[0..nrep)) as the persistent k_roll_run, behind k_roll_flag +
 // k_roll_order when a.perm / a.pflag are set (see clrrt_kernels.hip); best B ints, qnext one int.
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, int* qnext, int* best, int blocks);

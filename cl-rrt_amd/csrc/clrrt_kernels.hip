@@ -378,9 +378,15 @@ __global__ void k_nn_exact(const clrrt_sample* __restrict__ S, int B, const NnRe
 // with L_k >= R_k, L_k if L_k < R_{k-1} (else the left scan stops at the swapped R_{k-1}).  The wave
 // finds the stops 64 positions at a time from both ends, pairs them, and swaps the pairs (disjoint) once
 // the crossing is known.  pairs: LDS scratch of n / 2 + 64 int2.
-__device__ __forceinline__ void wave_std_sort(KeyId* a, int n, int2* pairs) {
+// need: only positions [0, need) of the result are read.  libstdc++ recurses on the right part
+// [cut, last) and loops on the left one; a right part that starts at or past `need` is left unsorted:
+// its elements are >= every element before `cut`, and neither its recursion nor the final insertion
+// sort (an element moves left only past strictly greater ones) changes a position before `cut`, so
+// positions [0, need) come out as in the full sort.
+__device__ __forceinline__ void wave_std_sort(KeyId* a, int n, int2* pairs, int need = INT_MAX) {
   const int lane = threadIdx.x & 63;
   if (n <= 1) return;
+  int lim = n;  // positions [0, lim) are sorted as std::sort sorts them
   struct Rg { int lo, hi, depth; };
   Rg stack[64];
   int sp = 0;
@@ -468,7 +474,8 @@ __device__ __forceinline__ void wave_std_sort(KeyId* a, int n, int2* pairs) {
         a[pr.y] = t;
       }
       __syncthreads();
-      stack[sp++] = Rg{cut, hi, depth};
+      if (cut < need) stack[sp++] = Rg{cut, hi, depth};
+      else lim = min(lim, cut);
       hi = cut;
     }
     if (sp == 0) break;
@@ -481,7 +488,7 @@ __device__ __forceinline__ void wave_std_sort(KeyId* a, int n, int2* pairs) {
   if (lane == 0) {
     if (n > 16) {
       insertion_sort_(a, a + 16);
-      for (KeyId* i = a + 16; i != a + n; ++i) unguarded_linear_insert_(i);
+      for (KeyId* i = a + 16; i < a + lim; ++i) unguarded_linear_insert_(i);
     } else {
       insertion_sort_(a, a + n);
     }
@@ -534,6 +541,119 @@ __global__ void __launch_bounds__(64) k_nn_exact_lds(const clrrt_sample* __restr
   }
   for (int j = cnt + lane; j < CAND_K; j += 64) cand[s * CAND_K + j] = -1;
   if (lane == 0) ncand[s] = cnt;
+}
+
+// EXACT-mode lists of a tree that fits in LDS, one wave per sample, in one kernel: every node's key (and
+// feasibleNode, kept in the id's top bit) into LDS; the first NN_K feasible entries in (key, id) order
+// (per-lane top lists merged across the wave) give the list as the brute force gives it, with its tie
+// flag; a tied sample replays std::sort on the LDS array (only the positions up to the last key <= the
+// list's `sort_limit`-th key are needed) and walks the sorted order for the first `sort_limit` feasible
+// entries (rrtplanner.cpp:227-268), exactly as k_nn_exact_lds does after the brute force.
+__global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __restrict__ S, int B,
+                                                       const NnRec* __restrict__ nodes, int N, DevParams p,
+                                                       int* __restrict__ cand, float* __restrict__ ckey,
+                                                       int* __restrict__ ncand, int* __restrict__ ctie) {
+  extern __shared__ KeyId s_kv[];
+  int2* s_pairs = (int2*)(s_kv + N);  // [N / 2 + 64]
+  const int s = blockIdx.x;
+  if (s >= B) return;
+  const int lane = threadIdx.x;
+  const double sx = S[s].x, sy = S[s].y;
+  const int ex = S[s].explore;
+  float tk[NN_K];
+  int ti[NN_K];
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) { tk[j] = __builtin_inff(); ti[j] = 0x7fffffff; }
+  for (int n = lane; n < N; n += 64) {
+    const NnRec& rec = nodes[n];
+    float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
+    if (!ex) k = rec.costE + k;
+    const bool f = feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len);
+    s_kv[n].id = f ? n : (int)((uint32_t)n | 0x80000000u);
+    s_kv[n].key = k;
+    if (f && lex_less(k, n, tk[NN_K - 1], ti[NN_K - 1])) topk_insert(tk, ti, k, n);
+  }
+  // wave merge of the lanes' sorted lists: NN_K times the (key, id)-smallest head
+  float keys[NN_K];
+  int ids[NN_K];
+  int h = 0;
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) {
+    float hk = __builtin_inff();
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < NN_K; q++)
+      if (q == h) { hk = tk[q]; hi = ti[q]; }
+    float bk = hk;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ok = __shfl_xor(bk, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (lex_less(ok, oi, bk, bi)) { bk = ok; bi = oi; }
+    }
+    keys[j] = bk;
+    ids[j] = bi;
+    if (bi != 0x7fffffff && hi == bi) h++;  // the owner's head moves on (ids are unique)
+  }
+  int valid = 0;
+#pragma unroll
+  for (int j = 0; j < NN_K; j++) valid += ids[j] != 0x7fffffff;
+  const int sel = min(p.sort_limit, valid);
+  int tie = 0;
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++) tie |= (j < sel && j + 1 < valid && keys[j] == keys[j + 1]);
+  if (!tie) {  // the (key, id) order is std::sort's on these entries
+    if (lane < CAND_K) {
+      float kk = 0.f;
+      int ii = -1;
+#pragma unroll
+      for (int j = 0; j < CAND_K; j++)
+        if (j == lane) { kk = keys[j]; ii = j < sel ? ids[j] : -1; }
+      cand[s * CAND_K + lane] = ii;
+      ckey[s * CAND_K + lane] = kk;
+    }
+    if (lane == 0) { ncand[s] = sel; ctie[s] = 0; }
+    return;
+  }
+  // positions needed: every entry with key <= the sort_limit-th feasible key (all when fewer are feasible)
+  int need = N;
+  if (sel == p.sort_limit) {
+    const float K = keys[sel - 1];
+    int c = 0, nan = 0;
+    for (int n = lane; n < N; n += 64) {
+      const float k = s_kv[n].key;
+      c += !(K < k);
+      nan |= k != k;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      c += __shfl_xor(c, o, 64);
+      nan |= __shfl_xor(nan, o, 64);
+    }
+    need = nan ? N : c;  // (a NaN key has no place in the order: the whole replay)
+  }
+  __syncthreads();
+  wave_std_sort(s_kv, N, s_pairs, need);
+  int cnt = 0;
+  for (int i0 = 0; i0 < N && cnt < p.sort_limit; i0 += 64) {
+    const int i = i0 + lane;
+    bool f = false;
+    KeyId e{0, 0.f};
+    if (i < N) {
+      e = s_kv[i];
+      f = e.id >= 0;
+    }
+    const uint64_t m = __ballot(f);
+    const int rank = cnt + __popcll(m & ((1ull << lane) - 1));
+    if (f && rank < p.sort_limit) {
+      cand[s * CAND_K + rank] = e.id;
+      ckey[s * CAND_K + rank] = e.key;
+    }
+    cnt = min(p.sort_limit, cnt + __popcll(m));
+  }
+  for (int j = cnt + lane; j < CAND_K; j += 64) cand[s * CAND_K + j] = -1;
+  if (lane == 0) { ncand[s] = cnt; ctie[s] = 1; }
 }
 
 // EXACT-mode tie replay for the samples with ctie set: in LDS when the tree fits, else one lane per
@@ -2260,6 +2380,21 @@ hipError_t launch_nn(hipStream_t st, const clrrt_sample* S, int B, const NnRec* 
   if (exact_scratch) return launch_nn_exact_any(st, S, B, nodes, N, p, ctie, exact_scratch, cand, ckey, ncand);
   return hipSuccess;
 }
+
+hipError_t launch_nn_exact_small(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
+                                 const DevParams& p, int* cand, float* ckey, int* ncand, int* ctie) {
+  if (N > NN_EXACT_LDS_MAX || B <= 0) return hipErrorInvalidValue;
+  const size_t lds = sizeof(KeyId) * (size_t)N + sizeof(int2) * (size_t)(N / 2 + 64);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)&k_nn_exact_fused, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_nn_exact_fused, dim3(B), dim3(64), lds, st, S, B, nodes, N, p, cand, ckey, ncand, ctie);
+  return hipGetLastError();
+}
+
+int nn_exact_small_max() { return NN_EXACT_LDS_MAX; }
 
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,

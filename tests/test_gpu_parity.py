@@ -39,7 +39,10 @@ def _nn_strategy(pl, name):
     """Select the nearest-node search: 'brute' (node order) or 'walk' (one wave per sample over
     place-ordered tiles, clrrt_nnwalk.hip; the default from 8192 nodes).  'walk_split*':
     the walk with a budget of one tile, so every sample hands its search to the split waves and the
-    merge (the overflow path of large trees), 7 waves per sample (odd interleave)."""
+    merge (the overflow path of large trees), 7 waves per sample (odd interleave).  'fused': EXACT lists of
+    small trees by one kernel per round (k_nn_exact_fused, the default); every other strategy turns it off
+    so that its own path runs."""
+    pl.set_option("nn_exact_fused", name == "fused")
     pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
     pl.set_option("nn_walk_stateless", name.endswith("stateless"))
     split = name.startswith("walk_split")
@@ -97,6 +100,7 @@ def test_rollout_parity(kind):
 
 
 @pytest.mark.parametrize("kind,strategy", [("empty", "brute"), ("obb200", "brute"), ("empty", "walk"), ("obb200", "walk"), ("moving", "walk"),
+                                           ("empty", "fused"), ("obb200", "fused"), ("moving", "fused"),
                                            ("obb200", "walk_stateless"), ("obb200", "walk_split"),
                                            ("moving", "walk_split"), ("obb200", "walk_split_stateless")])
 def test_nearest_node_parity(kind, strategy):
@@ -138,7 +142,9 @@ def _compare_trees(o, pl, label):
                                                       ("moving", 4, 250, "brute"), ("empty", 1, 200, "walk"),
                                                       ("obb200", 3, 300, "walk"), ("moving", 4, 250, "walk"),
                                                       ("obb200", 5, 300, "walk_stateless"),
-                                                      ("obb200", 3, 300, "walk_split")])
+                                                      ("obb200", 3, 300, "walk_split"),
+                                                      ("empty", 1, 200, "fused"), ("obb200", 3, 300, "fused"),
+                                                      ("obb200", 5, 300, "fused"), ("moving", 4, 250, "fused")])
 def test_exact_mode_tree_parity(kind, seed, iters, strategy):
     """EXACT mode reproduces the reference's sequential tree (the survey's golden configurations)."""
     mode, obs = _scene(kind)

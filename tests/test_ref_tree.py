@@ -168,9 +168,10 @@ def _planner(coll=0, goal=(40.0, 0.0, 0.0, 0.0), max_nodes=1 << 15, max_batch=51
     return clrrt.Planner(T.params(coll, goal), device=0, max_nodes=max_nodes, max_rows=1 << 20, max_batch=max_batch)
 
 
-STRATEGIES = {"default": {}, "brute": {"nn_walk_min": 1 << 40}, "walk": {"nn_walk_min": 0},
-              "walk_stateless": {"nn_walk_min": 0, "nn_walk_stateless": 1},
-              "walk_split": {"nn_walk_min": 0, "nn_walk_budget_tiles": 1, "nn_walk_budget_keys": 1}}
+STRATEGIES = {"default": {}, "brute": {"nn_exact_fused": 0, "nn_walk_min": 1 << 40},
+              "walk": {"nn_exact_fused": 0, "nn_walk_min": 0},
+              "walk_stateless": {"nn_exact_fused": 0, "nn_walk_min": 0, "nn_walk_stateless": 1},
+              "walk_split": {"nn_exact_fused": 0, "nn_walk_min": 0, "nn_walk_budget_tiles": 1, "nn_walk_budget_keys": 1}}
 
 
 @pytest.mark.gpu
