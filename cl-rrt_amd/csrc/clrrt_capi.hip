@@ -123,6 +123,7 @@ struct clrrt_ctx {
   int roll_priority = 1;      // option "roll_priority": likely-long rollouts first (k_roll_order)
   int roll_coop = 1;          // option "roll_coop": wave-cooperative collision checks in k_roll_run
   int roll_spread = 1;        // option "roll_spread": a short queue is spread over the persistent waves
+  int roll_lanes = 0;         // option "roll_lanes": lanes per wave that take jobs (0: 64, or fewer by roll_spread)
   int nn_exact_fused = 1;     // option "nn_exact_fused": EXACT lists of small trees by k_nn_exact_fused
   int exact_min_width = 8;    // option "exact_min_width": EXACT rounds speculate at least this many samples
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
@@ -1161,6 +1162,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "roll_priority") c->roll_priority = value != 0;
   else if (k == "roll_coop") c->roll_coop = value != 0;
   else if (k == "roll_spread") c->roll_spread = value != 0;
+  else if (k == "roll_lanes") c->roll_lanes = (int)std::max<int64_t>(0, std::min<int64_t>(64, value));
   else if (k == "nn_exact_fused") c->nn_exact_fused = value != 0;
   else if (k == "rows_deferred") {
     int rc = flush_replays(c);
@@ -1521,7 +1523,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
                        : c->cu_split > 0  ? std::max(1, (c->cu_split * c->n_cu) / 8)
                                           : std::max(1, (eighths * c->n_cu) / 8);
     a.coop_enable = c->roll_coop;
-    a.lanes_per_wave = c->roll_spread ? 0 : 64;
+    a.lanes_per_wave = c->roll_lanes > 0 ? c->roll_lanes : c->roll_spread ? 0 : 64;
     if (c->roll_priority) {
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;

@@ -2517,7 +2517,7 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
     return e;
   const int nqueue = a0.njobs + a0.nrep;
   // a queue shorter than the grid's lanes is spread over its waves (lanes per wave = ceil(queue / waves))
-  int lpw = 64;
+  int lpw = a0.lanes_per_wave > 0 && a0.lanes_per_wave < 64 ? a0.lanes_per_wave : 64;
   if (a0.lanes_per_wave <= 0) {
     const int waves = 4 * blocks;
     lpw = (nqueue + waves - 1) / waves;
