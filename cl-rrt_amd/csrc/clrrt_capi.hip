@@ -431,7 +431,8 @@ static void free_all(clrrt_ctx* c) {
                   c->cmp.tmp, c->d_samples2, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->d_samples3, c->cand3, c->ckey3,
                   c->ncand3, c->ctie3, c->nnw3.keys, c->nnw3.keys2, c->nnw3.vals, c->nnw3.vals2, c->nnw3.tmp, c->nnw3.P,
                   c->nnw3.Q, c->nnw3.CE, c->nnw3.ID, c->nnw3.tiles, c->nnw3.supers, c->nnw3.sorder, c->nnw3.HEAD,
-                  c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids};
+                  c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids,
+                  c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
@@ -1271,6 +1272,7 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.CE, Mp));
   HIPC(c, dalloc(&w.ID, Mp));
   HIPC(c, dalloc(&w.HEAD, Mp));
+  HIPC(c, dalloc(&w.trun, walk_tile_count(c->cap.max_nodes) + 1));
   // one record per tile / super-tile of the padded index (launch_nn_walk_build)
   HIPC(c, dalloc(&w.tiles, walk_tile_count(c->cap.max_nodes) + 1));
   HIPC(c, dalloc(&w.supers, walk_super_count(c->cap.max_nodes) + 1));
@@ -2226,7 +2228,7 @@ int clrrt_simulate(clrrt_ctx* c, const clrrt_sim_case* cases, int32_t n, clrrt_r
 }
 
 int clrrt_selftest_math(clrrt_ctx* c, int32_t fn, const double* a, const double* b, int32_t n, double* out) {
-  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 23) return CLRRT_EINVAL;
+  if (!c || n < 0 || (n > 0 && (!a || !b || !out)) || fn < 0 || fn > 28) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   if (n == 0) return CLRRT_OK;
   double *da = nullptr, *db = nullptr, *dout = nullptr;

@@ -388,6 +388,90 @@ CLRRT_HD inline void sin_cos_fma_sel(double x, double& sx, double& cx) {
   }
 }
 
+// The rollout step's trigonometry -- sincos(x2) (generic build), sin(x2) and cos(x2) (FMA build), tan(x3) --
+// as one branch-free block, so the five independent evaluation chains (two reductions, four table-driven
+// do_sin/do_cos, tan's polynomial or xfg row) interleave instead of running one basic block after another.
+// Every branch of the functions above becomes a select between values computed on both sides (the side
+// not taken reads valid table rows: the reduced arguments stay below pi/4, tan's row index is clamped), so
+// the results are theirs bit for bit.  Returns false (nothing written) outside the block's domain:
+// |x2| >= 105414350, |x3| > tan_g3 or non-finite arguments; the caller then takes the branched functions.
+namespace bf {
+CLRRT_HD inline double do_sin_fma(double x, double dx) {
+  const double t = taylor_sin(x, dx), tab = do_sin_tab(x, dx);
+  return fabs(x) < taylor_lim ? t : tab;
+}
+CLRRT_HD inline double do_sin_nofma(double x, double dx) {
+  const double t = nofma::taylor_sin(x, dx);
+  const double ddx = x <= 0 ? -dx : dx;
+  const double u = big + fabs(x);
+  const int k = lo_word(u) << 2;
+  const double xr = fabs(x) - (u - big);
+  const double xx = xr * xr;
+  const double s = xr + (ddx + xr * xx * (sn3 + xx * sn5));
+  const double c = xr * ddx + xx * (cs2 + xx * (cs4 + xx * cs6));
+  const double* T = sincostab();
+  const double sn = T[k], ssn = T[k + 1], cs = T[k + 2], ccs = T[k + 3];
+  const double cor = (ssn + s * ccs - sn * c) + cs * s;
+  const double tab = copysign_(sn + cor, x);
+  return fabs(x) < taylor_lim ? t : tab;
+}
+CLRRT_HD inline double tan_core(double x) {
+  const double w = (x < 0.0) ? -x : x;
+  const double x2 = x * x;
+  double t = fma_(x2, d11, d9);
+  t = fma_(x2, t, d7);
+  t = fma_(x2, t, d5);
+  t = fma_(x2, t, d3);
+  const double poly = fma_(x * x2, t, x);
+  int i = (int)fma_(w, two8, mfftnhf);
+  i = i < 0 ? 0 : i;  // (rows below the table serve only the unselected side)
+  const double* row = xfg() + 4 * i;
+  const double z = w - row[0];
+  const double z2 = z * z;
+  const double pz = fma_(z * z2, fma_(z2, e1, e0), z);
+  const double fi = row[1], gi = row[2];
+  const double y = ((fi + gi) * pz) / (gi - pz) + fi;
+  const double tab = (x >= 0.0 ? 1.0 : -1.0) * y;
+  return w <= tan_g1 ? x : (w <= tan_g2 ? poly : tab);
+}
+}  // namespace bf
+
+CLRRT_HD inline bool step_trig(double x2, double x3, double& s2, double& c2, double& swp, double& cwp, double& t3) {
+  const uint32_t k = hi_word(x2) & 0x7fffffffu;
+  if (!(k < 0x419921fbu) || !(fabs(x3) <= tan_g3)) return false;
+  const bool cA = k < 0x3feb6000u, cB = !cA && k < 0x400368fdu;
+  const double y = hp0 - fabs(x2);
+  const double aB = y + hp1, daB = (y - aB) + hp1;
+  // sincos (generic build): one do_sin and one do_cos on the case's arguments
+  double aCn, daCn;
+  const int nn = nofma::reduce_sincos(x2, aCn, daCn);
+  const double an = cA ? x2 : (cB ? aB : aCn), dan = cA ? 0.0 : (cB ? daB : daCn);
+  // sin, cos (FMA build): cos's case B is do_sin(aB, daB), sin's is do_cos(y, hp1)
+  double aCf, daCf;
+  const int nf = reduce_sincos(x2, aCf, daCf);
+  const double as = cA ? x2 : (cB ? aB : aCf), das = cA ? 0.0 : (cB ? daB : daCf);
+  const double ac = cA ? x2 : (cB ? y : aCf), dac = cA ? 0.0 : (cB ? hp1 : daCf);
+  const double rsn = bf::do_sin_nofma(an, dan), rcn = nofma::do_cos(an, dan);
+  const double rsf = bf::do_sin_fma(as, das), rcf = do_cos(ac, dac);
+  const double tn = bf::tan_core(x3);
+  // sincos_sel's selection
+  {
+    const double s0 = (nn & 1) ? rcn : rsn, c0 = ((nn + 1) & 1) ? rcn : rsn;
+    const double sC = (nn & 2) ? -s0 : s0, cC = ((nn + 1) & 2) ? -c0 : c0;
+    s2 = k < 0x3e400000u ? x2 : (cA ? rsn : (cB ? copysign_(rcn, x2) : sC));
+    c2 = k < 0x3e400000u ? 1.0 : (cA ? rcn : (cB ? rsn : cC));
+  }
+  // sin_cos_fma_sel's selection
+  {
+    const double s0 = (nf & 1) ? rcf : rsf, c0 = ((nf + 1) & 1) ? rcf : rsf;
+    const double sC = (nf & 2) ? -s0 : s0, cC = ((nf + 1) & 2) ? -c0 : c0;
+    swp = k < 0x3e500000u ? x2 : (cA ? rsf : (cB ? copysign_(rcf, x2) : sC));
+    cwp = k < 0x3e400000u ? 1.0 : (cA ? rcf : (cB ? rsf : cC));
+  }
+  t3 = tn;
+  return true;
+}
+
 // ------------------------------------------------------------------------------- float sincosf
 // glibc 2.35 sincosf (sysdeps/ieee754/flt-32/s_sincosf.c + sincosf.h; the FMA variant libm's ifunc
 // selects on FMA+AVX2 hosts): the float argument is widened to double, reduced by a Cody-Waite step

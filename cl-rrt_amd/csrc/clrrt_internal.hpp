@@ -160,6 +160,7 @@ struct WalkBufs {
   float* CE;               // costE
   int* ID;                 // node id (-1: padding)
   int* HEAD;               // first record of the run of records with equal Dubins-key inputs
+  int2* trun;              // per tile: (run head, smallest id) of a tile inside one run, else (-1, -1)
   WalkTile *tiles, *supers;
   // overflow of the walk: a sample whose walk passes the budget (tiles visited / exact keys) hands
   // its search to nch waves over interleaved super-tile subsets with the list's 11th entry as the

@@ -846,9 +846,11 @@ __device__ __forceinline__ double roll_step_pre(Roll& r, const DevParams& p, dou
   // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
   const double d2 = ode_euler(r, p, dc, ac);
   if (pc) pc->mark(2);
-  glibc::sincos_sel(r.x2, r.s2, r.c2);
-  r.t3 = glibc::tan(r.x3);
-  glibc::sin_cos_fma_sel(r.x2, r.swp, r.cwp);  // independent of sincos / tan: their latencies overlap
+  if (!glibc::step_trig(r.x2, r.x3, r.s2, r.c2, r.swp, r.cwp, r.t3)) {  // one branch-free block (in domain)
+    glibc::sincos_sel(r.x2, r.s2, r.c2);
+    r.t3 = glibc::tan(r.x3);
+    glibc::sin_cos_fma_sel(r.x2, r.swp, r.cwp);
+  }
   if (pc) pc->mark(3);
   col7 = (double)r.wp;
   col8 = vref;
@@ -2160,6 +2162,15 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 15: r = round(x); break;
     case 16: { double sx, cx; glibc::sincos(x, sx, cx); r = sx; } break;
     case 17: { double sx, cx; glibc::sincos(x, sx, cx); r = cx; } break;
+    case 24: case 25: case 26: case 27: case 28: {  // glibc::step_trig (x2 = x, x3 = y): s2, c2, swp, cwp, t3
+      double v[5];
+      if (!glibc::step_trig(x, y, v[0], v[1], v[2], v[3], v[4])) {
+        glibc::sincos_sel(x, v[0], v[1]);
+        glibc::sin_cos_fma_sel(x, v[2], v[3]);
+        v[4] = glibc::tan(y);
+      }
+      r = v[fn - 24];
+    } break;
     case 20: { double sx, cx; glibc::sincos_sel(x, sx, cx); r = sx; } break;
     case 21: { double sx, cx; glibc::sincos_sel(x, sx, cx); r = cx; } break;
     case 22: { double sx, cx; glibc::sin_cos_fma_sel(x, sx, cx); r = sx; } break;

@@ -116,6 +116,23 @@ __global__ void k_walk_skeys(const clrrt_sample* __restrict__ S, int B, double x
   vals[i] = i;
 }
 
+// Per tile: (run head, smallest id) when all 32 records lie in one run of equal key inputs (HEAD is the
+// run's first record: equal at the tile's ends), else (-1, -1).
+__global__ void k_walk_trun(const int* __restrict__ HEAD, const int* __restrict__ ID, int ntiles,
+                            int2* __restrict__ trun) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const int j0 = t * WALK_TILE;
+  const int h = HEAD[j0];
+  if (HEAD[j0 + WALK_TILE - 1] != h) {
+    trun[t] = make_int2(-1, -1);
+    return;
+  }
+  int m = 0x7fffffff;
+  for (int q = 0; q < WALK_TILE; q++) m = min(m, ID[j0 + q]);
+  trun[t] = m >= 0 ? make_int2(h, m) : make_int2(-1, -1);
+}
+
 // Place-ordered float records (relative to the frame origin); entries N .. Npad are padding (id -1).
 __global__ void k_walk_gather(const NnRec* __restrict__ nodes, int N, int Npad, const int* __restrict__ order,
                               double ox, double oy, float4* __restrict__ P, float4* __restrict__ Q,
@@ -437,6 +454,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
                                                     const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                     const float4* __restrict__ Q, const float* __restrict__ CE,
                                                     const int* __restrict__ ID, const int* __restrict__ HEAD,
+                                                    const int2* __restrict__ trun,
                                                     const WalkTile* __restrict__ tiles, int ntiles,
                                                     const WalkTile* __restrict__ sup, int nsup, DevParams p,
                                                     NnFrame fr, int* __restrict__ cand, float* __restrict__ ckey,
@@ -734,6 +752,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
     return v;
   };
+  // A tile whose 32 records all belong to the run whose key is known (kc, run head hc), none of them with
+  // an id below the tile's smallest, holds no pair that precedes the 11th entry: (kc, min id) >= (kth,
+  // idk) stays so as the list only improves.  (The root's zero-length children form runs of 10^4-10^5
+  // identical records on large trees; optimize samples' lists fill with their smallest ids.)
+  auto run_out = [&](int tl) -> bool {
+    const int2 tr = trun[tl];
+    return tr.x >= 0 && tr.x == hc && !w_less(kc, tr.y, kth, idk);
+  };
   // visit the tiles of super-tiles sa (lanes 0-31) and sb (lanes 32-63, -1: none) whose bounds lie in
   // (Tp, min(T, kth)] (STATE: not visited yet and <= min(T, kth)); the super-tiles' LDS bounds become
   // those of their tiles beyond T
@@ -759,6 +785,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
 #else
         lb = walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR);
 #endif
+        if (run_out(tl)) lb = __builtin_inff();
       }
       const bool take = st >= 0 && lb <= T && !(lb > kth);
       const bool drop = st >= 0 && lb > kth;  // never needed again (kth only decreases)
@@ -785,6 +812,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
 #else
       if (st >= 0 && tl < ntiles) lb = fmaxf(walk_lb(tiles[tl], rsx, rsy, ex, flen_t, dsR), slb);  // both bound
 #endif
+      if (st >= 0 && tl < ntiles && run_out(tl)) lb = __builtin_inff();
       const bool take = st >= 0 && (first || lb > Tp) && lb <= T && !(lb > kth);
       tm = __ballot(take);
       const float rest = hmin(st >= 0 && lb > T ? lb : __builtin_inff());
@@ -1108,6 +1136,8 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
     hipLaunchKernelGGL(k_wscan_fix, dim3(nt), dim3(256), 0, st, w.HEAD, Npad, tmax);
     LAUNCH_CHECK3();
   }
+  hipLaunchKernelGGL(k_walk_trun, dim3((ntiles + 255) / 256), dim3(256), 0, st, w.HEAD, w.ID, ntiles, w.trun);
+  LAUNCH_CHECK3();
   hipLaunchKernelGGL(k_walk_tiles, dim3((ntiles + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
                      fr.delta, nodes, fr.ox, fr.oy, w.tiles);
   LAUNCH_CHECK3();
@@ -1152,11 +1182,11 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   const int bt = split ? w.bud_tiles : 0, be = split ? w.bud_ex : 0;
   if (state)
     hipLaunchKernelGGL((k_walk_search<true, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q,
-                       w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder,
+                       w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder,
                        stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   else
     hipLaunchKernelGGL((k_walk_search<false, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P,
-                       w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,
+                       w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,
                        w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
   LAUNCH_CHECK3();
   if (split) {
@@ -1169,7 +1199,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
       if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL((k_walk_search<true, true>), dim3(w.max_over * w.nch), dim3(64), 2 * sizeof(float) * (size_t)nl,
-                       st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
+                       st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
                        ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
                        nl);
     LAUNCH_CHECK3();

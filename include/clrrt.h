@@ -337,7 +337,8 @@ int clrrt_nn_batch(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32
  * 6 exp, 7 a/b, 8 cosf, 9 sinf (glibc sincosf restatement), 10 atan2f, 11 acosf, 12 asinf (glibc
  * restatements), 13 sqrtf, 14 float a/b, 15 round,
  * 16 sin and 17 cos of glibc's generic sincos, 20/21 the same through the rollout step's case-selected
- * form, 22 sin and 23 cos through the case-selected pair of FMA-build calls
+ * form, 22 sin and 23 cos through the case-selected pair of FMA-build calls, 24..28 the rollout step's
+ * branch-free trig block with x2 = a, x3 = b: sincos sin / cos, FMA-build sin / cos of a, tan of b
  * (float functions take (float)a, (float)b and return the float widened to double). */
 int clrrt_selftest_math(clrrt_ctx* ctx, int32_t fn, const double* a, const double* b, int32_t n, double* out);
 /* Test hook: the hot-path units exactly as the kernels evaluate them, n cases (tests/test_ref_units.py

@@ -51,16 +51,20 @@ HOST = {
     # the rollout step's case-selected forms (glibc::sincos_sel, glibc::sin_cos_fma_sel)
     20: lambda a, b: _sincos(a, 0), 21: lambda a, b: _sincos(a, 1),
     22: lambda a, b: math.sin(a), 23: lambda a, b: math.cos(a),
+    # the rollout step's branch-free block (glibc::step_trig: x2 = a, x3 = b)
+    24: lambda a, b: _sincos(a, 0), 25: lambda a, b: _sincos(a, 1), 26: lambda a, b: math.sin(a),
+    27: lambda a, b: math.cos(a), 28: lambda a, b: math.tan(b),
 }
 NAMES = ["sin", "cos", "tan", "sqrt", "fmod", "atan2", "exp", "div", "cosf", "sinf", "atan2f", "acosf",
          "asinf", "sqrtf", "fdiv", "round", "sincos.sin", "sincos.cos", None, None, "sincos_sel.sin",
-         "sincos_sel.cos", "sin_cos_fma_sel.sin", "sin_cos_fma_sel.cos"]
-FNS = [f for f in range(24) if f not in (18, 19)]  # 18, 19: latency diagnostics
-EXACT = {0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 20, 21, 22, 23}
+         "sincos_sel.cos", "sin_cos_fma_sel.sin", "sin_cos_fma_sel.cos", "step_trig.s2", "step_trig.c2",
+         "step_trig.swp", "step_trig.cwp", "step_trig.t3"]
+FNS = [f for f in range(29) if f not in (18, 19)]  # 18, 19: latency diagnostics
+EXACT = {0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 20, 21, 22, 23, 24, 25, 26, 27, 28}
 
 
 def _inputs(fn, n, rng):
-    if fn in (0, 1, 8, 9, 16, 17, 20, 21, 22, 23):
+    if fn in (0, 1, 8, 9, 16, 17, 20, 21, 22, 23, 24, 25, 26, 27, 28):
         a = rng.uniform(-7, 7, n)
         a[: n // 8] = rng.uniform(-1e-8, 1e-8, n // 8)  # the tiny-argument cases
         a[n // 8: n // 4] = rng.uniform(-3e4, 3e4, n // 8)
@@ -77,6 +81,11 @@ def _inputs(fn, n, rng):
     else:
         a = rng.uniform(-60, 60, n)
     b = rng.uniform(-60, 60, n)
+    if fn >= 24:  # x3: steering angles (|x3| <= 0.52), tiny ones, tan's polynomial range, up to its table's end
+        b = rng.uniform(-0.6, 0.6, n)
+        b[: n // 8] = rng.uniform(-1e-9, 1e-9, n // 8)
+        b[n // 8: n // 4] = rng.uniform(-0.07, 0.07, n // 8)
+        b[n // 4: n // 4 + n // 16] = rng.uniform(-0.787, 0.787, n // 16)
     if fn == 4:
         b = np.full(n, 2 * math.pi)
     return a, b
