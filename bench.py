@@ -303,6 +303,7 @@ def main():
             goals += cdist.goal_sum(cat)
             if t_max >= horizon:
                 break
+        pl.rows_flush()  # the last round's accepted rows (part of the query's tree, so inside its time)
         return nodes, int(goals.item()), cap_stop
 
     def query(seed):

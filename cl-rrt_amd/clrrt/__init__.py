@@ -56,6 +56,7 @@ _SIGS = {
     "clrrt_expand": (C.c_int, [C.c_void_p, P(abi.Rng), C.c_int64, C.c_double, C.c_int32, C.c_int32, P(abi.Stats)]),
     "clrrt_round_eval": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, C.c_void_p, P(C.c_int32)]),
     "clrrt_round_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "clrrt_rows_flush": (C.c_int, [C.c_void_p]),
     "clrrt_round_prefetch": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32]),
     "clrrt_simulate": (C.c_int, [C.c_void_p, P(abi.SimCase), C.c_int32, P(abi.RolloutResult), P(C.c_double),
                                  C.c_int32, P(C.c_double), C.c_int32]),
@@ -325,6 +326,10 @@ class Planner:
     def round_commit(self, dev_nodes_ptr, n, local_first=0, local_count=0):
         self._chk(self.L.clrrt_round_commit(self.h, C.c_void_p(dev_nodes_ptr), n, local_first, local_count),
                   "round_commit")
+
+    def rows_flush(self):
+        """Write the deferred trajectory rows of the last commit (clrrt_rows_flush)."""
+        self._chk(self.L.clrrt_rows_flush(self.h), "rows_flush")
 
     def simulate_batch(self, jobs, rows=False):
         """jobs: list of (parent, gb, sx, sy).  Returns a list of result dicts (+ rows)."""

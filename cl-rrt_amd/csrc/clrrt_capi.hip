@@ -1725,6 +1725,12 @@ int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t l
   return CLRRT_OK;
 }
 
+int clrrt_rows_flush(clrrt_ctx* c) {
+  if (!c) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  return flush_replays(c);
+}
+
 int clrrt_round_prefetch(clrrt_ctx* c, const clrrt_sample* next, int32_t n) {
   if (!c || n < 0 || (n > 0 && !next)) return CLRRT_EINVAL;
   if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");

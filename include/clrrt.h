@@ -286,9 +286,10 @@ int clrrt_round_eval(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, voi
                      int32_t* n_out);
 /* Append `n` node records (device pointer) to the tree in their order.  `local_first`/`local_count`
  * name the slice of them that this context produced in its last clrrt_round_eval (informational:
- * clrrt_round_eval already wrote those records' rows into this context's arena, at the row_offset
- * the records carry); records outside the slice are remote nodes whose rows stay on their owner
- * (`owner`; clrrt_path_commit + a gather of the path's rows complete a committed path). */
+ * clrrt_round_eval reserved those records' rows in this context's arena, at the row_offset the
+ * records carry, and the rows are written by the next rollout launch or clrrt_rows_flush); records
+ * outside the slice are remote nodes whose rows stay on their owner (`owner`; clrrt_path_commit + a
+ * gather of the path's rows complete a committed path). */
 int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t local_first,
                        int32_t local_count);
 /* Engine extension (no reference counterpart): declares the samples of the NEXT clrrt_round_eval.
@@ -297,6 +298,12 @@ int clrrt_round_commit(clrrt_ctx* ctx, const void* dev_nodes, int32_t n, int32_t
  * clrrt_round_eval called with exactly these samples skips its search.  Results are identical to
  * calls without it; any other tree change discards the prefetch. */
 int clrrt_round_prefetch(clrrt_ctx* ctx, const clrrt_sample* next_samples, int32_t n);
+/* Engine extension (no reference counterpart): trajectory rows are deferred -- the rollouts a commit
+ * accepts are replayed into the arena by the next rollout launch (option "rows_deferred").  This
+ * writes the pending ones now (stream-ordered).  clrrt_expand does it before returning, and every call
+ * that reads rows (clrrt_tree_rows, clrrt_path_commit) or changes what they depend on
+ * (clrrt_set_obstacles, clrrt_set_params) does it first; a round-API caller ends a query with it. */
+int clrrt_rows_flush(clrrt_ctx* ctx);
 
 /* checkObsDistance(const vector<double>& x) (rrt/include/rrt/collision.h:41, the documented collision
  * hook README.md:40-47): out[i] = the distance the context's collision mode gives for states[i] (10
