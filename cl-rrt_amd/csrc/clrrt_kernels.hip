@@ -893,20 +893,22 @@ __device__ __forceinline__ int roll_step(Roll& r, const DevParams& p, const ObsV
 }
 
 // Wave-cooperative checkObsDistance without the gap value (k_roll_run; OBB collision with the static
-// grid): the same value and box-test count as obs_distance<false> for every lane with act set, but
-// the SAT tests of all lanes run spread over the wave.  Each lane culls its own candidates (its grid
-// cell's static obstacles, then the moving ones) and queues the survivors (lane, obstacle) in LDS; the
-// queued pairs are then tested 64 at a time, one per lane, each against its owner's vehicle box, and
-// every overlap lowers the owner's first-overlap index.  The result only depends on whether some
-// survivor overlaps (Dobs = 0; checkObsDistance returns at its first overlap, old_collisioncheck.cpp:
-// 24-51) and, for the work counter, on the smallest overlapping index (the lists ascend, so that is the
-// reference's first overlap).  A lane outside the grid's float frame takes obs_distance itself.
-// Called by every lane of the wave (wave-uniform control flow).
+// grid): the same value and box-test count as obs_distance<false> for every lane with act set, with the
+// work of all lanes spread over the wave.  The candidate pairs (lane, obstacle) of the active lanes -- each
+// lane's grid-cell list of static obstacles, then the moving ones -- are numbered by a wave prefix sum and
+// taken 64 at a time, one pair per lane: the lane culls its pair against the owner's vehicle circle and,
+// if it survives, SAT-tests it against the owner's vehicle box (built only by owners with a survivor);
+// an overlap lowers the owner's first-overlap index.  A lone rollout's ~10-30 candidates are thus culled
+// and tested in one pass instead of one after another.  The result only depends on whether some candidate
+// overlaps (Dobs = 0; checkObsDistance returns at its first overlap, old_collisioncheck.cpp:24-51) and,
+// for the work counter, on the smallest overlapping index (the lists ascend, so that is the reference's
+// first overlap).  A lane outside the grid's float frame takes obs_distance itself.  Called by every lane
+// of the wave (wave-uniform control flow).
 struct CoopLds {
   Box4* veh;      // [64] vehicle boxes
   double* t;      // [64] prediction time of each lane's step
   int* hit;       // [64] smallest overlapping obstacle index (INT_MAX: none)
-  uint32_t* q;    // [cap] queued pairs: lane << 16 | moving << 15 | obstacle
+  uint32_t* q;    // [cap] scratch: owner records (below)
   int cap;
 };
 #define COOP_QCAP 512
@@ -915,9 +917,16 @@ constexpr size_t kCoopLdsPerWave = 64 * sizeof(Box4) + 64 * sizeof(double) + 64 
 __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p, const ObsView& ov, uint32_t& tests,
                                     const CoopLds& cl) {
   const int lane = threadIdx.x & 63;
+  // owner records in the scratch: (fvx, fvy, ft, first item) | pair-range start | static count | window
+  // start owners | survivor flags
+  float4* s_pos = (float4*)cl.q;            // [64]
+  int* s_pre = (int*)(cl.q + 256);          // [64]
+  int* s_nst = (int*)(cl.q + 320);          // [64]
+  int* s_own = (int*)(cl.q + 384);          // [64]
+  int* s_need = (int*)(cl.q + 448);         // [64]
   double t = 0.0, vpx = 0.0, vpy = 0.0;
   float fvx = 0.f, fvy = 0.f, ft = 0.f;
-  bool use = false;  // this lane's check goes through the queue
+  bool use = false;  // this lane's check goes through the pairs
   int a = 0, ae = 0;
   if (act) {
     t = p.obs_use_pred ? r.x6 : 0.0;
@@ -934,54 +943,68 @@ __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p,
       }
     }
   }
+  const int nst = ae - a;
+  const int len = use ? nst + ov.nmov : 0;
+  // exclusive prefix sum of the pair counts over the wave
+  int inc = len;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  const int pre = inc - len;
+  const int total = __shfl(inc, 63, 64);
   cl.hit[lane] = 0x7fffffff;
   cl.t[lane] = t;
-  bool veh_done = false, need_veh = false;
-  int nq = 0;  // wave-uniform
-  auto flush = [&]() {
-    if (need_veh && !veh_done) {  // setVertices of the lanes with a queued survivor
-      Box4 vb;
-      veh_box(vpx, vpy, r.x2, vb);
-      cl.veh[lane] = vb;
-      veh_done = true;
-    }
+  s_pos[lane] = make_float4(fvx, fvy, ft, __int_as_float(a));
+  s_pre[lane] = pre;
+  s_nst[lane] = nst;
+  s_need[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  int carry = -1;  // owner of the window's first pair when its range began in an earlier window
+  for (int t0 = 0; t0 < total; t0 += 64) {
+    // the owners whose range starts inside this window, at their first position
+    const bool starts = len > 0 && pre >= t0 && pre < t0 + 64;
+    if (starts) s_own[pre - t0] = lane;
+    unsigned long long sm = starts ? (1ull << (pre - t0)) : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sm |= (unsigned long long)__shfl_xor((long long)sm, o, 64);
     __builtin_amdgcn_wave_barrier();
-    for (int i0 = 0; i0 < nq; i0 += 64) {
-      const int i = i0 + lane;
-      if (i < nq) {
-        const uint32_t e = cl.q[i];
-        const int owner = (int)(e >> 16), jj = (int)(e & 0x7fffu);
+    const int pidx = t0 + lane;
+    const bool valid = pidx < total;
+    const unsigned long long below = sm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const int owner = below ? s_own[63 - __clzll(below)] : carry;
+    int jj = 0;
+    bool mv = false, surv = false;
+    float4 op = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) {
+      op = s_pos[owner];
+      const int idx = pidx - s_pre[owner];
+      const int no = s_nst[owner];
+      mv = idx >= no;
+      jj = mv ? (int)ov.gmov[idx - no] : (int)ov.gitems[__float_as_int(op.w) + idx];
+      surv = !obs_culled(ov, jj, op.z, op.x, op.y);
+    }
+    // the window's last pair's owner continues into the next window
+    carry = __shfl(owner, 63, 64);
+    if (__ballot(surv)) {
+      if (surv && s_need[owner] != 2) s_need[owner] = 1;
+      __builtin_amdgcn_wave_barrier();
+      if (s_need[lane] == 1) {  // setVertices of the lanes with a survivor (once per step)
+        Box4 vb;
+        veh_box(vpx, vpy, r.x2, vb);
+        cl.veh[lane] = vb;
+        s_need[lane] = 2;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (surv) {
         const Box4 vb = cl.veh[owner];
-        const float gap = (e & 0x8000u) ? obs_sat(vb, ov, jj, cl.t[owner]) : obs_sat_static(vb, ov, jj);
+        const float gap = mv ? obs_sat(vb, ov, jj, cl.t[owner]) : obs_sat_static(vb, ov, jj);
         if (gap == 0) atomicMin(&cl.hit[owner], jj);
       }
     }
     __builtin_amdgcn_wave_barrier();
-    nq = 0;
-  };
-  auto push = [&](bool surv, int jj, uint32_t mv) {
-    const uint64_t m = __ballot(surv);
-    const int c = __popcll(m);
-    if (c == 0) return;
-    if (nq + c > cl.cap) flush();
-    if (surv) {
-      cl.q[nq + __popcll(m & ((1ull << lane) - 1))] = ((uint32_t)lane << 16) | mv | (uint32_t)jj;
-      need_veh = true;
-    }
-    nq += c;
-  };
-  __builtin_amdgcn_wave_barrier();
-  for (int k = 0;; k++) {  // static candidates: the lane's grid cell list
-    const bool has = use && a + k < ae;
-    if (__ballot(has) == 0) break;
-    const int jj = has ? (int)ov.gitems[a + k] : 0;
-    push(has && !obs_culled(ov, jj, ft, fvx, fvy), jj, 0u);
   }
-  for (int k = 0; k < ov.nmov; k++) {  // moving candidates (every lane)
-    const int jj = (int)ov.gmov[k];
-    push(use && !obs_culled(ov, jj, ft, fvx, fvy), jj, 0x8000u);
-  }
-  flush();
   double D = 10000;
   if (use) {
     const int h = cl.hit[lane];
