@@ -103,8 +103,9 @@ struct clrrt_ctx {
   int64_t nnw_min_nodes = 8192;       // walk search (clrrt_nnwalk.hip) from this tree size ("nn_walk_min")
   bool nnw_stateless = false;          // "nn_walk_stateless": the large-tree variant at every size (tests)
   // walk overflow ("nn_walk_budget_tiles", "nn_walk_budget_keys", 0 = off; "nn_walk_chunks" <= 64;
-  // "nn_walk_max_over" records <= 2048); defaults from the cfg3 bench sweep
-  int nnw_bud_tiles = 2048, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
+  // "nn_walk_max_over" records <= 2048); defaults from the cfg3 bench sweeps (round 3
+  // with lag 2: 3072 tiles 1.039 vs 2048 1.031 M nodes/s, 8192 keys 1.008, 12 chunks 1.030)
+  int nnw_bud_tiles = 3072, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
   // pipelined rounds: a second index set, so the next round's index is built while the side stream's
@@ -161,12 +162,12 @@ struct clrrt_ctx {
   float* ckey2 = nullptr;
   int* ncand2 = nullptr;
   int* ctie2 = nullptr;
-  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (2: expand_lag2;
-  // default 1: on cfg3 lag 2 measured 0.931 vs 0.951 M nodes/s -- the rollouts, not the search, bound the
-  // round, and a second search in flight slows them).
+  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (2: expand_lag2).
+  // Default 2 since the round-3 rollout kernel (shorter launches, flattened collision checks): cfg3 A/B
+  // 1.031 vs 1.015 M nodes/s; with round 2's kernel lag 1 was ahead (0.951 vs 0.931).
   // Lag 2 keeps a third list set (*3), a third walk index set and a second side stream (allocated on
   // first use).
-  int nn_lag = 1;
+  int nn_lag = 2;
   clrrt_sample* d_samples3 = nullptr;
   clrrt_sample* h_samples3 = nullptr;
   int* cand3 = nullptr;
