@@ -176,7 +176,15 @@ struct clrrt_ctx {
   int* ctie3 = nullptr;
   WalkBufs nnw3{};
   hipStream_t side2 = nullptr;
+  // lag 2: the appended-node merges run on their own stream (mst), behind the commit and the slot's walk
+  // (events ev_lagw); with option "stream_prio" (default 1) the main and merge streams have the device's
+  // highest priority and the walk streams (side, side2) its lowest, so the commit and merge kernels are
+  // not queued behind thousands of walk waves (kernel trace: k_select 16 us -> 1.9 ms late in a query)
+  hipStream_t mst = nullptr;
+  hipEvent_t ev_lagw[3] = {nullptr, nullptr, nullptr};
+  int stream_prio = 1;
   hipEvent_t ev_lag[3] = {nullptr, nullptr, nullptr};
+  int stream_prio_applied = 0;  // the priority setting the current streams were created with
   // clrrt_round_prefetch: declared next samples; pf_state 1 = their walk was launched (lists in the
   // *2 buffers, merge pending), 2 = merged and swapped in for pf_samples
   std::vector<clrrt_sample> pf_next, pf_samples;
@@ -443,6 +451,10 @@ static void free_all(clrrt_ctx* c) {
   if (c->side2) hipStreamDestroy(c->side2);
   for (auto e : c->ev_lag)
     if (e) hipEventDestroy(e);
+  for (auto e : c->ev_lagw)
+    if (e) hipEventDestroy(e);
+  if (c->mst) hipStreamSynchronize(c->mst);
+  if (c->mst) hipStreamDestroy(c->mst);
   if (c->side) hipStreamSynchronize(c->side);
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
@@ -1193,6 +1205,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
       if (!c->ev_rs1) HIPC(c, hipEventCreateWithFlags(&c->ev_rs1, hipEventDisableTiming));
     }
   }
+  else if (k == "stream_prio") c->stream_prio = value != 0;
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
     HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1757,6 +1770,7 @@ struct LagSlot {
   int* ncand = nullptr;
   int* ctie = nullptr;
   hipEvent_t ev = nullptr;  // recorded after its merge
+  hipEvent_t evw = nullptr; // recorded after its walk (the merge waits for it on the merge stream)
   int n = 0;                // samples searched (0: none)
   int64_t tree_n = 0;       // size of the tree its walk searched
   int stream = 0;           // side stream index
@@ -1772,6 +1786,7 @@ static int lag_alloc(clrrt_ctx* c) {
   HIPC(c, dalloc(&c->ctie3, B));
   HIPC(c, hipHostMalloc((void**)&c->h_samples3, sizeof(clrrt_sample) * B, hipHostMallocDefault));
   for (auto& e : c->ev_lag) HIPC(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : c->ev_lagw) HIPC(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (c->cu_split > 0) {  // the same CUs as the side stream
     const int nw = (c->n_cu + 31) / 32;
     std::vector<uint32_t> ms(nw, 0u);
@@ -1781,12 +1796,37 @@ static int lag_alloc(clrrt_ctx* c) {
   } else {
     HIPC(c, hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking));
   }
+  HIPC(c, hipStreamCreateWithFlags(&c->mst, hipStreamNonBlocking));
+  return CLRRT_OK;
+}
+
+// Stream priorities of the lag-2 rounds (option "stream_prio"): main and merge streams highest, the walk
+// streams lowest (1), or all equal (0).  CU-masked streams (cu_split) keep theirs.  Scheduling only.
+static int apply_stream_prio(clrrt_ctx* c) {
+  const int want = c->stream_prio ? 1 : 2;  // 2: equal priorities
+  if (c->stream_prio_applied == want || c->cu_split > 0) return CLRRT_OK;
+  int lo = 0, hi = 0;
+  HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+  const int p_hi = want == 1 ? hi : 0, p_lo = want == 1 ? lo : 0;
+  HIPC(c, hipDeviceSynchronize());
+  auto remake = [&](hipStream_t& st, int pr) -> int {
+    if (st) HIPC(c, hipStreamDestroy(st));
+    HIPC(c, hipStreamCreateWithPriority(&st, hipStreamNonBlocking, pr));
+    return CLRRT_OK;
+  };
+  int rc;
+  if ((rc = remake(c->side, p_lo)) != CLRRT_OK || (rc = remake(c->side2, p_lo)) != CLRRT_OK ||
+      (rc = remake(c->mst, p_hi)) != CLRRT_OK)
+    return rc;
+  if (c->own_stream && (rc = remake(c->stream, p_hi)) != CLRRT_OK) return rc;
+  c->stream_prio_applied = want;
   return CLRRT_OK;
 }
 
 static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t batch,
                        clrrt_stats* out) {
   int rc = lag_alloc(c);
+  if (rc == CLRRT_OK) rc = apply_stream_prio(c);
   if (rc != CLRRT_OK) return rc;
   clrrt_stats st{};
   const auto t0 = std::chrono::steady_clock::now();
@@ -1801,10 +1841,11 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   // list sets: this round's (c->*), round r+1's (A) and round r+2's (B)
   LagSlot A, B;
   A.d = c->d_samples2; A.h = c->h_samples2; A.cand = c->cand2; A.ckey = c->ckey2; A.ncand = c->ncand2;
-  A.ctie = c->ctie2; A.ev = c->ev_lag[0];
+  A.ctie = c->ctie2; A.ev = c->ev_lag[0]; A.evw = c->ev_lagw[0];
   B.d = c->d_samples3; B.h = c->h_samples3; B.cand = c->cand3; B.ckey = c->ckey3; B.ncand = c->ncand3;
-  B.ctie = c->ctie3; B.ev = c->ev_lag[1];
+  B.ctie = c->ctie3; B.ev = c->ev_lag[1]; B.evw = c->ev_lagw[1];
   hipEvent_t cur_ev = c->ev_lag[2];  // the event of the set this round's lists are in
+  hipEvent_t cur_evw = c->ev_lagw[2];
   bool have_cur = false;             // this round's lists come from slot A of the previous round
   int cur_stream = 0;
   double last_round_ms = 0;
@@ -1843,6 +1884,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       HIPC(c, launch_nn_walk_search(s, sl.d, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1, su.y1,
                                     *W[k], sl.cand, sl.ckey, sl.ncand, sl.ctie, c->work_ctr + 18, c->nnw_stateless));
     }
+    HIPC(c, hipEventRecord(sl.evw, s));
     sl.n = n;
     sl.tree_n = c->n_nodes;
     sl.stream = si;
@@ -1892,6 +1934,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         // the side streams' work is done (a first pipelined round searches nothing ahead yet)
         HIPC(c, hipStreamSynchronize(c->side));
         HIPC(c, hipStreamSynchronize(c->side2));
+        HIPC(c, hipStreamSynchronize(c->mst));
         if ((rc = build(wk, su)) != CLRRT_OK) break;
         c->nn_bf_keys += (int64_t)nb * c->n_nodes;
         c->nn_samples += nb;
@@ -1928,9 +1971,10 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
     // slot A: merge the nodes appended since its walk's tree
     if (A.n > 0) {
-      hipStream_t s = sides[A.stream];
+      hipStream_t s = c->mst;  // behind the commit and slot A's walk
       HIPC(c, hipEventRecord(c->ev_commit, c->stream));
       HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
+      HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
       const int64_t first = A.tree_n, cnt = c->n_nodes - A.tree_n;
       if (cnt > 0) {
         KTimer kt(c, 0, s);
@@ -1960,10 +2004,11 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     {
       LagSlot old;
       old.d = c->d_samples; old.h = c->h_samples; old.cand = c->cand; old.ckey = c->ckey; old.ncand = c->ncand;
-      old.ctie = c->ctie; old.ev = cur_ev; old.stream = cur_stream;
+      old.ctie = c->ctie; old.ev = cur_ev; old.evw = cur_evw; old.stream = cur_stream;
       have_cur = A.n > 0;
       c->d_samples = A.d; c->h_samples = A.h; c->cand = A.cand; c->ckey = A.ckey; c->ncand = A.ncand; c->ctie = A.ctie;
       cur_ev = A.ev;
+      cur_evw = A.evw;
       cur_stream = A.stream;
       A = B;
       B = old;
@@ -1976,6 +2021,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   if (rc == CLRRT_OK) rc = flush_replays(c);
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->side2));
+  HIPC(c, hipStreamSynchronize(c->mst));
   HIPC(c, hipStreamSynchronize(c->stream));
   // the buffers the context's other paths use keep their roles: (d_samples, cand, ...) and the *2 set
   // are whichever two of the three sets, *3 the third
@@ -1983,6 +2029,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     c->d_samples2 = A.d; c->h_samples2 = A.h; c->cand2 = A.cand; c->ckey2 = A.ckey; c->ncand2 = A.ncand; c->ctie2 = A.ctie;
     c->d_samples3 = B.d; c->h_samples3 = B.h; c->cand3 = B.cand; c->ckey3 = B.ckey; c->ncand3 = B.ncand; c->ctie3 = B.ctie;
     c->ev_lag[0] = A.ev; c->ev_lag[1] = B.ev; c->ev_lag[2] = cur_ev;
+    c->ev_lagw[0] = A.evw; c->ev_lagw[1] = B.evw; c->ev_lagw[2] = cur_evw;
     c->nnw_built.n = -1;
     c->nnw.sorted_n = -1;
     c->nnw_alt.sorted_n = -1;
