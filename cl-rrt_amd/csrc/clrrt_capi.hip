@@ -162,12 +162,13 @@ struct clrrt_ctx {
   float* ckey2 = nullptr;
   int* ncand2 = nullptr;
   int* ctie2 = nullptr;
-  // option "nn_lag" (1 or 2): how many rounds ahead the pipelined BATCH rounds search (2: expand_lag2).
-  // Default 2 since the round-3 rollout kernel (shorter launches, flattened collision checks): cfg3 A/B
-  // 1.031 vs 1.015 M nodes/s; with round 2's kernel lag 1 was ahead (0.951 vs 0.931).
+  // option "nn_lag" (1 or 2; 0 = by query length): how many rounds ahead the pipelined BATCH rounds search
+  // (2: expand_lag2).  The default picks 2 for long queries (a budget of >= 1 s or >= 64 rounds), 1 for
+  // short ones: round-3 A/B, cfg3 (2 s) 1.031 vs 1.015 M nodes/s for lag 2; cfg2 (200 ms) 0.551 vs 0.565 M
+  // for lag 1; cfg5 (200 ms) equal.  (With round 2's rollout kernel lag 1 was ahead on cfg3 too.)
   // Lag 2 keeps a third list set (*3), a third walk index set and a second side stream (allocated on
   // first use).
-  int nn_lag = 2;
+  int nn_lag = 0;
   clrrt_sample* d_samples3 = nullptr;
   clrrt_sample* h_samples3 = nullptr;
   int* cand3 = nullptr;
@@ -183,6 +184,7 @@ struct clrrt_ctx {
   hipStream_t mst = nullptr;
   hipEvent_t ev_lagw[3] = {nullptr, nullptr, nullptr};
   int stream_prio = 1;
+  int walk_cu_reserve = 0;  // option "walk_cu_reserve" k = 1..7: lag-2 walk streams kept off k/8 of the CUs
   hipEvent_t ev_lag[3] = {nullptr, nullptr, nullptr};
   int stream_prio_applied = 0;  // the priority setting the current streams were created with
   // clrrt_round_prefetch: declared next samples; pf_state 1 = their walk was launched (lists in the
@@ -1169,7 +1171,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
-  else if (k == "nn_lag" && (value == 1 || value == 2)) c->nn_lag = (int)value;
+  else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
@@ -1206,6 +1208,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     }
   }
   else if (k == "stream_prio") c->stream_prio = value != 0;
+  else if (k == "walk_cu_reserve" && value >= 0 && value <= 7) c->walk_cu_reserve = (int)value;
   else if (k == "side_priority") {  // -1: lower than the main stream's, 0: equal, 1: higher
     int lo = 0, hi = 0;
     HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1803,7 +1806,7 @@ static int lag_alloc(clrrt_ctx* c) {
 // Stream priorities of the lag-2 rounds (option "stream_prio"): main and merge streams highest, the walk
 // streams lowest (1), or all equal (0).  CU-masked streams (cu_split) keep theirs.  Scheduling only.
 static int apply_stream_prio(clrrt_ctx* c) {
-  const int want = c->stream_prio ? 1 : 2;  // 2: equal priorities
+  const int want = (c->stream_prio ? 1 : 2) + 4 * c->walk_cu_reserve;  // 2: equal priorities
   if (c->stream_prio_applied == want || c->cu_split > 0) return CLRRT_OK;
   int lo = 0, hi = 0;
   HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1815,9 +1818,20 @@ static int apply_stream_prio(clrrt_ctx* c) {
     return CLRRT_OK;
   };
   int rc;
-  if ((rc = remake(c->side, p_lo)) != CLRRT_OK || (rc = remake(c->side2, p_lo)) != CLRRT_OK ||
-      (rc = remake(c->mst, p_hi)) != CLRRT_OK)
+  if (c->walk_cu_reserve > 0) {  // the walk streams on the CUs with (cu % 8) >= k (no priority on CU-masked streams)
+    const int nw = (c->n_cu + 31) / 32;
+    std::vector<uint32_t> ms(nw, 0u);
+    for (int i = 0; i < c->n_cu; i++)
+      if ((i % 8) >= c->walk_cu_reserve) ms[i / 32] |= 1u << (i % 32);
+    for (hipStream_t* st : {&c->side, &c->side2}) {
+      if (*st) HIPC(c, hipStreamDestroy(*st));
+      HIPC(c, hipExtStreamCreateWithCUMask(st, (uint32_t)nw, ms.data()));
+    }
+    if ((rc = remake(c->mst, p_hi)) != CLRRT_OK) return rc;
+  } else if ((rc = remake(c->side, p_lo)) != CLRRT_OK || (rc = remake(c->side2, p_lo)) != CLRRT_OK ||
+             (rc = remake(c->mst, p_hi)) != CLRRT_OK) {
     return rc;
+  }
   if (c->own_stream && (rc = remake(c->stream, p_hi)) != CLRRT_OK) return rc;
   c->stream_prio_applied = want;
   return CLRRT_OK;
@@ -2050,7 +2064,9 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
   HIPC(c, hipSetDevice(c->device));
   batch = std::max(1, std::min<int32_t>(batch > 0 ? batch : c->cap.max_batch, c->cap.max_batch));
-  if (mode == CLRRT_MODE_BATCH && c->nn_pipeline && c->nn_lag == 2) return expand_lag2(c, rng, n_iters, budget_ms, batch, out);
+  const int lag = c->nn_lag ? c->nn_lag
+                  : (n_iters == 0 ? budget_ms >= 1000.0 : n_iters >= 64 * (int64_t)batch) ? 2 : 1;
+  if (mode == CLRRT_MODE_BATCH && c->nn_pipeline && lag == 2) return expand_lag2(c, rng, n_iters, budget_ms, batch, out);
   clrrt_stats st{};
   auto t0 = std::chrono::steady_clock::now();
   clrrt_rng work = *rng;       // draws ahead (speculative samples)

@@ -312,7 +312,8 @@ def test_walk_matches_brute_force_large_tree():
 
 @pytest.mark.gpu
 def test_pipelined_batch_rounds_identical():
-    """Full-size property: BATCH rounds with the walk search of the round after next (nn_lag 2, the default, or of the
+    """Full-size property: BATCH rounds with the walk search of the round after next (nn_lag 2, the default for
+    long queries, with or without its stream priorities, or of the
     next round: nn_lag 1) overlapped with the current
     round's rollouts (+ the merge of the appended nodes, launch_nn_delta) grow exactly the tree of
     plain rounds (every node record and trajectory row).  So do the scheduling and search options: the
@@ -323,7 +324,8 @@ def test_pipelined_batch_rounds_identical():
     replayed for the accepted ones only (the default: each replay must run exactly its node's row count)."""
     mode, obs = _scene("obb200")
     trees = []
-    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=1), dict(roll_priority=0, roll_blocks=512),
+    variants = [dict(nn_pipeline=0), dict(nn_pipeline=1), dict(nn_lag=1), dict(nn_lag=2),
+                dict(nn_lag=2, stream_prio=0), dict(roll_priority=0, roll_blocks=512),
                 dict(roll_coop=0), dict(rows_deferred=0),
                 dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
                 dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
