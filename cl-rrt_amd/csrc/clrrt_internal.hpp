@@ -222,7 +222,7 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, i
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t replay_bytes();
 // deferred rows: the committed rollouts' start states (jobs/recs from launch_compact, prep and res of the
-// round's k_roll_prep / k_roll_run) into out[0..n) for the next persistent launch's replays
+// round's lists / k_roll_run results) into out[0..n) for the next persistent launch's replays
 hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const clrrt_node* tree,
                                 const int* cand, const clrrt_sample* S, const RollRes* res, void* out);
 hipError_t launch_select(hipStream_t st, const SelArgs& a);

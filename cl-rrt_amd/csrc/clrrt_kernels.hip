@@ -1274,15 +1274,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
 // The candidate rollouts of a round differ wildly in length (a collision can end one after a few
 // steps, an end-of-reference one runs hundreds), so one lane per job leaves most lanes of a wave idle
 // behind its longest rollout.  Instead:
-//   k_roll_prep : one lane per job j = (sample s, candidate k) builds the Simulation state
-//                 (getReference + Simulation ctor: make_ref, roll_init) and writes row 0;
-//   k_roll_run  : persistent waves; idle lanes take the next jobs from a queue in candidate-major
+//   k_roll_run  : persistent waves; idle lanes take the next jobs (j = (sample s, candidate k)) from a
+//                 queue whose first positions replay the previous commit's accepted rollouts, then the
+//                 round's jobs in candidate-major
 //                 order (all first candidates, then all second ones, ...), so when candidate k of
 //                 sample s is taken the earlier ones have usually finished: a job whose sample
 //                 already has a successful earlier candidate is skipped (or abandoned while
 //                 running) -- expandTree never looks past the first success (:150-160), so the
 //                 round's result is unchanged.  A successful regular rollout that passes the
-//                 goal-bias gate continues in the same lane with the goal-biased rollout.
+//                 goal-bias gate continues in the same lane with the goal-biased rollout.  Every start
+//                 (getReference / getGoalReference + the Simulation ctor) is built in the kernel at one
+//                 code site (until round 3 a k_roll_prep kernel materialised it per job).
+
 // What a rollout starts from (getReference / getGoalReference + the Simulation ctor): the parent state,
 // the parent's ref.back() and ref.v.back(), the sample (regular rollouts) and the goal-bias flag.
 struct RollSrc {
@@ -2511,7 +2514,7 @@ static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   return hipSuccess;
 }
 
-// The queue order from k_roll_prep's flags: perm = flagged positions, then the others (both ascending).
+// The queue order from k_roll_flag's flags: perm = flagged positions, then the others (both ascending).
 // a.pflag's buffer holds [njobs flags][njobs exclusive-scan positions][scan scratch].
 size_t roll_order_scratch_bytes(int n) {
   size_t bytes = 0;
