@@ -187,6 +187,7 @@ struct clrrt_ctx {
   int walk_cu_reserve = 0;  // option "walk_cu_reserve" k = 1..7: lag-2 walk streams kept off k/8 of the CUs
   hipEvent_t ev_lag[3] = {nullptr, nullptr, nullptr};
   int stream_prio_applied = 0;  // the priority setting the current streams were created with
+  bool side_prio_set = false;   // option "side_priority" made the side stream (apply_stream_prio keeps it)
   // clrrt_round_prefetch: declared next samples; pf_state 1 = their walk was launched (lists in the
   // *2 buffers, merge pending), 2 = merged and swapped in for pf_samples
   std::vector<clrrt_sample> pf_next, pf_samples;
@@ -1194,6 +1195,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     if (c->roll_st) HIPC(c, hipStreamDestroy(c->roll_st));
     c->roll_st = nullptr;
     c->cu_split = (int)value;
+    c->stream_prio_applied = 0;  // the lag-2 streams are re-made for the new split
     if (value == 0) {
       HIPC(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     } else {
@@ -1216,6 +1218,8 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     HIPC(c, hipStreamDestroy(c->side));
     const int pr = value > 0 ? hi : value < 0 ? lo : 0;
     HIPC(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, pr));
+    c->side_prio_set = true;
+    c->stream_prio_applied = 0;
     if (value < 0 && c->own_stream) {  // and the main stream gets the highest priority
       HIPC(c, hipStreamSynchronize(c->stream));
       HIPC(c, hipStreamDestroy(c->stream));
@@ -1642,6 +1646,17 @@ static int ensure_slots(clrrt_ctx* c) {
   return CLRRT_OK;
 }
 
+// Every replay must run exactly as many steps as its committed node has rows (k_roll_run counts the
+// ones that do not in work counter 61 and stores no row past the node's count).  Nonzero means the
+// arena's rows are not the committed rollouts': reported as an error instead of a silently wrong tree.
+static int replay_check(clrrt_ctx* c) {
+  HIPC(c, hipMemcpyAsync(c->h_int + 2, (const char*)(c->work_ctr + 61), sizeof(int), hipMemcpyDeviceToHost,
+                         c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->h_int[2] != 0) return fail(c, CLRRT_EHIP, "a deferred-row replay diverged from its committed rollout");
+  return CLRRT_OK;
+}
+
 // Run the pending replays (the last commit's accepted rollouts, deferred rows) on their own: before
 // anything reads the arena, changes what a replay depends on (parameters, obstacles), or at the end of
 // an expansion.  Same kernel, no jobs of a round.
@@ -1658,7 +1673,7 @@ static int flush_replays(clrrt_ctx* c) {
   a.lanes_per_wave = c->roll_spread ? 0 : 64;
   HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, c->n_cu));
   c->rep_n = 0;
-  return CLRRT_OK;
+  return replay_check(c);
 }
 
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n) {
@@ -1719,7 +1734,8 @@ int clrrt_round_eval(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, void*
 
 int clrrt_round_commit(clrrt_ctx* c, const void* dev_nodes, int32_t n, int32_t local_first, int32_t local_count) {
   (void)local_first;
-  (void)local_count;  // rows of local records were written to the arena by clrrt_round_eval
+  (void)local_count;  // the local records' rows are only reserved by clrrt_round_eval: the next rollout
+                      // launch (or clrrt_rows_flush) replays them into the arena (deferred rows)
   if (!c || n < 0 || (n > 0 && !dev_nodes)) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
   const int64_t first_new = c->n_nodes;
@@ -1810,7 +1826,8 @@ static int apply_stream_prio(clrrt_ctx* c) {
   if (c->stream_prio_applied == want || c->cu_split > 0) return CLRRT_OK;
   int lo = 0, hi = 0;
   HIPC(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const int p_hi = want == 1 ? hi : 0, p_lo = want == 1 ? lo : 0;
+  // the priorities follow stream_prio alone (the CU reservation only masks the walk streams)
+  const int p_hi = c->stream_prio ? hi : 0, p_lo = c->stream_prio ? lo : 0;
   HIPC(c, hipDeviceSynchronize());
   auto remake = [&](hipStream_t& st, int pr) -> int {
     if (st) HIPC(c, hipStreamDestroy(st));
@@ -1828,9 +1845,9 @@ static int apply_stream_prio(clrrt_ctx* c) {
       HIPC(c, hipExtStreamCreateWithCUMask(st, (uint32_t)nw, ms.data()));
     }
     if ((rc = remake(c->mst, p_hi)) != CLRRT_OK) return rc;
-  } else if ((rc = remake(c->side, p_lo)) != CLRRT_OK || (rc = remake(c->side2, p_lo)) != CLRRT_OK ||
-             (rc = remake(c->mst, p_hi)) != CLRRT_OK) {
-    return rc;
+  } else if ((!c->side_prio_set && (rc = remake(c->side, p_lo)) != CLRRT_OK) ||
+             (rc = remake(c->side2, p_lo)) != CLRRT_OK || (rc = remake(c->mst, p_hi)) != CLRRT_OK) {
+    return rc;  // (an explicit side_priority keeps the side stream it made)
   }
   if (c->own_stream && (rc = remake(c->stream, p_hi)) != CLRRT_OK) return rc;
   c->stream_prio_applied = want;
@@ -1860,6 +1877,22 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   B.ctie = c->ctie3; B.ev = c->ev_lag[1]; B.evw = c->ev_lagw[1];
   hipEvent_t cur_ev = c->ev_lag[2];  // the event of the set this round's lists are in
   hipEvent_t cur_evw = c->ev_lagw[2];
+  // The three list sets rotate every round; whichever way the function is left (an error return of HIPC
+  // included), the buffers the context's other paths use get their roles back: (d_samples, cand, ...) and
+  // the *2 set are whichever two of the three sets, *3 the third, each freed once by free_all.
+  struct RoleGuard {
+    std::function<void()> f;
+    ~RoleGuard() { f(); }
+  } role_guard{[&]() {
+    c->d_samples2 = A.d; c->h_samples2 = A.h; c->cand2 = A.cand; c->ckey2 = A.ckey; c->ncand2 = A.ncand; c->ctie2 = A.ctie;
+    c->d_samples3 = B.d; c->h_samples3 = B.h; c->cand3 = B.cand; c->ckey3 = B.ckey; c->ncand3 = B.ncand; c->ctie3 = B.ctie;
+    c->ev_lag[0] = A.ev; c->ev_lag[1] = B.ev; c->ev_lag[2] = cur_ev;
+    c->ev_lagw[0] = A.evw; c->ev_lagw[1] = B.evw; c->ev_lagw[2] = cur_evw;
+    c->nnw_built.n = -1;
+    c->nnw.sorted_n = -1;
+    c->nnw_alt.sorted_n = -1;
+    c->nnw3.sorted_n = -1;
+  }};
   bool have_cur = false;             // this round's lists come from slot A of the previous round
   int cur_stream = 0;
   double last_round_ms = 0;
@@ -2033,21 +2066,9 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   }
   // the last round's accepted rows (part of the query's output tree, so inside its time)
   if (rc == CLRRT_OK) rc = flush_replays(c);
-  HIPC(c, hipStreamSynchronize(c->side));
-  HIPC(c, hipStreamSynchronize(c->side2));
-  HIPC(c, hipStreamSynchronize(c->mst));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  // the buffers the context's other paths use keep their roles: (d_samples, cand, ...) and the *2 set
-  // are whichever two of the three sets, *3 the third
-  {
-    c->d_samples2 = A.d; c->h_samples2 = A.h; c->cand2 = A.cand; c->ckey2 = A.ckey; c->ncand2 = A.ncand; c->ctie2 = A.ctie;
-    c->d_samples3 = B.d; c->h_samples3 = B.h; c->cand3 = B.cand; c->ckey3 = B.ckey; c->ncand3 = B.ncand; c->ctie3 = B.ctie;
-    c->ev_lag[0] = A.ev; c->ev_lag[1] = B.ev; c->ev_lag[2] = cur_ev;
-    c->ev_lagw[0] = A.evw; c->ev_lagw[1] = B.evw; c->ev_lagw[2] = cur_evw;
-    c->nnw_built.n = -1;
-    c->nnw.sorted_n = -1;
-    c->nnw_alt.sorted_n = -1;
-    c->nnw3.sorted_n = -1;
+  for (hipStream_t s : {c->side, c->side2, c->mst, c->stream}) {  // every stream drained, the first error kept
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess && rc == CLRRT_OK) rc = fail(c, CLRRT_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
   }
   st.nodes_added = c->n_nodes - nodes_before;
   st.elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

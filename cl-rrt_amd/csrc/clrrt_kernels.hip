@@ -1574,7 +1574,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     }
 #endif
     w.steps++;
-    if (rows) store_row(rows + (int64_t)steps * 10, 1, r, c7, c8, c9);
+    // a replay writes no row past its committed node's (a longer one is counted in n_rep_bad below)
+    if (rows && (!rp || steps < nrows_rp)) store_row(rows + (int64_t)steps * 10, 1, r, c7, c8, c9);
     if (pc) pc->mark(5);
     if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {

@@ -149,6 +149,7 @@ class Engine {
   Engine& operator=(const Engine&) = delete;
 
   clrrt_ctx* ctx() { return ctx_; }
+  const clrrt_params& params() const { return p_; }
   void set_params(const clrrt_params& p) {
     check(ctx_, clrrt_set_params(ctx_, &p), "clrrt_set_params");
     p_ = p;
@@ -448,8 +449,13 @@ class Simulation {
       throw Error("Simulation: the reference is not a getReference line");
     const int32_t cap = (int32_t)std::max<size_t>(ref.x.size(), 1);
     clrrt_rollout_result res;
-    std::vector<double> rows(10 * 1100), refo(3 * (size_t)cap);
-    check(eng.ctx(), clrrt_simulate(eng.ctx(), &q, 1, &res, rows.data(), 1100, refo.data(), cap), "clrrt_simulate");
+    /* propagate's loop runs while i < 20/sim_dt (simulation.cpp:58): that many steps + the initial row */
+    int32_t n_steps = 0;
+    while (n_steps < 20 / eng.params().sim_dt) n_steps++;
+    const int32_t rows_cap = n_steps + 1;
+    std::vector<double> rows(10 * (size_t)rows_cap), refo(3 * (size_t)cap);
+    check(eng.ctx(), clrrt_simulate(eng.ctx(), &q, 1, &res, rows.data(), rows_cap, refo.data(), cap),
+          "clrrt_simulate");
     if (res.ref_n != (int32_t)ref.x.size()) throw Error("Simulation: the reference is not the one getGoalReference builds");
     for (int32_t i = 0; i < res.ref_n; i++)
       if (!(refo[i] == ref.x[i]) || !(refo[cap + i] == ref.y[i]))
