@@ -192,6 +192,38 @@ struct clrrt_ctx {
   // *2 buffers, merge pending), 2 = merged and swapped in for pf_samples
   std::vector<clrrt_sample> pf_next, pf_samples;
   int pf_state = 0;
+  // Deferred samples (BATCH option "defer_steps" T > 0; see Carry in clrrt_kernels.hip): every rollout chain
+  // runs at most T more steps per launch; suspended chains resume at the front of the next launch and a
+  // sample commits at the first commit after which nothing its result depends on is still running.  The
+  // per-job results, lists and first-success flags of the rounds in flight live in rings of R round slots
+  // (a chain of at most 2 n_steps_max steps resolves within ceil(2 n_steps_max / T) launches, so a slot is
+  // free again when the ring comes round); the commit buffers hold vcap views (deferred + this round's).
+  struct {
+    int T = 0;                    // option value (0: off)
+    bool active = false;          // the current expansion defers
+    int R = 0;                    // ring slots allocated (for T_alloc / n_steps_alloc)
+    int T_alloc = 0, n_steps_alloc = 0;
+    int64_t vcap = 0;             // views the commit buffers hold
+    RollRes* res = nullptr;       // [R][B][K]
+    RollRes* res_gb = nullptr;    // [R][B][K]
+    int* cand = nullptr;          // [R][B][K]
+    int* ncand = nullptr;         // [R][B]
+    clrrt_sample* samp = nullptr; // [R][B]
+    int* best = nullptr;          // [R][B]
+    int* dlist[2] = {nullptr, nullptr};  // ring indices of the deferred samples (views 0 .. nd)
+    int cur_dl = 0, nd = 0;
+    int nd_eval = -1;             // nd when the current round's views were selected (-1: no views)
+    int* gv = nullptr;            // [vcap]
+    uint8_t* pend = nullptr;      // [vcap]
+    void* sel_tmp = nullptr;
+    size_t sel_bytes = 0;
+    int* d_cnt = nullptr;         // [2] selected views, suspended chains (device)
+    void* carry[2] = {nullptr, nullptr};
+    int cur_c = 0, ncarry = 0, carry_cap = 0;
+    int64_t round = 0;            // rounds of the current expansion
+    int slot = 0;                 // ring slot of the current round
+    int64_t deferred_total = 0;   // samples deferred at least once (statistics)
+  } def;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -213,6 +245,8 @@ struct clrrt_ctx {
 // ------------------------------------------------------------------------------------------ util
 static void pf_reset(clrrt_ctx* c);
 static int flush_replays(clrrt_ctx* c);
+static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n);
+static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped);
 static int ensure_slots(clrrt_ctx* c);
 
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
@@ -446,6 +480,11 @@ static void free_all(clrrt_ctx* c) {
                   c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids,
                   c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun};
   for (void* p : ptrs)
+    if (p) hipFree(p);
+  void* dptrs[] = {c->def.res, c->def.res_gb, c->def.cand, c->def.ncand, c->def.samp, c->def.best, c->def.dlist[0],
+                   c->def.dlist[1], c->def.gv, c->def.pend, c->def.sel_tmp, c->def.d_cnt, c->def.carry[0],
+                   c->def.carry[1]};
+  for (void* p : dptrs)
     if (p) hipFree(p);
   if (c->h_samples) hipHostFree(c->h_samples);
   if (c->h_samples2) hipHostFree(c->h_samples2);
@@ -1187,6 +1226,12 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     c->rows_deferred = value != 0;
   }
   else if (k == "exact_min_width" && value >= 1 && value <= 1 << 20) c->exact_min_width = (int)value;
+  else if (k == "defer_steps" && value >= 0 && value <= 1 << 20) {
+    // BATCH rounds with deferred samples (changes the BATCH tree: samples whose rollouts run past T steps
+    // per launch commit in a later round, by a deterministic rule the oracle restates); 0 = off
+    if (value > 0 && value < 8) return fail(c, CLRRT_EINVAL, "defer_steps must be 0 or >= 8");
+    c->def.T = (int)value;
+  }
   else if (k == "cu_split" && value >= 0 && value <= 7) {
     HIPC(c, hipStreamSynchronize(c->side));
     if (c->roll_st) HIPC(c, hipStreamSynchronize(c->roll_st));
@@ -1522,11 +1567,28 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     if (rc == CLRRT_OK) rc = ensure_slots(c);
     if (rc != CLRRT_OK) return rc;
   }
+  const bool defer = c->def.active && !exact && persistent && deferred;
+  if (defer) {  // this round's lists and samples into its ring slot (k_select / the replays read them there)
+    auto& d = c->def;
+    d.slot = (int)(d.round % d.R);
+    const int64_t B = c->cap.max_batch;
+    HIPC(c, hipMemcpyAsync(d.cand + (int64_t)d.slot * B * CAND_K, c->cand, sizeof(int) * n * CAND_K,
+                           hipMemcpyDeviceToDevice, st));
+    HIPC(c, hipMemcpyAsync(d.ncand + (int64_t)d.slot * B, c->ncand, sizeof(int) * n, hipMemcpyDeviceToDevice, st));
+    HIPC(c, hipMemcpyAsync(d.samp + (int64_t)d.slot * B, c->d_samples, sizeof(clrrt_sample) * n,
+                           hipMemcpyDeviceToDevice, st));
+    if (d.nd + (int64_t)n > d.vcap) return fail(c, CLRRT_ECAPACITY, "deferred samples exceed the commit buffers");
+    if (rst != st) {  // the copies precede the rollouts' ring writes
+      HIPC(c, hipEventRecord(c->ev_rs0, st));
+      HIPC(c, hipStreamWaitEvent(rst, c->ev_rs0, 0));
+    }
+  }
   {
     KTimer kt(c, 1, rst);
     RollArgs a = roll_args(c, n * CAND_K);
     a.res = c->res_spec;
     a.res_gb = c->res_gb;
+    if (defer) defer_roll_args(c, a, true);
     a.slots = deferred ? nullptr : c->slots;
     a.slot_rows = c->slot_rows;
     a.slot_jobs = (int)(c->cap.max_batch * CAND_K);
@@ -1552,7 +1614,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.pflag = c->roll_pflag;
     }
     if (persistent)
-      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, c->roll_best, blocks));
+      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, defer ? c->def.best : c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
     if (deferred) c->rep_n = 0;
@@ -1567,8 +1629,20 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     if (rc != CLRRT_OK) return rc;
   }
   SelArgs s;
+  memset(&s, 0, sizeof(s));
   s.p = c->dp; s.tree = c->tree; s.cand = c->cand; s.ckey = c->ckey; s.ncand = c->ncand; s.res = c->res_spec;
   s.res_gb = c->res_gb; s.regnodes = c->regnodes; s.gbnodes = c->gbnodes; s.so = c->so; s.B = n;
+  if (defer) {  // views: the deferred samples of earlier rounds, then this round's
+    auto& d = c->def;
+    s.cand = d.cand; s.ncand = d.ncand; s.res = d.res; s.res_gb = d.res_gb;
+    s.view = d.dlist[d.cur_dl];
+    s.nd = d.nd;
+    s.sbase = d.slot * (int)c->cap.max_batch;
+    s.gv = d.gv;
+    s.pend = d.pend;
+    s.B = d.nd + n;
+  }
+  c->def.nd_eval = defer ? c->def.nd : -1;
   {
     KTimer kt(c, 2);
     HIPC(c, launch_select(st, s));
@@ -1594,16 +1668,36 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
 // copy the accepted trajectories into the arena.  *n_out = records.
 static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   hipStream_t st = c->stream;
+  auto& d = c->def;
+  const bool defer = d.nd_eval >= 0;  // eval_samples selected views (deferred samples + this round's)
+  const int V = defer ? d.nd_eval + L : L;
   {
     KTimer kt(c, 2);
-    HIPC(c, launch_compact(st, L, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
+    HIPC(c, launch_compact(st, V, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
                            c->out_nodes, c->jobs, c->totals, c->cmp));
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
+    // the views still pending, in view order: the next commit's deferred samples
+    if (defer) HIPC(c, launch_defer_select(st, d.gv, d.pend, V, d.dlist[1 - d.cur_dl], d.d_cnt, d.sel_tmp, d.sel_bytes));
   }
   HIPC(c, hipMemcpyAsync(c->h_totals, c->totals, sizeof(int64_t) * 8, hipMemcpyDeviceToHost, st));
   if (merge_bbox) HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
+  if (defer) {
+    HIPC(c, hipMemcpyAsync(c->h_int, d.d_cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+    HIPC(c, hipMemcpyAsync(c->h_int + 2, (const char*)(c->work_ctr + 62), sizeof(int), hipMemcpyDeviceToHost, st));
+  }
   HIPC(c, hipStreamSynchronize(st));
   if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+  if (defer) {
+    if (c->h_int[2] != 0 || c->h_int[1] > d.carry_cap)
+      return fail(c, CLRRT_ECAPACITY, "suspended rollouts exceed the carry buffer (raise defer_steps)");
+    d.deferred_total += std::max(0, c->h_int[0] - d.nd_eval);  // this round's samples that stay pending
+    d.cur_dl ^= 1;
+    d.nd = c->h_int[0];
+    d.cur_c ^= 1;
+    d.ncarry = c->h_int[1];
+    d.round++;
+    d.nd_eval = -1;
+  }
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
   c->counters.sim_count += c->h_totals[2];
@@ -1618,8 +1712,11 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
       if (rc != CLRRT_OK) return rc;
     }
     KTimer kt(c, 2);
-    HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->tree, c->cand, c->d_samples, c->res_spec,
-                                 c->rep_buf));
+    if (defer)  // the committed samples' lists and results sit in the rings
+      HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->tree, d.cand, d.samp, d.res, c->rep_buf));
+    else
+      HIPC(c, launch_replay_gather(st, c->jobs, c->out_nodes, (int)nn, c->tree, c->cand, c->d_samples, c->res_spec,
+                                   c->rep_buf));
     c->rep_n = (int)nn;
   } else {
     KTimer kt(c, 2);
@@ -1630,6 +1727,87 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   c->last_eval_rows = nr;
   *n_out = (int)nn;
   return CLRRT_OK;
+}
+
+// Deferred samples: the rings for the context's T and n_steps_max, the view-sized commit buffers and the
+// carry buffers (allocated on the first expansion that defers, grown when T shrinks or sim_dt does).
+static int ensure_defer(clrrt_ctx* c) {
+  auto& d = c->def;
+  const int64_t B = c->cap.max_batch;
+  const int n = std::max(1, c->dp.n_steps_max);
+  const int R = (int)((2LL * n + d.T - 1) / d.T) + 2;
+  if (!d.res || d.R < R) {
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (void* p : {(void*)d.res, (void*)d.res_gb, (void*)d.cand, (void*)d.ncand, (void*)d.samp, (void*)d.best})
+      if (p) HIPC(c, hipFree(p));
+    d.res = nullptr; d.res_gb = nullptr; d.cand = nullptr; d.ncand = nullptr; d.samp = nullptr; d.best = nullptr;
+    d.R = 0;
+    HIPC(c, dalloc(&d.res, (size_t)R * B * CAND_K));
+    HIPC(c, dalloc(&d.res_gb, (size_t)R * B * CAND_K));
+    HIPC(c, dalloc(&d.cand, (size_t)R * B * CAND_K));
+    HIPC(c, dalloc(&d.ncand, (size_t)R * B));
+    HIPC(c, dalloc(&d.samp, (size_t)R * B));
+    HIPC(c, dalloc(&d.best, (size_t)R * B));
+    d.R = R;
+  }
+  if (!d.gv) {
+    // every commit path holds up to vcap views: the deferred samples + one round
+    const int64_t V = 2 * B;
+    int rc = flush_replays(c);  // rep_buf is re-made below
+    if (rc != CLRRT_OK) return rc;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (void* p : {(void*)c->regnodes, (void*)c->gbnodes, (void*)c->so, (void*)c->out_nodes, (void*)c->jobs,
+                    c->rep_buf, (void*)c->cmp.packed, (void*)c->cmp.scanned, c->cmp.tmp})
+      if (p) HIPC(c, hipFree(p));
+    c->regnodes = nullptr; c->gbnodes = nullptr; c->so = nullptr; c->out_nodes = nullptr; c->jobs = nullptr;
+    c->rep_buf = nullptr; c->cmp.packed = nullptr; c->cmp.scanned = nullptr; c->cmp.tmp = nullptr;
+    HIPC(c, dalloc(&c->regnodes, V));
+    HIPC(c, dalloc(&c->gbnodes, V));
+    HIPC(c, dalloc(&c->so, V));
+    HIPC(c, dalloc(&c->out_nodes, 2 * V));
+    HIPC(c, dalloc(&c->jobs, 2 * V));
+    HIPC(c, hipMalloc(&c->rep_buf, replay_bytes() * (size_t)2 * V));
+    HIPC(c, dalloc(&c->cmp.packed, V));
+    HIPC(c, dalloc(&c->cmp.scanned, V));
+    c->cmp.tmp_bytes = compact_scan_bytes((int)V);
+    HIPC(c, hipMalloc(&c->cmp.tmp, std::max<size_t>(c->cmp.tmp_bytes, 256)));
+    HIPC(c, dalloc(&d.dlist[0], V));
+    HIPC(c, dalloc(&d.dlist[1], V));
+    HIPC(c, dalloc(&d.gv, V));
+    HIPC(c, dalloc(&d.pend, V));
+    d.sel_bytes = defer_select_bytes((int)V);
+    HIPC(c, hipMalloc(&d.sel_tmp, std::max<size_t>(d.sel_bytes, 256)));
+    HIPC(c, dalloc(&d.d_cnt, 2));
+    d.carry_cap = (int)std::min<int64_t>(B * CAND_K, INT_MAX / 2);
+    HIPC(c, hipMalloc(&d.carry[0], carry_bytes() * (size_t)d.carry_cap));
+    HIPC(c, hipMalloc(&d.carry[1], carry_bytes() * (size_t)d.carry_cap));
+    d.vcap = V;
+  }
+  return CLRRT_OK;
+}
+
+// The start of an expansion: deferral on for BATCH rounds when the option asks for it and the rollouts run
+// persistent with deferred rows (the paths the carry records exist for).
+static int defer_begin(clrrt_ctx* c, bool batch) {
+  auto& d = c->def;
+  d.active = batch && d.T > 0 && c->roll_persistent && c->rows_deferred && c->dp.n_steps_max > 0;
+  d.nd = 0; d.ncarry = 0; d.round = 0; d.slot = 0; d.nd_eval = -1; d.deferred_total = 0;
+  return d.active ? ensure_defer(c) : CLRRT_OK;
+}
+
+// Ring / carry fields of a rollout launch: this round's slot (cap T) or, for the drain (cap 0), no new jobs.
+static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped) {
+  auto& d = c->def;
+  a.res = d.res;
+  a.res_gb = d.res_gb;
+  a.jbase = d.slot * (int)c->cap.max_batch * CAND_K;
+  a.sbase = d.slot * (int)c->cap.max_batch;
+  a.cap = capped ? d.T : 0;
+  a.carry_in = d.carry[d.cur_c];
+  a.ncarry = d.ncarry;
+  a.carry_out = d.carry[1 - d.cur_c];
+  a.ncarry_out = d.d_cnt + 1;
+  a.carry_cap = d.carry_cap;
 }
 
 // Row slots for the paths that store speculative rows (option "rows_deferred" 0, non-persistent rollouts).
@@ -1661,7 +1839,8 @@ static int replay_check(clrrt_ctx* c) {
 // anything reads the arena, changes what a replay depends on (parameters, obstacles), or at the end of
 // an expansion.  Same kernel, no jobs of a round.
 static int flush_replays(clrrt_ctx* c) {
-  if (c->rep_n <= 0) return CLRRT_OK;
+  auto& d = c->def;
+  if (c->rep_n <= 0 && d.ncarry <= 0) return CLRRT_OK;
   HIPC(c, hipSetDevice(c->device));
   KTimer kt(c, 1);
   RollArgs a = roll_args(c, 0);
@@ -1671,9 +1850,55 @@ static int flush_replays(clrrt_ctx* c) {
   a.nrep = c->rep_n;
   a.coop_enable = c->roll_coop;
   a.lanes_per_wave = c->roll_spread ? 0 : 64;
+  if (d.ncarry > 0) {  // suspended replays (or, after an error, chains) of a deferring expansion: run to their end
+    defer_roll_args(c, a, false);
+    d.ncarry = 0;
+  }
   HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, c->n_cu));
   c->rep_n = 0;
   return replay_check(c);
+}
+
+// The end of a deferring expansion: one launch without a cap runs every suspended chain (and replay) to its
+// end, the samples still pending commit in view order (the oldest round first), then their rows replay.
+static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
+  auto& d = c->def;
+  if (!d.active) return CLRRT_OK;
+  if (d.nd > 0 || d.ncarry > 0) {
+    hipStream_t st = c->stream;
+    {
+      KTimer kt(c, 1);
+      RollArgs a = roll_args(c, 0);
+      a.rep = c->rep_buf;
+      a.nrep = c->rep_n;
+      a.coop_enable = c->roll_coop;
+      a.lanes_per_wave = c->roll_spread ? 0 : 64;
+      defer_roll_args(c, a, false);
+      HIPC(c, launch_rollout_persistent(st, a, 0, c->roll_q, d.best, c->n_cu));
+      c->rep_n = 0;
+      d.ncarry = 0;
+    }
+    if (d.nd > 0) {
+      SelArgs s;
+      memset(&s, 0, sizeof(s));
+      s.p = c->dp; s.tree = c->tree; s.cand = d.cand; s.ckey = c->ckey; s.ncand = d.ncand; s.res = d.res;
+      s.res_gb = d.res_gb; s.regnodes = c->regnodes; s.gbnodes = c->gbnodes; s.so = c->so;
+      s.view = d.dlist[d.cur_dl]; s.nd = d.nd; s.sbase = 0; s.gv = d.gv; s.pend = d.pend; s.B = d.nd;
+      {
+        KTimer kt(c, 2);
+        HIPC(c, launch_select(st, s));
+      }
+      d.nd_eval = d.nd;
+      int nn = 0;
+      int rc = compact_and_copy(c, 0, &nn, true);
+      if (rc == CLRRT_OK) rc = append_nodes(c, c->out_nodes, nn);
+      if (rc != CLRRT_OK) return rc;
+      if (goal_nodes) *goal_nodes += c->last_goal_nodes;
+      if (d.nd != 0 || d.ncarry != 0) return fail(c, CLRRT_EHIP, "deferred samples left after the drain");
+    }
+  }
+  d.active = false;
+  return flush_replays(c);
 }
 
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n) {
@@ -1858,6 +2083,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
                        clrrt_stats* out) {
   int rc = lag_alloc(c);
   if (rc == CLRRT_OK) rc = apply_stream_prio(c);
+  if (rc == CLRRT_OK) rc = defer_begin(c, true);
   if (rc != CLRRT_OK) return rc;
   clrrt_stats st{};
   const auto t0 = std::chrono::steady_clock::now();
@@ -1951,8 +2177,9 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     if (n_iters == 0 && !(ms0 < budget_ms)) break;
     const int64_t left = n_iters > 0 ? n_iters - st.iterations : INT64_MAX;
     const int nb = (int)std::min<int64_t>(cur, left);
-    if (c->n_nodes + 2 * (int64_t)nb > c->cap.max_nodes ||
-        c->n_rows + 2 * (int64_t)nb * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+    // (a commit also takes the deferred samples that resolve)
+    const int64_t nc = nb + (int64_t)c->def.nd;
+    if (c->n_nodes + 2 * nc > c->cap.max_nodes || c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;
@@ -2064,8 +2291,12 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     }
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
-  // the last round's accepted rows (part of the query's output tree, so inside its time)
+  // the deferred samples still pending and the last round's accepted rows (part of the query's output
+  // tree, so inside its time)
+  if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
+  st.deferred = c->def.deferred_total;
   if (rc == CLRRT_OK) rc = flush_replays(c);
+  c->def.active = false;
   for (hipStream_t s : {c->side, c->side2, c->mst, c->stream}) {  // every stream drained, the first error kept
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess && rc == CLRRT_OK) rc = fail(c, CLRRT_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
@@ -2096,10 +2327,10 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   const bool exact = mode == CLRRT_MODE_EXACT;
   int cur = exact ? std::min(batch, std::max(16, c->exact_min_width)) : batch;
   int64_t nodes_before = c->n_nodes;
-  int rc = CLRRT_OK;
+  int rc = defer_begin(c, !exact);
   bool have_next = false;  // this round's samples and lists were prepared by the previous round
   double last_round_ms = 0;
-  for (;;) {
+  for (; rc == CLRRT_OK;) {
     const auto tr0 = std::chrono::steady_clock::now();
     if (n_iters > 0 && st.iterations >= n_iters) break;
     if (n_iters == 0) {
@@ -2108,9 +2339,9 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     }
     int nb = cur;
     if (n_iters > 0) nb = (int)std::min<int64_t>(nb, n_iters - st.iterations);
-    // a round appends at most 2 nodes and 2 full-horizon trajectories per sample
-    if (c->n_nodes + 2 * (int64_t)nb > c->cap.max_nodes ||
-        c->n_rows + 2 * (int64_t)nb * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+    // a round appends at most 2 nodes and 2 full-horizon trajectories per sample (+ the deferred samples)
+    const int64_t nc = nb + (int64_t)c->def.nd;
+    if (c->n_nodes + 2 * nc > c->cap.max_nodes || c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;
@@ -2189,8 +2420,12 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if (exact) cur = std::max(c->exact_min_width, std::min(batch, L == nb ? 2 * nb : 2 * L));
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
   }
-  // the last round's accepted rows (part of the query's output tree, so inside its time)
+  // the deferred samples still pending and the last round's accepted rows (part of the query's output
+  // tree, so inside its time)
+  if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
+  st.deferred = c->def.deferred_total;
   if (rc == CLRRT_OK) rc = flush_replays(c);
+  c->def.active = false;
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->stream));
   st.nodes_added = c->n_nodes - nodes_before;

@@ -9,6 +9,9 @@
 
 namespace clrrt {
 
+// RollRes::outcome of a rollout suspended at its chain's cap (deferred samples): not known yet.
+#define CLRRT_ROLL_PENDING (-2)
+
 // Result of one rollout (what Simulation exposes after propagate).
 struct RollRes {
   double st[10];       // stateArray.back()
@@ -50,6 +53,8 @@ struct SampleOut {
   int32_t gb_ok;    // goal-biased node accepted
   int32_t nrows_reg, nrows_gb;
   int32_t rollouts, steps, f_col, f_acc, f_it;
+  int32_t g;        // ring index of the sample (job of candidate k: g K + k)
+  int32_t pend;     // 1: a rollout the result depends on is still suspended (deferred sample)
 };
 
 // Job sources:
@@ -114,20 +119,39 @@ struct RollArgs {
   // k_roll_run lanes per wave that take jobs: <= 0 spreads the queue over the grid's waves (set by
   // launch_rollout_persistent), 64 fills every lane (option "roll_spread" 0)
   int lanes_per_wave;
+  // Deferred samples (BATCH option "defer_steps" = cap > 0, see k_roll_run): a rollout chain (a regular
+  // rollout + its goal-biased follow-up) runs at most `cap` more steps per launch; one that reaches its cap
+  // is suspended into carry_out (count *ncarry_out) and resumed from carry_in[0 .. ncarry) -- the queue's
+  // first positions -- by the next launch.  res / res_gb / best are rings over the rounds in flight: this
+  // launch's job j = s K + k writes res[jbase + j] and its sample's first success best[sbase + s].
+  int cap;
+  const void* carry_in;
+  int ncarry;
+  void* carry_out;
+  int* ncarry_out;
+  int carry_cap;
+  int jbase, sbase;
 };
 
+// k_select over B "views": view v < nd is the still unresolved sample view[v] of an earlier round (deferred
+// samples), view v >= nd is sample v - nd of this round; a sample is addressed by its ring index g (cand,
+// ncand, res, res_gb at g K + k); without deferred samples nd = 0 and sbase = 0 (the round's own arrays).
 struct SelArgs {
   DevParams p;
   const clrrt_node* __restrict__ tree;
   const int* __restrict__ cand;
   const float* __restrict__ ckey;
   const int* __restrict__ ncand;
-  const RollRes* __restrict__ res;   // [B][K]
-  const RollRes* __restrict__ res_gb; // [B][K]
+  const RollRes* __restrict__ res;   // [.][K]
+  const RollRes* __restrict__ res_gb; // [.][K]
   clrrt_node* regnodes;              // [B]
   clrrt_node* gbnodes;               // [B]
   SampleOut* so;                     // [B]
   int B;
+  const int* view;                   // [nd] ring indices of the deferred samples (oldest round first)
+  int nd, sbase;
+  int* gv;                           // [B] ring index of view v (null: not needed)
+  uint8_t* pend;                     // [B] 1 = view v is not resolved yet (null: every sample resolves)
 };
 
 // Frame of the brute-force search's float prune: positions relative to (ox, oy) in float are within
@@ -221,6 +245,7 @@ int nn_exact_small_max();
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, int* qnext, int* best, int blocks);
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t replay_bytes();
+size_t carry_bytes();  // one suspended rollout (deferred samples)
 // deferred rows: the committed rollouts' start states (jobs/recs from launch_compact, prep and res of the
 // round's lists / k_roll_run results) into out[0..n) for the next persistent launch's replays
 hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const clrrt_node* tree,
@@ -239,6 +264,9 @@ struct CompactBufs {
   size_t tmp_bytes;
 };
 size_t compact_scan_bytes(int n);
+size_t defer_select_bytes(int n);
+hipError_t launch_defer_select(hipStream_t st, const int* gv, const uint8_t* pend, int n, int* out, int* n_out,
+                               void* tmp, size_t tmp_bytes);
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
                           clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb);

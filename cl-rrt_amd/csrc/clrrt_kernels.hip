@@ -1308,6 +1308,25 @@ struct Replay {
   int32_t pad;
 };
 
+// Deferred samples (BATCH option "defer_steps" T).  A round's launch used to last as long as its longest
+// chain (a regular rollout + its goal-biased follow-up, up to ~1000 steps), three quarters of it a few
+// straggling lanes (profiles/r03x_roll_phases.txt).  With a cap T, every chain runs at most T more steps per
+// launch; a chain that reaches its cap is suspended here (its whole lane state) and resumed at the front of
+// the next launch's queue, and its sample is committed by the first commit after which every rollout its
+// result depends on has ended -- deterministically launch ceil(C / T) - 1 after its own, C = the longest of
+// those chains in steps (the oracle's orc_expand_batch_defer restates the rule).  Replays (deferred rows)
+// are capped the same way; they only write rows.
+struct Carry {
+  Roll r;
+  double c7, c8, c9;
+  int64_t row_off;   // replays: arena row of stateArray[0]; -1: no rows
+  int32_t j;         // ring index of the job (res / res_gb); 0 for replays
+  int32_t bs;        // ring index of the sample (best)
+  int32_t k, pass, steps, chain, rp, nrows_rp;
+};
+
+size_t carry_bytes() { return sizeof(Carry); }
+
 // Scheduling only: a rollout toward a sample 8-20 m away (1.7-4.2 turning radii) at 30-90 degrees off
 // the heading is the kind that ends in the iteration limit after the full horizon (the vehicle
 // circles without reaching the reference: tools/orbit_predict.py, cfg3 round 40: this class is 3% of
@@ -1377,13 +1396,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   WorkCtr w{0, 0, 0};
   Roll r;
   double c7 = 0, c8 = 0, c9 = 0;
-  int j = -1, k = 0, s = 0, pass = 0, steps = 0;
+  // j: ring index of the lane's job (res / res_gb; -1 idle, 0 for replays), bs: ring index of its sample
+  // (best), k: its candidate; chain: steps of the chain so far (regular + goal-biased), cap_at: the chain
+  // step count at which it is suspended (defer_steps)
+  int j = -1, k = 0, bs = 0, pass = 0, steps = 0, chain = 0, cap_at = 0x7fffffff;
   bool exhausted = false;
   // rows: where this lane's rollout writes stateArray (a replay's arena rows; nullptr for the speculative
   // rollouts when rows are deferred, else their job slots); rp: the lane replays a committed rollout of
   // nrows_rp rows
   const Replay* __restrict__ reps = (const Replay*)a.rep;
-  const int nq = a.nrep + a.njobs;  // queue: the replays, then the round's jobs
+  const Carry* __restrict__ cin = (const Carry*)a.carry_in;
+  Carry* __restrict__ cout = (Carry*)a.carry_out;
+  // queue: the suspended chains of the previous launch, the replays, then the round's jobs
+  const int nq = a.ncarry + a.nrep + a.njobs;
   double* rows = nullptr;
   bool rp = false;
   int nrows_rp = 0;
@@ -1435,7 +1460,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
         } else {
           a.res[j] = out;
           const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
-          if (ok) atomicMin(&best[s], k);
+          if (ok) atomicMin(&best[bs], k);
           if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
             // goal-biased rollout from the node this rollout would append (expandTree :163-173)
 #pragma unroll
@@ -1492,23 +1517,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           const int q0 = base + __popcll(m & ((1ull << lane) - 1));
           if (q0 >= nq) {
             exhausted = true;
-          } else if (q0 < a.nrep) {  // replay of a committed rollout: rows into the arena
-            const Replay& rq = reps[q0];
+          } else if (q0 < a.ncarry) {  // a chain suspended by the previous launch: resumed where it stopped
+            const Carry& cr = cin[q0];
+            r = cr.r;
+            c7 = cr.c7; c8 = cr.c8; c9 = cr.c9;
+            j = cr.j; bs = cr.bs; k = cr.k; pass = cr.pass; steps = cr.steps; chain = cr.chain;
+            rp = cr.rp != 0;
+            nrows_rp = cr.nrows_rp;
+            rows = cr.row_off >= 0 ? a.arena + cr.row_off * 10 : nullptr;
+            cap_at = a.cap > 0 ? chain + a.cap : 0x7fffffff;
+            if (!rp && __atomic_load_n(&best[bs], __ATOMIC_RELAXED) < k) {  // an earlier candidate succeeded
+              if (pass == 0) a.res[j].outcome = -1;
+              a.res_gb[j].outcome = -1;
+              j = -1;
+            }
+          } else if (q0 - a.ncarry < a.nrep) {  // replay of a committed rollout: rows into the arena
+            const Replay& rq = reps[q0 - a.ncarry];
             rp = true;
             nrows_rp = rq.nrows;
             rows = a.arena + rq.row_off * 10;
             j = 0;  // busy (replays touch no per-job result)
-            k = 0; s = 0; pass = 0; steps = 0;
+            k = 0; bs = 0; pass = 0; steps = 0; chain = 0;
+            cap_at = a.cap > 0 ? a.cap : 0x7fffffff;
             src = rq.src;
             iq = true;
           } else {
-            const int qj = q0 - a.nrep;
+            const int qj = q0 - a.ncarry - a.nrep;
             const int q = a.perm ? a.perm[qj] : qj;
             k = q / B;
-            s = q - k * B;
-            j = s * CAND_K + k;
-            const int id = a.cand[j];
-            if (id < 0 || __atomic_load_n(&best[s], __ATOMIC_RELAXED) < k) {
+            const int s = q - k * B;
+            const int jl = s * CAND_K + k;
+            j = a.jbase + jl;
+            bs = a.sbase + s;
+            const int id = a.cand[jl];
+            if (id < 0 || __atomic_load_n(&best[bs], __ATOMIC_RELAXED) < k) {
               a.res[j].outcome = -1;
               a.res_gb[j].outcome = -1;
               j = -1;
@@ -1522,7 +1564,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               iq = true;
               pass = 0;
               steps = 0;
-              rows = a.slots ? a.slots + j * slot : nullptr;
+              chain = 0;
+              cap_at = a.cap > 0 ? a.cap : 0x7fffffff;
+              rows = a.slots ? a.slots + jl * slot : nullptr;
 #ifdef CLRRT_ROLL_PROFILE
               job_steps = 0;
 #endif
@@ -1539,6 +1583,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       if (parked == 0 && qdone) break;
       continue;
     }
+    // a chain at its cap (defer_steps) is suspended before it takes another step: its lane state goes to
+    // carry_out (one slot reservation per wave), the lane turns idle and refills
+    {
+      const bool at_cap = j >= 0 && fin < 0 && chain >= cap_at;
+      const uint64_t cm = __ballot(at_cap);
+      if (cm) {
+        const int leader = __ffsll((unsigned long long)cm) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(a.ncarry_out, __popcll(cm));
+        base = __shfl(base, leader, 64);
+        if (at_cap) {
+          const int slot_c = base + __popcll(cm & ((1ull << lane) - 1));
+          if (slot_c < a.carry_cap) {
+            Carry& co = cout[slot_c];
+            co.r = r;
+            co.c7 = c7; co.c8 = c8; co.c9 = c9;
+            co.row_off = rows ? (int64_t)((rows - a.arena) / 10) : -1;
+            co.j = j; co.bs = bs; co.k = k; co.pass = pass; co.steps = steps; co.chain = chain;
+            co.rp = rp ? 1 : 0;
+            co.nrows_rp = nrows_rp;
+            if (!rp) {  // the sample's result waits for this rollout (k_select: pending)
+              if (pass == 0) a.res[j].outcome = CLRRT_ROLL_PENDING;
+              else a.res_gb[j].outcome = CLRRT_ROLL_PENDING;
+            }
+          } else {  // no carry slot left: the host reports it (the chain is dropped, the round is void)
+            if (a.ctr) atomicAdd(&a.ctr[62], 1ull);
+          }
+          rp = false;
+          rows = nullptr;
+          j = -1;
+        }
+      }
+    }
     // the lanes with a rollout in flight take a step; with the cooperative collision check (COOP) the
     // whole wave takes part in its SAT tests, so the check sits outside the lanes' divergent region
     const bool act = j >= 0 && fin < 0;
@@ -1547,12 +1624,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     double d2 = 0.0;
     if (act) {
       steps++;
+      chain++;
       // The abandon check's load of best[s] is issued BEFORE this step's row stores: vmcnt counts loads
       // and stores in issue order, so a load issued after the stores would wait for all ten of them to
       // complete (measured: ~60% of the kernel's wave time); issued here it only waits for the previous
       // step's stores, long retired.
       const bool check = !rp && (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
-      best_s = check ? __atomic_load_n(&best[s], __ATOMIC_RELAXED) : 0x7fffffff;
+      best_s = check ? __atomic_load_n(&best[bs], __ATOMIC_RELAXED) : 0x7fffffff;
       if (pc) pc->mark(6);
       d2 = roll_step_pre(r, a.p, c7, c8, c9, w, pc);
     }
@@ -1654,13 +1732,19 @@ __device__ __forceinline__ void fill_node(clrrt_node& n, const RollRes& r, int p
 }
 
 
-// The first candidate whose rollout succeeded (expandTree :150-160) and its goal-biased follow-up.
+// The first candidate whose rollout succeeded (expandTree :150-160) and its goal-biased follow-up, for
+// view v of the commit (SelArgs: a deferred sample of an earlier round, or a sample of this round).  A
+// sample whose result still depends on a suspended rollout (deferred samples) is marked pending and
+// commits nothing now.
 __global__ void k_select(SelArgs a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.B) return;
-  const int nc = a.ncand[s];
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= a.B) return;
+  const int g = v < a.nd ? a.view[v] : a.sbase + (v - a.nd);
+  const int64_t g0 = (int64_t)g * CAND_K;
+  const int nc = a.ncand[g];
   SampleOut o = {};
   o.k = -1;
+  o.g = g;
   // (outcome, nrows) of every candidate loaded up front: independent loads, one memory latency instead
   // of one per candidate tried
   static_assert(offsetof(RollRes, nrows) == offsetof(RollRes, outcome) + 4 && offsetof(RollRes, outcome) % 8 == 0,
@@ -1668,10 +1752,12 @@ __global__ void k_select(SelArgs a) {
   int2 on[CAND_K];
 #pragma unroll
   for (int k = 0; k < CAND_K; k++)
-    on[k] = k < nc ? *(const int2*)&a.res[s * CAND_K + k].outcome : make_int2(-1, 1);
+    on[k] = k < nc ? *(const int2*)&a.res[g0 + k].outcome : make_int2(-1, 1);
+  bool pend = false;
 #pragma unroll
   for (int k = 0; k < CAND_K; k++) {
-    if (k >= nc || o.k >= 0) break;
+    if (k >= nc || o.k >= 0 || pend) break;
+    if (on[k].x == CLRRT_ROLL_PENDING) { pend = true; break; }
     o.rollouts++;
     o.steps += on[k].y - 1;
     o.f_col += on[k].x == CLRRT_ROLL_COLLISION;
@@ -1679,33 +1765,46 @@ __global__ void k_select(SelArgs a) {
     o.f_it += on[k].x == CLRRT_ROLL_ITERLIMIT;
     if (on[k].x == CLRRT_ROLL_END || on[k].x == CLRRT_ROLL_GOAL) o.k = k;
   }
+  if (!pend && o.k >= 0 && a.res_gb[g0 + o.k].outcome == CLRRT_ROLL_PENDING) pend = true;
+  if (pend) {  // resolved by a later commit
+    SampleOut z = {};
+    z.k = -1;
+    z.g = g;
+    z.pend = 1;
+    a.so[v] = z;
+    if (a.gv) a.gv[v] = g;
+    if (a.pend) a.pend[v] = 1;
+    return;
+  }
+  if (a.gv) a.gv[v] = g;
+  if (a.pend) a.pend[v] = 0;
   // EXACT-mode conflict threshold: the key a new node must beat (<=) to be tried before the result.
-  o.thr = o.k >= 0 ? a.ckey[s * CAND_K + o.k] : (nc == a.p.sort_limit ? a.ckey[s * CAND_K + nc - 1] : __builtin_inff());
+  o.thr = o.k >= 0 ? a.ckey[g0 + o.k] : (nc == a.p.sort_limit ? a.ckey[g0 + nc - 1] : __builtin_inff());
   o.gb_ok = 0;
   if (o.k >= 0) {
-    const int pid = a.cand[s * CAND_K + o.k];
+    const int pid = a.cand[g0 + o.k];
     const clrrt_node& par = a.tree[pid];
     clrrt_node n;
-    fill_node(n, a.res[s * CAND_K + o.k], pid, par.costE, par.costS);
-    a.regnodes[s] = n;
+    fill_node(n, a.res[g0 + o.k], pid, par.costE, par.costS);
+    a.regnodes[v] = n;
     o.nrows_reg = n.nrows;
-    const RollRes& g = a.res_gb[s * CAND_K + o.k];
-    if (g.outcome >= 0) {  // the gate passed and the goal-biased rollout ran (:163-173)
+    const RollRes& gr = a.res_gb[g0 + o.k];
+    if (gr.outcome >= 0) {  // the gate passed and the goal-biased rollout ran (:163-173)
       o.rollouts++;
-      o.steps += g.nrows - 1;
-      o.f_col += g.outcome == CLRRT_ROLL_COLLISION;
-      o.f_acc += g.outcome == CLRRT_ROLL_ACCLIMIT;
-      o.f_it += g.outcome == CLRRT_ROLL_ITERLIMIT;
-      if (g.outcome == CLRRT_ROLL_END || g.outcome == CLRRT_ROLL_GOAL) {
+      o.steps += gr.nrows - 1;
+      o.f_col += gr.outcome == CLRRT_ROLL_COLLISION;
+      o.f_acc += gr.outcome == CLRRT_ROLL_ACCLIMIT;
+      o.f_it += gr.outcome == CLRRT_ROLL_ITERLIMIT;
+      if (gr.outcome == CLRRT_ROLL_END || gr.outcome == CLRRT_ROLL_GOAL) {
         clrrt_node gn;
-        fill_node(gn, g, CLRRT_PARENT_PREV, n.costE, n.costS);
-        a.gbnodes[s] = gn;
+        fill_node(gn, gr, CLRRT_PARENT_PREV, n.costE, n.costS);
+        a.gbnodes[v] = gn;
         o.gb_ok = 1;
         o.nrows_gb = gn.nrows;
       }
     }
   }
-  a.so[s] = o;
+  a.so[v] = o;
 }
 
 // EXACT mode: sample j conflicts when a node produced by an earlier sample of the round would sort
@@ -1797,8 +1896,8 @@ __global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut*
     n.owner = rank;
     n.row_offset = row_base + row_off;
     out[node_off] = n;
-    Job jb;  // row copy: slot of job (s, k*) pass 0 -> arena
-    jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 0; jb.pad = 0;
+    Job jb;  // row copy / replay: ring job (g, k*) pass 0 -> arena
+    jb.parent = o.g * CAND_K + o.k; jb.from_reg = 0; jb.gb = 0; jb.pad = 0;
     jb.sx = 0; jb.sy = 0;
     jb.row_off = row_base + row_off;
     jobs[node_off] = jb;
@@ -1810,8 +1909,8 @@ __global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut*
     n.owner = rank;
     n.row_offset = row_base + row_off;
     out[node_off] = n;
-    Job jb;  // row copy: slot of job (s, k*) pass 1 (goal-biased rollout) -> arena
-    jb.parent = s * CAND_K + o.k; jb.from_reg = 0; jb.gb = 1; jb.pad = 0;
+    Job jb;  // row copy / replay: ring job (g, k*) pass 1 (goal-biased rollout) -> arena
+    jb.parent = o.g * CAND_K + o.k; jb.from_reg = 0; jb.gb = 1; jb.pad = 0;
     jb.sx = 0; jb.sy = 0;
     jb.row_off = row_base + row_off;
     jobs[node_off] = jb;
@@ -2534,10 +2633,11 @@ static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
 }
 
 hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, int* qnext, int* best, int blocks) {
-  if (a0.njobs <= 0 && a0.nrep <= 0) return hipSuccess;
   hipError_t e;
+  if (a0.ncarry_out && (e = hipMemsetAsync(a0.ncarry_out, 0, sizeof(int), st)) != hipSuccess) return e;
+  if (a0.njobs <= 0 && a0.nrep <= 0 && a0.ncarry <= 0) return hipSuccess;
   if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(best, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
+  if (B > 0 && (e = hipMemsetAsync(best + a0.sbase, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
   RollArgs a = a0;
   a.B = B;
   // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then (COOP) the cooperative
@@ -2553,7 +2653,7 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
                                 : (const void*)&k_roll_run<false, false>;
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
-  const int nqueue = a0.njobs + a0.nrep;
+  const int nqueue = a0.njobs + a0.nrep + a0.ncarry;
   // a queue shorter than the grid's lanes is spread over its waves (lanes per wave = ceil(queue / waves))
   int lpw = a0.lanes_per_wave > 0 && a0.lanes_per_wave < 64 ? a0.lanes_per_wave : 64;
   if (a0.lanes_per_wave <= 0) {
@@ -2607,6 +2707,21 @@ hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrr
   hipLaunchKernelGGL(k_conflict, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, ctie, first);
   LAUNCH_CHECK();
   return hipSuccess;
+}
+
+// Deferred samples: the ring indices gv[v] of the views still pending after a commit, in view order (the
+// oldest round first, then this round's in sample order), into out[0 .. *n_out) -- the next commit's views.
+size_t defer_select_bytes(int n) {
+  size_t bytes = 0;
+  hipcub::DeviceSelect::Flagged(nullptr, bytes, (const int*)nullptr, (const uint8_t*)nullptr, (int*)nullptr,
+                                (int*)nullptr, n);
+  return bytes;
+}
+hipError_t launch_defer_select(hipStream_t st, const int* gv, const uint8_t* pend, int n, int* out, int* n_out,
+                               void* tmp, size_t tmp_bytes) {
+  if (n <= 0) return hipMemsetAsync(n_out, 0, sizeof(int), st);
+  size_t bytes = tmp_bytes;
+  return hipcub::DeviceSelect::Flagged(tmp, bytes, gv, pend, out, n_out, n, st);
 }
 
 size_t compact_scan_bytes(int n) {

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 8
+#define CLRRT_ABI_VERSION 9
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -173,6 +173,7 @@ typedef struct clrrt_stats {
   int64_t speculated;   /* samples evaluated (>= iterations in EXACT mode) */
   double elapsed_ms;
   int64_t capacity_stop; /* 1 when the loop ended because the next round could overflow capacity */
+  int64_t deferred;      /* BATCH with option "defer_steps": samples committed at least one round late */
 } clrrt_stats;
 
 typedef struct clrrt_capacity {

@@ -550,6 +550,10 @@ static bool feasible_goal_bias(Oracle& o, const Node& node) {  // :292-315 (cos 
 struct IterResult {
   bool added = false, gb_added = false;
   Node node, gb_node;
+  // the longest rollout chain the result depends on, in simulated steps: every candidate tried (a failed
+  // one: its steps; the accepted one: its steps + the goal-biased rollout's, when that ran) -- the BATCH
+  // engine's deferred-sample rule (defer_steps) commits the sample ceil(chain / T) - 1 rounds late
+  long chain = 0;
 };
 
 static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_t upto, bool stable = false) {
@@ -558,6 +562,7 @@ static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_
   for (int id : cand) {
     Ref r = get_reference(o, s, o.tree[id], 1);
     Sim sim = simulate(o, o.tree[id].state, r, false, o.tree[id].ref.v.back());
+    res.chain = std::max(res.chain, (long)sim.rows.size() - 1);
     if (sim.endReached || sim.goalReached) {
       Node n;
       n.state = sim.rows.back(); n.parentID = id; n.ref = r; n.tra = sim.rows;
@@ -572,6 +577,7 @@ static IterResult evaluate_iteration(Oracle& o, const Pt& s, bool explore, size_
     vector<double> g(o.p.goal, o.p.goal + 4);
     Ref rg = get_goal_reference(o, res.node, g);
     Sim sg = simulate(o, res.node.state, rg, true, res.node.ref.v.back());
+    res.chain = std::max(res.chain, (long)(res.node.tra.size() - 1) + (long)(sg.rows.size() - 1));
     if (sg.endReached || sg.goalReached) {
       Node n;
       n.state = sg.rows.back(); n.parentID = -2 /* set at append */; n.ref = rg; n.tra = sg.rows;
@@ -786,6 +792,51 @@ void orc_expand_batch(void* h, long n_iters, int B, int stable) {
     for (int j = 0; j < nb; j++) append_result(*o, rs[j]);
     done += nb;
   }
+}
+
+// BATCH mode with deferred samples (the engine's option "defer_steps" T, clrrt_kernels.hip Carry): every
+// sample is evaluated against the tree as it was at the start of its own round, exactly as above, but it is
+// appended by the commit of round r + D, D = ceil(chain / T) - 1 (its longest rollout chain, IterResult::chain,
+// runs T steps per round's launch); a commit appends the samples of earlier rounds that come due (oldest
+// round first, each round's in sample order), then the round's own samples with D = 0; after the last round
+// every sample still pending is appended in the same order.  T = 0: plain BATCH rounds.
+void orc_expand_batch_defer(void* h, long n_iters, int B, int stable, int T, long* deferred) {
+  Oracle* o = (Oracle*)h;
+  struct Pend { long due; IterResult r; };
+  std::vector<Pend> pend;  // (origin round, sample) order
+  long done = 0, round = 0, ndef = 0;
+  while (done < n_iters) {
+    int nb = (int)std::min<long>(B, n_iters - done);
+    std::vector<Pt> ss(nb);
+    std::vector<char> ex(nb);
+    for (int j = 0; j < nb; j++) {
+      ss[j] = sample_around(*o);
+      double r = static_cast<double>(rand()) / (static_cast<double>(RAND_MAX / (1)));
+      ex[j] = r <= 0.7;
+    }
+    size_t upto = o->tree.size();
+    std::vector<IterResult> rs(nb);
+    for (int j = 0; j < nb; j++) rs[j] = evaluate_iteration(*o, ss[j], ex[j], upto, stable != 0);
+    std::vector<Pend> keep;
+    for (auto& p : pend) {
+      if (p.due == round) append_result(*o, p.r);
+      else keep.push_back(std::move(p));
+    }
+    for (int j = 0; j < nb; j++) {
+      const long D = (T > 0 && rs[j].chain > 0) ? (rs[j].chain + T - 1) / T - 1 : 0;
+      if (D == 0) {
+        append_result(*o, rs[j]);
+      } else {
+        keep.push_back(Pend{round + D, std::move(rs[j])});
+        ndef++;
+      }
+    }
+    pend.swap(keep);
+    done += nb;
+    round++;
+  }
+  for (auto& p : pend) append_result(*o, p.r);
+  if (deferred) *deferred = ndef;
 }
 
 long orc_tree_size(void* h) { return (long)((Oracle*)h)->tree.size(); }

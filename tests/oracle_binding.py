@@ -35,6 +35,7 @@ def lib():
             "orc_expand": (None, [vp, l]),
             "orc_expand_budget": (l, [vp, d, i]),
             "orc_expand_batch": (None, [vp, l, i, i]),
+            "orc_expand_batch_defer": (None, [vp, l, i, i, i, C.POINTER(C.c_long)]),
             "orc_tree_size": (l, [vp]),
             "orc_get_nodes": (None, [vp, l, l, P(abi.Node)]),
             "orc_node_ref_len": (l, [vp, l]),
@@ -127,8 +128,15 @@ class Oracle:
     def expand(self, n):
         self.L.orc_expand(self.h, n)
 
-    def expand_batch(self, n, batch, stable=True):
-        self.L.orc_expand_batch(self.h, n, batch, 1 if stable else 0)
+    def expand_batch(self, n, batch, stable=True, defer_steps=0):
+        """BATCH rounds (the engine's semantics); defer_steps T > 0: deferred samples (orc_expand_batch_defer).
+        Returns the number of samples deferred at least one round."""
+        if defer_steps <= 0:
+            self.L.orc_expand_batch(self.h, n, batch, 1 if stable else 0)
+            return 0
+        nd = C.c_long(0)
+        self.L.orc_expand_batch_defer(self.h, n, batch, 1 if stable else 0, defer_steps, C.byref(nd))
+        return nd.value
 
     def expand_budget(self, ms, wall=True):
         return self.L.orc_expand_budget(self.h, ms, 1 if wall else 0)

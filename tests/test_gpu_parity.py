@@ -203,6 +203,45 @@ def test_batch_mode_tree_parity(kind, batch, strategy, persistent):
     assert bad is None and len(on["parent"]) == len(gn["parent"])
 
 
+@pytest.mark.parametrize("kind,batch,T,strategy,lag", [("obb200", 256, 24, "brute", 1), ("obb200", 256, 96, "walk", 1),
+                                                       ("moving", 128, 40, "brute", 1), ("empty", 64, 16, "brute", 1),
+                                                       ("obb200", 256, 32, "walk", 2), ("moving", 128, 8, "walk", 2)])
+def test_batch_deferred_tree_parity(kind, batch, T, strategy, lag):
+    """BATCH rounds with deferred samples (option defer_steps T): the rollout chains run at most T steps per
+    launch, suspended chains resume in the next launch, and a sample commits at the first commit after which
+    every rollout its result depends on has ended -- ceil(chain / T) - 1 rounds after its own (the oracle's
+    orc_expand_batch_defer).  The tree equals the oracle's node for node, bit for bit (rows and counters too),
+    with the lag-1 and lag-2 pipelines."""
+    mode, obs = _scene(kind)
+    iters = 6 * batch
+    o = Oracle(abi.default_params(collision_mode=mode), obs)
+    Oracle.srand(6)
+    o.init_tree()
+    ndef = o.expand_batch(iters, batch, stable=True, defer_steps=T)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 21,
+                       max_batch=batch)
+    _nn_strategy(pl, strategy)
+    pl.set_option("defer_steps", T)
+    pl.set_option("nn_lag", lag)
+    if obs is not None:
+        pl.set_obstacles(obs)
+    pl.tree_init()
+    st = pl.expand(clrrt.Rng(6), n_iters=iters, mode=clrrt.CLRRT_MODE_BATCH, batch=batch)
+    assert st["iterations"] == iters and st["rounds"] == 6
+    print(f"defer T={T}: {ndef} of {iters} samples deferred by the oracle")
+    assert ndef > 0
+    on, gn, bad = _compare_trees(o, pl, f"batch deferred {kind} B={batch} T={T} lag {lag}")
+    assert bad is None and len(on["parent"]) == len(gn["parent"])
+    assert np.array_equal(gn["costS"].view(np.uint32), on["costS"].view(np.uint32))
+    oc, gc = o.counters(), pl.counters()
+    for k in ("sim_count", "fail_collision", "fail_acclimit", "fail_iterlimit", "rollouts"):
+        assert oc[k] == gc[k], (k, oc[k], gc[k])
+    for i in range(1, len(on["parent"])):
+        rows = pl.rows(int(gn["row_offset"][i]), int(gn["nrows"][i]))
+        assert np.array_equal(rows.view(np.uint64), np.ascontiguousarray(o.rows(i)).view(np.uint64)), i
+    assert pl.debug_counters()[61] == 0
+
+
 def test_lockstep_iteration_parity():
     """Every iteration of a sequential oracle run, evaluated by the GPU on the oracle's own tree."""
     mode, obs = _scene("obb200")
@@ -348,6 +387,36 @@ def test_pipelined_batch_rounds_identical():
     assert trees[0][2] > 20000
     for t in trees[1:]:
         assert trees[0][0] == t[0] and trees[0][1] == t[1]
+
+
+@pytest.mark.gpu
+def test_deferred_batch_rounds_identical():
+    """Full-size property of the deferred-sample rounds (defer_steps): the pipelines (none, lag 1, lag 2) and
+    the scheduling options (grid width, queue order, per-lane collision checks) grow exactly the same tree --
+    which samples are deferred, and by how many rounds, depends on their rollouts' step counts only -- and
+    a sample is deferred in every variant; rows of every node replay exactly."""
+    mode, obs = _scene("obb200")
+    trees = []
+    variants = [dict(nn_pipeline=0), dict(nn_lag=1), dict(nn_lag=2), dict(nn_lag=2, roll_priority=0, roll_blocks=512),
+                dict(nn_lag=1, roll_coop=0, roll_blocks=64)]
+    for opts in variants:
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
+                           max_batch=16384)
+        pl.set_option("defer_steps", 64)
+        for k, v in opts.items():
+            pl.set_option(k, v)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(12), n_iters=16384 * 6, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+        assert st["rounds"] == 6 and st["deferred"] > 0, st
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), n, st["deferred"]))
+        assert pl.debug_counters()[61] == 0
+        pl.close()
+    print(f"deferred rounds: {trees[0][2]} nodes, {trees[0][3]} samples deferred")
+    assert trees[0][2] > 20000
+    for t in trees[1:]:
+        assert trees[0][0] == t[0] and trees[0][1] == t[1] and trees[0][3] == t[3]
 
 
 @pytest.mark.gpu
