@@ -44,6 +44,8 @@ PEAK_HBM_GBS = 8000.0
 # point scanned by findClosestPoint; FP32 per OBB box test = 36.
 FLOP_STEP, FLOP_SCAN, FLOP_BOX = 160, 6, 36
 FLOP_KEY = 40  # FP32 FLOP per nearest-node (Dubins) key
+# BATCH option defer_steps of the headline run
+DEFER_STEPS = 128
 
 
 def parse():
@@ -61,6 +63,13 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-exact", action="store_true", help="skip the secondary EXACT-mode figure")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--defer-steps", type=int, default=DEFER_STEPS,
+                    help="BATCH deferred samples: rollout chains run at most this many steps per round's launch, "
+                         "longer ones resume in the next and their sample commits in a later round (0: off)")
+    ap.add_argument("--no-sync", action="store_true", help="skip the secondary figure without deferred samples")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = batch samples per GPU per round (N x batch per round), strong = batch "
+                         "samples per round split over the GPUs")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path (e.g. several ranks sharing one GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -255,8 +264,13 @@ def main():
     # horizon instead of stopping at capacity (rows: 80 B x rows_per_node per node, 82 GB at 16 Mi nodes)
     max_nodes = args.max_nodes if args.max_nodes > 0 else max(6 << 20, (2 << 20) * world)
     max_rows = max_nodes * args.rows_per_node
-    pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B,
+    # samples per round over all ranks (weak: B per GPU; strong: B split over the GPUs) and per rank
+    G = B * world if args.scaling == "weak" else B
+    B_rank = -(-G // world)
+    pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B_rank,
                        max_obstacles=max(1, len(obs)))
+    defer = args.defer_steps
+    pl.set_option("defer_steps", defer)
     for kv in args.opt:
         k, v = kv.split("=", 1)
         pl.set_option(k, int(v))
@@ -266,8 +280,10 @@ def main():
     pl.set_stream(stream.cuda_stream)
 
     if world > 1:
+        # one code path for 1 and N GPUs: clrrt_expand runs the sharded rounds itself (this rank's slice of
+        # every round, lag-2 pipeline, deferred samples) and calls back once per round for the all-gather
         from clrrt import dist as cdist
-        ex = cdist.RoundExchange(2 * B, "cuda")
+        ex = cdist.ShardExchange(pl, cdist.exchange_capacity(B_rank, defer), "cuda")
 
     replanning = bool(cfg.get("replan"))
     if replanning:
@@ -276,35 +292,12 @@ def main():
         backend = replan.PlannerBackend(pl, make_params)
         rp = {"pose": [0.0, 0.0, 0.0, 0.0, 0.0, 0.0], "q": 0, "outcomes": [], "reinit_ms": 0.0, "path_len": []}
 
+    deferred = [0]
+
     def expand_query(rng):
-        if world == 1:
-            st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
-            return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
-        nodes = 0
-        goals = torch.zeros((), dtype=torch.int64, device="cuda")
-        cap_stop = 0
-        t0 = time.perf_counter()
-        first, count = cdist.shard(world * B, world, rank)
-        nxt = rng.draw_samples(pl.params, world * B)
-        while True:
-            n_now = pl.size()[0]
-            if n_now + 2 * world * B > max_nodes:
-                cap_stop = 1
-                break
-            allsmp, nxt = nxt, rng.draw_samples(pl.params, world * B)
-            mine = (abi.Sample * count).from_buffer(allsmp, first * C_SAMPLE)
-            # the next round's shard is searched beside this round's rollouts (clrrt_round_prefetch)
-            pl.round_prefetch((abi.Sample * count).from_buffer(nxt, first * C_SAMPLE))
-            n_local = pl.round_eval(mine, ex.records_ptr())
-            # one count-prefixed all-gather of the accepted-node records (RCCL over xGMI)
-            cat, counts, my_first, t_max = ex.exchange(n_local, (time.perf_counter() - t0) * 1e3)
-            pl.round_commit(cat.data_ptr() if cat.shape[0] else 0, cat.shape[0], my_first, counts[rank])
-            nodes += cat.shape[0]
-            goals += cdist.goal_sum(cat)
-            if t_max >= horizon:
-                break
-        pl.rows_flush()  # the last round's accepted rows (part of the query's tree, so inside its time)
-        return nodes, int(goals.item()), cap_stop
+        st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
+        deferred[0] += st["deferred"]
+        return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
 
     def query(seed):
         """One planning query; returns (nodes appended, goal nodes appended, capacity_stop)."""
@@ -378,6 +371,19 @@ def main():
     cnt = pl.counters()
     sw = pl.search_work()
 
+    sync_line = None
+    if world == 1 and not replanning and not args.no_sync and defer > 0:
+        # secondary figure: plain BATCH rounds (every sample commits in its own round), one query from a
+        # fresh tree, same scene, horizon and seed
+        pl.set_option("defer_steps", 0)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(args.seed), n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+        sync_line = {"value": st["nodes_added"] / (st["elapsed_ms"] * 1e-3), "unit": "nodes/s",
+                     "feasible_paths_per_s": st["goal_nodes_added"] / (st["elapsed_ms"] * 1e-3),
+                     "rounds": st["rounds"], "horizon_ms": horizon,
+                     "note": "BATCH rounds without deferred samples (defer_steps 0); 1 query, wall clock"}
+        pl.set_option("defer_steps", defer)
+
     exact_line = None
     if world == 1 and not replanning and not args.no_exact:
         # secondary figure: EXACT mode (the reference's sequential expandTree tree, bit for bit) on the
@@ -421,7 +427,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
@@ -429,11 +435,14 @@ def main():
         "config": {
             "workload": cfg["desc"],
             "samples_per_batch": B,
+            "samples_per_round": G,
             "obstacles": cfg["obstacles"] + cfg["moving"],
             "horizon_ms": horizon,
             "mode": "BATCH",
             "parallelism": f"dp{world}",
             "capacity_stops": cap_stops,
+            "defer_steps": defer,
+            "samples_deferred": deferred[0],
             "trees_identical_across_ranks": trees_identical,
         },
         "roofline": {
@@ -485,6 +494,8 @@ def main():
             "path_lengths": rp["path_len"][-args.steps:], "goal_nodes": rp["goal_nodes"][-args.steps:],
             "tree_nodes_last": pl.size()[0], "reinit_ms_avg": rp["reinit_ms"] / nq,
             "note": "outcome 0 empty, 1 all erased, 2 committed path collides, 3 re-initialised from the path"}
+    if sync_line:
+        line["batch_sync"] = sync_line
     if exact_line:
         line["exact_mode"] = exact_line
     if cpu_line:

@@ -25,6 +25,8 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "clrrt.h")
 
 _lib = None
 P = C.POINTER
+# clrrt_exchange_fn (include/clrrt.h): (user, n_local, elapsed_ms, *dev_all, *n_all, *max_elapsed_ms) -> status
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_double, P(C.c_void_p), P(C.c_int32), P(C.c_double))
 
 _SIGS = {
     "clrrt_abi_version": (C.c_int, []),
@@ -39,6 +41,7 @@ _SIGS = {
     "clrrt_set_params": (C.c_int, [C.c_void_p, P(abi.Params)]),
     "clrrt_set_obstacles": (C.c_int, [C.c_void_p, P(abi.Obstacle), C.c_int32]),
     "clrrt_set_rank": (C.c_int, [C.c_void_p, C.c_int32]),
+    "clrrt_set_shards": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, EXCHANGE_FN, C.c_void_p]),
     "clrrt_tree_init": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "clrrt_tree_load": (C.c_int, [C.c_void_p, P(abi.Node), C.c_int64]),
     "clrrt_tree_size": (C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64)]),
@@ -101,7 +104,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.clrrt_abi_version() != abi.CLRRT_ABI_VERSION:
+        if L.clrrt_abi_version() != abi.CLRRT_ABI_VERSION and not os.environ.get("CLRRT_ABI_ANY"):  # (bisection builds)
             raise ClrrtError(f"{LIB_PATH}: ABI version {L.clrrt_abi_version()} != {abi.CLRRT_ABI_VERSION}; rebuild")
         _lib = L
     return _lib
@@ -206,6 +209,14 @@ class Planner:
 
     def set_rank(self, rank):
         self._chk(self.L.clrrt_set_rank(self.h, rank), "set_rank")
+
+    def set_shards(self, rank, world, dev_local=0, cap_local=0, exchange=None):
+        """Sharded BATCH expansion (clrrt_set_shards): `exchange` is an EXCHANGE_FN (keep a reference to it
+        for as long as the planner uses it; clrrt.dist.ShardExchange does)."""
+        self._exchange = exchange
+        fn = exchange if exchange is not None else EXCHANGE_FN()
+        self._chk(self.L.clrrt_set_shards(self.h, rank, world, C.c_void_p(dev_local), cap_local, fn, None),
+                  "set_shards")
 
     def set_obstacles(self, obs):
         obs = np.ascontiguousarray(obs, dtype=np.float64).reshape(-1, 7)

@@ -82,6 +82,55 @@ class RoundExchange:
         return cat.contiguous(), counts, sum(counts[:self.rank]), t_max
 
 
+class ShardExchange:
+    """The exchange hook of the engine's own sharded rounds (clrrt_set_shards): clrrt_expand runs every
+    round -- this rank's slice of the samples, the lag-2 pipeline, deferred samples -- and calls back once
+    per round with its records already in `records_ptr()`; the callback runs RoundExchange's count-prefixed
+    all-gather (RCCL over xGMI with the nccl backend) and hands the concatenation in rank order back, with
+    the largest elapsed query time over the ranks (the engine's budget decision, identical on every rank).
+    One code path for 1 and N GPUs: with world 1 the engine appends its records itself."""
+
+    def __init__(self, planner, cap_records, device, group=None, first_bound=1024):
+        import ctypes
+        import traceback
+        from . import EXCHANGE_FN
+        self.rx = RoundExchange(cap_records, device, group, first_bound)
+        self.rank, self.world = self.rx.rank, self.rx.world
+        self._keep = None
+        self.rounds = 0
+
+        def cb(user, n_local, elapsed_ms, dev_all, n_all, max_ms):
+            try:
+                cat, counts, _, t_max = self.rx.exchange(n_local, elapsed_ms)
+                self._keep = cat  # the engine reads it (stream-ordered) before the next exchange
+                dev_all[0] = ctypes.c_void_p(cat.data_ptr() if cat.shape[0] else None).value
+                n_all[0] = int(cat.shape[0])
+                max_ms[0] = float(t_max)
+                self.rounds += 1
+                return 0
+            except Exception:  # reported to the engine, which returns CLRRT_EHIP
+                traceback.print_exc()
+                return -1
+
+        self._cb = EXCHANGE_FN(cb)
+        planner.set_shards(self.rank, self.world, self.rx.records_ptr(), self.rx.cap, self._cb)
+
+    @property
+    def second_gathers(self):
+        return self.rx.second_gathers
+
+
+def exchange_capacity(max_batch, defer_steps=0, sim_dt=0.04):
+    """Records one rank may commit in a round: 2 per sample of its slice and of its deferred samples (at
+    most the ring's R - 1 earlier rounds: R = ceil(2 n_steps / T) + 2, clrrt_capi.hip ensure_defer)."""
+    import math
+    n_steps = 0
+    while n_steps < 20.0 / sim_dt:
+        n_steps += 1
+    R = (2 * n_steps + defer_steps - 1) // defer_steps + 2 if defer_steps > 0 else 1
+    return 2 * max_batch * R
+
+
 def goal_sum(records):
     """Appended nodes with goalReached set (feasible paths) among the records, as a device tensor (no
     host sync: accumulate per query, read once)."""
@@ -95,9 +144,10 @@ def goal_count(records):
 
 
 def shard(n_total, world, rank):
-    """Contiguous slice [first, first + count) of a round's samples handled by `rank`."""
-    per = n_total // world
-    return rank * per, per
+    """Contiguous slice [first, first + count) of a round's samples handled by `rank` (the engine's
+    shard_slice, clrrt_capi.hip)."""
+    first = n_total * rank // world
+    return first, n_total * (rank + 1) // world - first
 
 
 def fetch_path_rows(planner, rank, group=None):

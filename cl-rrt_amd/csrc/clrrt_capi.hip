@@ -224,6 +224,22 @@ struct clrrt_ctx {
     int slot = 0;                 // ring slot of the current round
     int64_t deferred_total = 0;   // samples deferred at least once (statistics)
   } def;
+  // Sharded BATCH expansion (clrrt_set_shards): this rank's slice of every round, one exchange of the
+  // accepted-node records per round through the caller's collective
+  struct {
+    int rank = 0, world = 1;
+    void* dev_local = nullptr;     // the caller's buffer the local records go to
+    int cap_local = 0;
+    clrrt_exchange_fn fn = nullptr;
+    void* user = nullptr;
+    double max_ms = 0;             // largest elapsed query time over the ranks at the last exchange
+    clrrt_node* xbuf = nullptr;    // the exchanged records in commit order (deferred samples: by age)
+    uint32_t* xkey = nullptr;      // [2 xcap] sort keys (age), [2 xcap] record indices
+    void* xtmp = nullptr;
+    size_t xtmp_bytes = 0;
+    int64_t xcap = 0;
+    unsigned long long* d_goal = nullptr;  // goal nodes among the appended records (device counter)
+  } sh;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -247,6 +263,7 @@ static void pf_reset(clrrt_ctx* c);
 static int flush_replays(clrrt_ctx* c);
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n);
 static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped);
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app);
 static int ensure_slots(clrrt_ctx* c);
 
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
@@ -480,6 +497,9 @@ static void free_all(clrrt_ctx* c) {
                   c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids,
                   c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun};
   for (void* p : ptrs)
+    if (p) hipFree(p);
+  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal};
+  for (void* p : sptrs)
     if (p) hipFree(p);
   void* dptrs[] = {c->def.res, c->def.res_gb, c->def.cand, c->def.ncand, c->def.samp, c->def.best, c->def.dlist[0],
                    c->def.dlist[1], c->def.gv, c->def.pend, c->def.sel_tmp, c->def.d_cnt, c->def.carry[0],
@@ -1673,8 +1693,10 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   const int V = defer ? d.nd_eval + L : L;
   {
     KTimer kt(c, 2);
+    const bool tag = defer && c->sh.world > 1;  // the exchange orders deferred samples by age
     HIPC(c, launch_compact(st, V, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
-                           c->out_nodes, c->jobs, c->totals, c->cmp));
+                           c->out_nodes, c->jobs, c->totals, c->cmp, tag ? d.slot : 0, tag ? d.R : 0,
+                           (int)c->cap.max_batch));
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
     // the views still pending, in view order: the next commit's deferred samples
     if (defer) HIPC(c, launch_defer_select(st, d.gv, d.pend, V, d.dlist[1 - d.cur_dl], d.d_cnt, d.sel_tmp, d.sel_bytes));
@@ -1750,9 +1772,10 @@ static int ensure_defer(clrrt_ctx* c) {
     HIPC(c, dalloc(&d.best, (size_t)R * B));
     d.R = R;
   }
-  if (!d.gv) {
-    // every commit path holds up to vcap views: the deferred samples + one round
-    const int64_t V = 2 * B;
+  if (!d.gv || d.vcap < (int64_t)d.R * B) {
+    // every commit path holds up to vcap views: the deferred samples (at most R - 1 earlier rounds' worth,
+    // the ring) + one round
+    const int64_t V = (int64_t)d.R * B;
     int rc = flush_replays(c);  // rep_buf is re-made below
     if (rc != CLRRT_OK) return rc;
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -1761,6 +1784,11 @@ static int ensure_defer(clrrt_ctx* c) {
       if (p) HIPC(c, hipFree(p));
     c->regnodes = nullptr; c->gbnodes = nullptr; c->so = nullptr; c->out_nodes = nullptr; c->jobs = nullptr;
     c->rep_buf = nullptr; c->cmp.packed = nullptr; c->cmp.scanned = nullptr; c->cmp.tmp = nullptr;
+    for (void* p : {(void*)d.dlist[0], (void*)d.dlist[1], (void*)d.gv, (void*)d.pend, d.sel_tmp, (void*)d.d_cnt,
+                    d.carry[0], d.carry[1]})
+      if (p) HIPC(c, hipFree(p));
+    d.dlist[0] = d.dlist[1] = nullptr; d.gv = nullptr; d.pend = nullptr; d.sel_tmp = nullptr; d.d_cnt = nullptr;
+    d.carry[0] = d.carry[1] = nullptr;
     HIPC(c, dalloc(&c->regnodes, V));
     HIPC(c, dalloc(&c->gbnodes, V));
     HIPC(c, dalloc(&c->so, V));
@@ -1778,7 +1806,8 @@ static int ensure_defer(clrrt_ctx* c) {
     d.sel_bytes = defer_select_bytes((int)V);
     HIPC(c, hipMalloc(&d.sel_tmp, std::max<size_t>(d.sel_bytes, 256)));
     HIPC(c, dalloc(&d.d_cnt, 2));
-    d.carry_cap = (int)std::min<int64_t>(B * CAND_K, INT_MAX / 2);
+    // suspended chains: at most every job of the rounds in flight (a launch's chains all come from them)
+    d.carry_cap = (int)std::min<int64_t>(V * CAND_K, 1 << 21);
     HIPC(c, hipMalloc(&d.carry[0], carry_bytes() * (size_t)d.carry_cap));
     HIPC(c, hipMalloc(&d.carry[1], carry_bytes() * (size_t)d.carry_cap));
     d.vcap = V;
@@ -1864,7 +1893,8 @@ static int flush_replays(clrrt_ctx* c) {
 static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
   auto& d = c->def;
   if (!d.active) return CLRRT_OK;
-  if (d.nd > 0 || d.ncarry > 0) {
+  const bool sharded = c->sh.world > 1;  // every rank takes part in the final exchange
+  if (d.nd > 0 || d.ncarry > 0 || sharded) {
     hipStream_t st = c->stream;
     {
       KTimer kt(c, 1);
@@ -1878,20 +1908,20 @@ static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
       c->rep_n = 0;
       d.ncarry = 0;
     }
-    if (d.nd > 0) {
+    if (d.nd > 0 || sharded) {
       SelArgs s;
       memset(&s, 0, sizeof(s));
       s.p = c->dp; s.tree = c->tree; s.cand = d.cand; s.ckey = c->ckey; s.ncand = d.ncand; s.res = d.res;
       s.res_gb = d.res_gb; s.regnodes = c->regnodes; s.gbnodes = c->gbnodes; s.so = c->so;
       s.view = d.dlist[d.cur_dl]; s.nd = d.nd; s.sbase = 0; s.gv = d.gv; s.pend = d.pend; s.B = d.nd;
-      {
+      if (d.nd > 0) {
         KTimer kt(c, 2);
         HIPC(c, launch_select(st, s));
       }
       d.nd_eval = d.nd;
-      int nn = 0;
+      int nn = 0, n_app = 0;
       int rc = compact_and_copy(c, 0, &nn, true);
-      if (rc == CLRRT_OK) rc = append_nodes(c, c->out_nodes, nn);
+      if (rc == CLRRT_OK) rc = commit_round(c, nn, c->sh.max_ms, &n_app);
       if (rc != CLRRT_OK) return rc;
       if (goal_nodes) *goal_nodes += c->last_goal_nodes;
       if (d.nd != 0 || d.ncarry != 0) return fail(c, CLRRT_EHIP, "deferred samples left after the drain");
@@ -1997,6 +2027,75 @@ int clrrt_round_prefetch(clrrt_ctx* c, const clrrt_sample* next, int32_t n) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sharded rounds: goal nodes among the records appended since the last reset (every rank's), read once at
+// the end of an expansion.
+static int shard_goal_reset(clrrt_ctx* c) {
+  HIPC(c, hipMemsetAsync(c->sh.d_goal, 0, sizeof(unsigned long long), c->stream));
+  return CLRRT_OK;
+}
+static int shard_goal_count(clrrt_ctx* c, int64_t* out) {
+  unsigned long long v = 0;
+  HIPC(c, hipMemcpyAsync(c->h_totals, c->sh.d_goal, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  memcpy(&v, c->h_totals, sizeof(v));
+  *out = (int64_t)v;
+  return CLRRT_OK;
+}
+
+// Sharded rounds (clrrt_set_shards): this rank's contiguous slice [f, f + n) of a round of g samples.
+static inline void shard_slice(const clrrt_ctx* c, int64_t g, int64_t* f, int* n) {
+  const int64_t W = c->sh.world, r = c->sh.rank;
+  *f = g * r / W;
+  *n = (int)(g * (r + 1) / W - *f);
+}
+
+// The commit of a round's records (c->out_nodes[0 .. nn)): appended as they are (one rank), or exchanged
+// with the other ranks and the union appended in the same order on every rank.  *n_app = records appended.
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
+  auto& h = c->sh;
+  *n_app = 0;
+  if (h.world <= 1) {
+    *n_app = nn;
+    return append_nodes(c, c->out_nodes, nn);
+  }
+  if (nn > h.cap_local) return fail(c, CLRRT_ECAPACITY, "the round's records exceed the exchange buffer");
+  if (nn > 0)
+    HIPC(c, hipMemcpyAsync(h.dev_local, c->out_nodes, sizeof(clrrt_node) * nn, hipMemcpyDeviceToDevice, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));  // the caller's collective reads dev_local
+  void* all = nullptr;
+  int32_t n_all = 0;
+  double mx = elapsed_ms;
+  if (h.fn(h.user, nn, elapsed_ms, &all, &n_all, &mx) != 0 || n_all < 0 || (n_all > 0 && !all))
+    return fail(c, CLRRT_EHIP, "the exchange of the round's records failed");
+  h.max_ms = mx;
+  if (n_all > 0) {
+    if (n_all > h.xcap) {
+      HIPC(c, hipStreamSynchronize(c->stream));
+      for (void* p : {(void*)h.xbuf, (void*)h.xkey, h.xtmp})
+        if (p) HIPC(c, hipFree(p));
+      h.xbuf = nullptr; h.xkey = nullptr; h.xtmp = nullptr;
+      const int64_t cap = std::max<int64_t>(2 * (int64_t)n_all, 4096);
+      HIPC(c, dalloc(&h.xbuf, cap));
+      HIPC(c, dalloc(&h.xkey, 4 * cap));
+      h.xtmp_bytes = xorder_sort_bytes((int)cap);
+      HIPC(c, hipMalloc(&h.xtmp, std::max<size_t>(h.xtmp_bytes, 256)));
+      h.xcap = cap;
+    }
+    HIPC(c, launch_xorder(c->stream, (const clrrt_node*)all, n_all, c->def.active, h.xkey, h.xtmp, h.xtmp_bytes,
+                          h.xbuf, h.d_goal));
+    int rc = append_nodes(c, h.xbuf, n_all);
+    if (rc != CLRRT_OK) return rc;
+    // the tree's bounding box takes every rank's records (the walk frame is then the same on every rank)
+    HIPC(c, launch_bbox(c->stream, h.xbuf, nullptr, n_all, c->d_bbox));
+    HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+  }
+  *n_app = n_all;
+  return CLRRT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Lag-2 pipelined BATCH rounds (option "nn_lag" 2).  BATCH rounds commit every sample, so the samples of
 // the next rounds are known ahead.  The walk search of round r+2's samples runs over the tree T_r (the
 // tree round r's rollouts start from) on a side stream, beside rounds r and r+1; after round r+1's
@@ -2015,7 +2114,8 @@ struct LagSlot {
   int* ctie = nullptr;
   hipEvent_t ev = nullptr;  // recorded after its merge
   hipEvent_t evw = nullptr; // recorded after its walk (the merge waits for it on the merge stream)
-  int n = 0;                // samples searched (0: none)
+  int n = 0;                // samples searched (0: none): this rank's slice
+  int64_t g = 0;            // samples of the round (all ranks)
   int64_t tree_n = 0;       // size of the tree its walk searched
   int stream = 0;           // side stream index
 };
@@ -2089,7 +2189,10 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   const auto t0 = std::chrono::steady_clock::now();
   clrrt_rng work = *rng, committed = *rng;
   std::deque<clrrt_sample> pending;
-  const int cur = batch;
+  const int cur = batch;  // samples per round, all ranks
+  const bool sharded = c->sh.world > 1;
+  c->sh.max_ms = 0;
+  if (sharded && (rc = shard_goal_reset(c)) != CLRRT_OK) return rc;
   const int64_t nodes_before = c->n_nodes;
   hipStream_t sides[2] = {c->side, c->side2};
   WalkBufs* W[3] = {&c->nnw, &c->nnw_alt, &c->nnw3};
@@ -2170,16 +2273,23 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       pending.push_back(smp);
     }
   };
-  for (int64_t k = 0;; k++) {
+  for (int64_t k = 0; rc == CLRRT_OK; k++) {
     const auto tr0 = std::chrono::steady_clock::now();
     if (n_iters > 0 && st.iterations >= n_iters) break;
     const double ms0 = std::chrono::duration<double, std::milli>(tr0 - t0).count();
-    if (n_iters == 0 && !(ms0 < budget_ms)) break;
+    // sharded: every rank decides on the largest elapsed time over the ranks (the same rounds everywhere)
+    if (n_iters == 0 && !((sharded ? c->sh.max_ms : ms0) < budget_ms)) break;
     const int64_t left = n_iters > 0 ? n_iters - st.iterations : INT64_MAX;
-    const int nb = (int)std::min<int64_t>(cur, left);
-    // (a commit also takes the deferred samples that resolve)
-    const int64_t nc = nb + (int64_t)c->def.nd;
-    if (c->n_nodes + 2 * nc > c->cap.max_nodes || c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+    // gb samples this round over all ranks; this rank's slice [f0, f0 + nb)
+    const int64_t gb = std::min<int64_t>(cur, left);
+    int64_t f0 = 0;
+    int nb = (int)gb;
+    if (sharded) shard_slice(c, gb, &f0, &nb);
+    // (a commit also takes the deferred samples that resolve; sharded, the stop decision must be the same
+    // on every rank: node counts only, the deferred samples bounded by the ring's rounds)
+    const int64_t nc = sharded ? gb * std::max(1, c->def.active ? c->def.R : 1) : gb + (int64_t)c->def.nd;
+    if (c->n_nodes + 2 * nc > c->cap.max_nodes ||
+        (!sharded && c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;
@@ -2187,22 +2297,29 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     const int wk = (int)(k % 3);
     const NnSetup su = nn_setup(c);
     const bool serve = c->n_nodes >= c->nnw_min_nodes && su.region_ok;
-    // samples of rounds r+1 (slot A, unless already searched) and r+2 (slot B) to search this round
+    // samples of rounds r+1 (slot A, unless already searched) and r+2 (slot B) to search this round (gA, gB
+    // over all ranks; nA, nB this rank's slices)
+    int64_t gA = 0, gB = 0, fA = 0, fB = 0;
     int nA = 0, nB = 0;
     if (serve) {
       const bool more = n_iters > 0 || ms0 + 2.0 * last_round_ms < budget_ms;
-      if (A.n == 0 && (n_iters > 0 || ms0 + last_round_ms < budget_ms)) nA = (int)std::min<int64_t>(cur, left - nb);
-      const int64_t nA_eff = A.n > 0 ? A.n : nA;
-      if (more && nA_eff > 0) nB = (int)std::min<int64_t>(cur, left - nb - nA_eff);
-      nA = std::max(nA, 0);
-      nB = std::max(nB, 0);
+      if (A.n == 0 && (n_iters > 0 || ms0 + last_round_ms < budget_ms)) gA = std::max<int64_t>(0, std::min<int64_t>(cur, left - gb));
+      const int64_t gA_eff = A.n > 0 ? A.g : gA;
+      if (more && gA_eff > 0) gB = std::max<int64_t>(0, std::min<int64_t>(cur, left - gb - gA_eff));
+      nA = (int)gA;
+      nB = (int)gB;
+      if (sharded) {
+        shard_slice(c, gA, &fA, &nA);
+        shard_slice(c, gB, &fB, &nB);
+      }
     }
-    draw_to(nb + (int64_t)std::max(A.n, nA) + nB);
+    const int64_t gA_all = A.n > 0 ? A.g : gA;
+    draw_to(gb + gA_all + gB);
     // this round's lists
     if (have_cur) {
       HIPC(c, hipStreamWaitEvent(c->stream, cur_ev, 0));
     } else {
-      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
+      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[f0 + j];
       HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
       if (serve) {
         // the side streams' work is done (a first pipelined round searches nothing ahead yet)
@@ -2226,23 +2343,26 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     // is shared: one stream)
     auto ahead = [&]() -> int {
       if (nA > 0) {
-        for (int j = 0; j < nA; j++) A.h[j] = pending[nb + j];
+        for (int j = 0; j < nA; j++) A.h[j] = pending[gb + fA + j];
         const int r2 = walk(A, nA, wk, su, cur_stream);
         if (r2 != CLRRT_OK) return r2;
+        A.g = gA;
       }
       if (nB > 0) {
-        for (int j = 0; j < nB; j++) B.h[j] = pending[nb + A.n + j];
+        for (int j = 0; j < nB; j++) B.h[j] = pending[gb + gA_all + fB + j];
         const int r2 = walk(B, nB, wk, su, nA > 0 ? A.stream : 1 - A.stream);
         if (r2 != CLRRT_OK) return r2;
+        B.g = gB;
       }
       return CLRRT_OK;
     };
-    int L = nb, nn = 0;
+    int L = nb, nn = 0, n_app = 0;
     if ((rc = eval_samples(c, nb, false, &L, true, (nA > 0 || nB > 0) ? std::function<int()>(ahead) : nullptr,
                            nullptr)) != CLRRT_OK)
       break;
     if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
-    if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
+    const double ms_commit = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if ((rc = commit_round(c, nn, ms_commit, &n_app)) != CLRRT_OK) break;
     // slot A: merge the nodes appended since its walk's tree
     if (A.n > 0) {
       hipStream_t s = c->mst;  // behind the commit and slot A's walk
@@ -2266,13 +2386,13 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       if (B.n > 0 && c->n_nodes >= c->nnw_min_nodes && sn.region_ok && (rc = build((int)((k + 1) % 3), sn)) != CLRRT_OK)
         break;
     }
-    for (int j = 0; j < L; j++) {
+    for (int64_t j = 0; j < gb; j++) {
       pending.pop_front();
       for (int q = 0; q < 3; q++) clrrt_rng_next(&committed);
     }
-    st.iterations += L;
+    st.iterations += gb;
     st.goal_nodes_added += c->last_goal_nodes;
-    st.speculated += nb;
+    st.speculated += gb;
     st.rounds++;
     // rotate: A becomes this round's set, B slot A, this round's set slot B
     {
@@ -2297,6 +2417,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   st.deferred = c->def.deferred_total;
   if (rc == CLRRT_OK) rc = flush_replays(c);
   c->def.active = false;
+  if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);
   for (hipStream_t s : {c->side, c->side2, c->mst, c->stream}) {  // every stream drained, the first error kept
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess && rc == CLRRT_OK) rc = fail(c, CLRRT_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
@@ -2314,8 +2435,13 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   pf_reset(c);
   if (n_iters == 0 && !(budget_ms > 0)) return CLRRT_EINVAL;
   if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
+  const bool sharded = c->sh.world > 1;
+  if (sharded && mode != CLRRT_MODE_BATCH) return fail(c, CLRRT_EINVAL, "sharded expansion runs BATCH rounds only");
   HIPC(c, hipSetDevice(c->device));
-  batch = std::max(1, std::min<int32_t>(batch > 0 ? batch : c->cap.max_batch, c->cap.max_batch));
+  // samples per round (all ranks when sharded: each rank's slice must fit max_batch)
+  const int64_t bmax = (int64_t)c->cap.max_batch * c->sh.world;
+  batch = (int32_t)std::max<int64_t>(1, std::min<int64_t>(batch > 0 ? batch : bmax, bmax));
+  if (sharded && batch < c->sh.world) return fail(c, CLRRT_EINVAL, "fewer samples per round than ranks");
   const int lag = c->nn_lag ? c->nn_lag
                   : (n_iters == 0 ? budget_ms >= 1000.0 : n_iters >= 64 * (int64_t)batch) ? 2 : 1;
   if (mode == CLRRT_MODE_BATCH && c->nn_pipeline && lag == 2) return expand_lag2(c, rng, n_iters, budget_ms, batch, out);
@@ -2328,31 +2454,43 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   int cur = exact ? std::min(batch, std::max(16, c->exact_min_width)) : batch;
   int64_t nodes_before = c->n_nodes;
   int rc = defer_begin(c, !exact);
+  c->sh.max_ms = 0;
+  if (rc == CLRRT_OK && sharded) rc = shard_goal_reset(c);
   bool have_next = false;  // this round's samples and lists were prepared by the previous round
   double last_round_ms = 0;
+  auto draw_to = [&](int64_t want) {
+    while ((int64_t)pending.size() < want) {
+      clrrt_sample smp;
+      clrrt_draw_samples(&c->params, &work, 1, &smp);
+      pending.push_back(smp);
+    }
+  };
   for (; rc == CLRRT_OK;) {
     const auto tr0 = std::chrono::steady_clock::now();
     if (n_iters > 0 && st.iterations >= n_iters) break;
     if (n_iters == 0) {
       double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      if (!(ms < budget_ms)) break;
+      // sharded: every rank decides on the largest elapsed time over the ranks (the same rounds everywhere)
+      if (!((sharded ? c->sh.max_ms : ms) < budget_ms)) break;
     }
-    int nb = cur;
-    if (n_iters > 0) nb = (int)std::min<int64_t>(nb, n_iters - st.iterations);
-    // a round appends at most 2 nodes and 2 full-horizon trajectories per sample (+ the deferred samples)
-    const int64_t nc = nb + (int64_t)c->def.nd;
-    if (c->n_nodes + 2 * nc > c->cap.max_nodes || c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows) {
+    // gb samples this round over all ranks; this rank's slice [f0, f0 + nb)
+    int64_t gb = cur;
+    if (n_iters > 0) gb = std::min<int64_t>(gb, n_iters - st.iterations);
+    int64_t f0 = 0;
+    int nb = (int)gb;
+    if (sharded) shard_slice(c, gb, &f0, &nb);
+    // a round appends at most 2 nodes and 2 full-horizon trajectories per sample (+ the deferred samples;
+    // sharded, the same decision on every rank: node counts only, deferred samples bounded by the ring)
+    const int64_t nc = sharded ? gb * std::max(1, c->def.active ? c->def.R : 1) : gb + (int64_t)c->def.nd;
+    if (c->n_nodes + 2 * nc > c->cap.max_nodes ||
+        (!sharded && c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;
     }
-    while ((int)pending.size() < nb) {
-      clrrt_sample smp;
-      clrrt_draw_samples(&c->params, &work, 1, &smp);
-      pending.push_back(smp);
-    }
+    draw_to(gb);
     if (!have_next) {
-      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[j];
+      for (int j = 0; j < nb; j++) c->h_samples[j] = pending[f0 + j];
       HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * nb, hipMemcpyHostToDevice, c->stream));
     }
     // Pipelined BATCH rounds: the next round's samples are known now (BATCH rounds commit every
@@ -2360,30 +2498,29 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     // rollouts run (the rollout kernel's last waves leave most CUs idle); after the commit, the nodes
     // this round appended are searched and merged in (launch_nn_delta).  The lists equal a search over
     // the committed tree, so the rounds' results are unchanged.
+    int64_t gb2 = 0, f2 = 0;
     int nb2 = 0;
     NnSetup su{};
     if (!exact && c->nn_pipeline) {
-      nb2 = cur;
-      if (n_iters > 0) nb2 = (int)std::min<int64_t>(nb2, n_iters - st.iterations - nb);
+      gb2 = cur;
+      if (n_iters > 0) gb2 = std::max<int64_t>(0, std::min<int64_t>(gb2, n_iters - st.iterations - gb));
       if (n_iters == 0) {
         double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        if (!(ms + last_round_ms < budget_ms)) nb2 = 0;  // this is probably the last round
+        if (!(ms + last_round_ms < budget_ms)) gb2 = 0;  // this is probably the last round
       }
+      nb2 = (int)gb2;
+      if (sharded) shard_slice(c, gb2, &f2, &nb2);
       if (nb2 > 0) {
         su = nn_setup(c);
         if (!walk_serves(c, su)) nb2 = 0;
       }
     }
     auto prefetch = [&]() -> int {
-      while ((int64_t)pending.size() < (int64_t)nb + nb2) {
-        clrrt_sample smp;
-        clrrt_draw_samples(&c->params, &work, 1, &smp);
-        pending.push_back(smp);
-      }
-      for (int j = 0; j < nb2; j++) c->h_samples2[j] = pending[nb + j];
+      draw_to(gb + gb2);
+      for (int j = 0; j < nb2; j++) c->h_samples2[j] = pending[gb + f2 + j];
       return launch_side_walk(c, nb2, su);
     };
-    int L = nb, nn = 0;
+    int L = nb, nn = 0, n_app = 0;
     auto build = [&]() -> int { return pre_roll_build(c, su); };
     if ((rc = eval_samples(c, nb, exact, &L, have_next, nb2 > 0 ? std::function<int()>(prefetch) : nullptr,
                            nb2 > 0 ? std::function<int()>(build) : nullptr)) != CLRRT_OK)
@@ -2391,31 +2528,30 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     if (!exact) {
       // BATCH rounds commit every sample, so the next round's samples are known now: draw them
       // while the GPU evaluates this round (the draw is ~0.05 us per sample on the host)
-      int64_t want = nb + (int64_t)cur;
+      int64_t want = gb + (int64_t)cur;
       if (n_iters > 0) want = std::min<int64_t>(want, n_iters - st.iterations);
-      while ((int64_t)pending.size() < want) {
-        clrrt_sample smp;
-        clrrt_draw_samples(&c->params, &work, 1, &smp);
-        pending.push_back(smp);
-      }
+      draw_to(want);
     }
     if ((rc = compact_and_copy(c, L, &nn, true)) != CLRRT_OK) break;
     const int64_t first_new = c->n_nodes;
-    if ((rc = append_nodes(c, c->out_nodes, nn)) != CLRRT_OK) break;
+    const double ms_commit = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if ((rc = commit_round(c, nn, ms_commit, &n_app)) != CLRRT_OK) break;
     have_next = false;
     if (nb2 > 0) {
-      if ((rc = side_delta_launch(c, nb2, first_new, nn)) != CLRRT_OK) break;
+      if ((rc = side_delta_launch(c, nb2, first_new, n_app)) != CLRRT_OK) break;
       if (c->nnw_double && (rc = next_round_build(c)) != CLRRT_OK) break;
       if ((rc = side_lists_join(c)) != CLRRT_OK) break;
       have_next = true;
     }
-    for (int j = 0; j < L; j++) {
+    // iterations consumed: the committed prefix (EXACT) or the whole round (BATCH, every rank's samples)
+    const int64_t used = exact ? L : gb;
+    for (int64_t j = 0; j < used; j++) {
       pending.pop_front();
       for (int k = 0; k < 3; k++) clrrt_rng_next(&committed);
     }
-    st.iterations += L;
+    st.iterations += used;
     st.goal_nodes_added += c->last_goal_nodes;
-    st.speculated += nb;
+    st.speculated += exact ? nb : gb;
     st.rounds++;
     if (exact) cur = std::max(c->exact_min_width, std::min(batch, L == nb ? 2 * nb : 2 * L));
     last_round_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
@@ -2426,6 +2562,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   st.deferred = c->def.deferred_total;
   if (rc == CLRRT_OK) rc = flush_replays(c);
   c->def.active = false;
+  if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->stream));
   st.nodes_added = c->n_nodes - nodes_before;
@@ -2433,6 +2570,23 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   *rng = committed;
   if (out) *out = st;
   return rc;
+}
+
+int clrrt_set_shards(clrrt_ctx* c, int32_t rank, int32_t world, void* dev_local, int32_t cap_local,
+                     clrrt_exchange_fn exchange, void* user) {
+  if (!c || world < 1 || rank < 0 || rank >= world) return CLRRT_EINVAL;
+  if (world > 1 && (!dev_local || cap_local <= 0 || !exchange)) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  auto& h = c->sh;
+  h.rank = rank;
+  h.world = world;
+  h.dev_local = world > 1 ? dev_local : nullptr;
+  h.cap_local = world > 1 ? cap_local : 0;
+  h.fn = world > 1 ? exchange : nullptr;
+  h.user = world > 1 ? user : nullptr;
+  c->rank = rank;  // owner of this rank's records
+  if (world > 1 && !h.d_goal) HIPC(c, dalloc(&h.d_goal, 1));
+  return CLRRT_OK;
 }
 
 int clrrt_rollout_batch(clrrt_ctx* c, const clrrt_rollout_job* jobs, int32_t n, clrrt_rollout_result* out,

@@ -267,9 +267,17 @@ size_t compact_scan_bytes(int n);
 size_t defer_select_bytes(int n);
 hipError_t launch_defer_select(hipStream_t st, const int* gv, const uint8_t* pend, int n, int* out, int* n_out,
                                void* tmp, size_t tmp_bytes);
+// tag_R > 0 (sharded rounds with deferred samples): each record's age in rounds relative to ring slot
+// tag_slot (ring of tag_R slots of tag_B samples) in bits 8..15 of its goal field
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
-                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb);
+                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb, int tag_slot = 0,
+                          int tag_R = 0, int tag_B = 1);
+// The exchanged records (sort: by age tag, stable) into out in commit order, tags cleared; goal flags
+// counted into *goal.  keys: [4 n] scratch.
+size_t xorder_sort_bytes(int n);
+hipError_t launch_xorder(hipStream_t st, const clrrt_node* recs, int n, bool sort, uint32_t* keys, void* tmp,
+                         size_t tmp_bytes, clrrt_node* out, unsigned long long* goal);
 // Bounding box (x0, y0, x1, y1) of the finite positions of recs[0 .. n), n = *n_dev when non-null.
 hipError_t launch_bbox(hipStream_t st, const clrrt_node* recs, const int64_t* n_dev, int n_host, double* out4);
 hipError_t launch_append(hipStream_t st, const clrrt_node* in, int n, int64_t base, clrrt_node* tree, NnRec* nn);

@@ -1880,7 +1880,8 @@ __global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut*
                                                          const uint64_t* __restrict__ packed,
                                                          const uint64_t* __restrict__ scanned, int64_t row_base,
                                                          int rank, clrrt_node* __restrict__ out, Job* __restrict__ jobs,
-                                                         int64_t* __restrict__ totals) {
+                                                         int64_t* __restrict__ totals, int tag_slot, int tag_R,
+                                                         int tag_B) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= L) return;
   const uint64_t off = scanned[s];
@@ -1891,8 +1892,12 @@ __global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut*
     totals[1] = (int64_t)(tot >> 24);
   }
   const SampleOut& o = so[s];
+  // sharded rounds with deferred samples: the record's age in rounds (0: this round's sample) rides in
+  // bits 8..15 of `goal` through the exchange, which orders the union oldest round first (k_xorder_keys)
+  const int tag = tag_R > 0 ? ((tag_slot - o.g / tag_B + tag_R) % tag_R) << 8 : 0;
   if (o.k >= 0) {
     clrrt_node n = regnodes[s];
+    n.goal |= tag;
     n.owner = rank;
     n.row_offset = row_base + row_off;
     out[node_off] = n;
@@ -1906,6 +1911,7 @@ __global__ void __launch_bounds__(256) k_compact_scatter(int L, const SampleOut*
   }
   if (o.gb_ok) {
     clrrt_node n = gbnodes[s];
+    n.goal |= tag;
     n.owner = rank;
     n.row_offset = row_base + row_off;
     out[node_off] = n;
@@ -2730,9 +2736,62 @@ size_t compact_scan_bytes(int n) {
   return bytes;
 }
 
+// Sharded rounds (clrrt_set_shards) with deferred samples: the exchanged union of every rank's records (each
+// rank's in (age desc, sample) order, ranks holding contiguous slices) into the global commit order, the
+// oldest round first, by a stable sort on the age tag; the tag is cleared.  The appended records' goal
+// flags are counted into *goal.
+__global__ void k_xorder_keys(const clrrt_node* __restrict__ recs, int n, uint32_t* __restrict__ keys,
+                              uint32_t* __restrict__ idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = 255u - (((uint32_t)recs[i].goal >> 8) & 0xffu);
+  idx[i] = (uint32_t)i;
+}
+__global__ void k_xgather(const clrrt_node* __restrict__ recs, const uint32_t* __restrict__ idx, int n,
+                          clrrt_node* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  clrrt_node r = recs[idx ? idx[i] : i];
+  r.goal &= 0xff;
+  out[i] = r;
+}
+__global__ void k_goal_count(const clrrt_node* __restrict__ recs, int n, unsigned long long* goal) {
+  unsigned long long c = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) c += recs[i].goal & 1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(goal, c);
+}
+size_t xorder_sort_bytes(int n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, 8);
+  return bytes;
+}
+hipError_t launch_xorder(hipStream_t st, const clrrt_node* recs, int n, bool sort, uint32_t* keys, void* tmp,
+                         size_t tmp_bytes, clrrt_node* out, unsigned long long* goal) {
+  if (n <= 0) return hipSuccess;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  uint32_t* idx = nullptr;
+  if (sort) {
+    hipLaunchKernelGGL(k_xorder_keys, dim3(g), dim3(256), 0, st, recs, n, keys, keys + n);
+    LAUNCH_CHECK();
+    size_t bytes = tmp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, keys + 2 * n, keys + n, keys + 3 * n, n, 0, 8, st);
+    if (e != hipSuccess) return e;
+    idx = keys + 3 * n;
+  }
+  hipLaunchKernelGGL(k_xgather, dim3(g), dim3(256), 0, st, recs, idx, n, out);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_goal_count, dim3(g < 1024 ? g : 1024), dim3(256), 0, st, out, n, goal);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
-                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb) {
+                          clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb, int tag_slot, int tag_R,
+                          int tag_B) {
   hipError_t e = hipMemsetAsync(totals, 0, sizeof(int64_t) * 8, st);
   if (e != hipSuccess) return e;
   if (L <= 0) return hipSuccess;
@@ -2742,7 +2801,7 @@ hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const in
   e = hipcub::DeviceScan::ExclusiveSum(cb.tmp, bytes, cb.packed, cb.scanned, L, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_compact_scatter, dim3((L + 255) / 256), dim3(256), 0, st, L, so, reg, gbn, cb.packed, cb.scanned,
-                     row_base, rank, out, jobs, totals);
+                     row_base, rank, out, jobs, totals, tag_slot, tag_R, tag_B);
   LAUNCH_CHECK();
   return hipSuccess;
 }

@@ -279,6 +279,23 @@ int clrrt_path_mpc_message(clrrt_ctx* ctx, int32_t filtered, double* out, int32_
 int clrrt_expand(clrrt_ctx* ctx, clrrt_rng* rng, int64_t n_iters, double budget_ms, int32_t mode,
                  int32_t batch, clrrt_stats* out);
 
+/* ---- multi-GPU expansion (engine extension, no reference counterpart) ----
+ * With world > 1, clrrt_expand in BATCH mode runs sharded rounds: `batch` is the GLOBAL number of samples
+ * per round (all drawn from the one glibc stream, as the reference's loop draws them); this rank evaluates
+ * the contiguous slice [batch*rank/world, batch*(rank+1)/world) against the replicated tree, writes its
+ * accepted-node records (clrrt_node, owner = rank, rows in this rank's arena) to dev_local, and calls
+ * `exchange` once per round, which must return in *dev_all the records of every rank concatenated in
+ * rank order (device memory, valid until the next call; a collective such as one all-gather over RCCL) and
+ * in *n_all their count, and in *max_elapsed_ms the largest `elapsed_ms` over the ranks -- the budget is
+ * checked against it, so every rank runs the same rounds.  Every rank then appends the same records in
+ * the same order (deferred samples: the oldest round first), so the trees stay identical.  The caller
+ * chooses weak scaling (batch = world x per-GPU samples) or strong scaling (batch fixed).  world = 1 turns
+ * sharding off.  dev_local holds cap_local records (>= 2 x the slice, + the deferred samples). */
+typedef int32_t (*clrrt_exchange_fn)(void* user, int32_t n_local, double elapsed_ms, void** dev_all,
+                                     int32_t* n_all, double* max_elapsed_ms);
+int clrrt_set_shards(clrrt_ctx* ctx, int32_t rank, int32_t world, void* dev_local, int32_t cap_local,
+                     clrrt_exchange_fn exchange, void* user);
+
 /* Evaluate `n` samples (host array) against the current tree; accepted nodes (regular and
  * goal-biased, in sample order) are written compacted to `dev_out` (device pointer, capacity
  * 2*n records) with row_offset local to this context's arena and owner = this rank.

@@ -115,3 +115,75 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
         assert np.array_equal(r["prow"].view(np.uint64), prow.view(np.uint64))
     assert sum(int(r["moved"]) for r in ranks) > 0  # the path crossed ranks
     pl.close()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# The engine's own sharded rounds (clrrt_set_shards + clrrt.dist.ShardExchange): clrrt_expand runs every round
+# on each rank -- its slice of the samples, the lag-1 / lag-2 pipelines, deferred samples -- and the exchange
+# hook all-gathers the records; the same code path as one GPU.
+SHARD_CASES = [  # (samples per round over both ranks, defer_steps, nn_lag, rounds)
+    (2 * B, 0, 1, 4),
+    (2 * B, 64, 2, 6),
+    (2 * B - 7, 48, 1, 4),   # uneven slices (shard_slice), deferred samples
+]
+
+
+def _shard_worker(rank, port, out_dir, G, T, lag, rounds):
+    sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    import clrrt
+    from clrrt import dist as cdist
+    pl = _planner()
+    pl.set_option("defer_steps", T)
+    pl.set_option("nn_lag", lag)
+    pl.set_stream(torch.cuda.current_stream().cuda_stream)
+    ex = cdist.ShardExchange(pl, cdist.exchange_capacity(B, T), "cuda", first_bound=256)
+    st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
+    raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
+    g = pl.nodes()
+    own = np.nonzero(g["owner"] == rank)[0]
+    rows = [pl.rows(int(g["row_offset"][i]), int(g["nrows"][i])) for i in own]
+    np.savez(os.path.join(out_dir, f"shard{rank}.npz"), hdr=raw[:, :HDR], own=own,
+             rows=np.concatenate(rows) if rows else np.zeros((0, 10)), rounds=st["rounds"], it=st["iterations"],
+             goals=st["goal_nodes_added"], deferred=st["deferred"], ex_rounds=ex.rounds)
+    dist.barrier()
+    dist.destroy_process_group()
+    pl.close()
+
+
+@pytest.mark.parametrize("G,T,lag,rounds", SHARD_CASES)
+def test_sharded_expand_matches_single_process(tmp_path, G, T, lag, rounds):
+    """Two ranks sharing GPU 0 run clrrt_expand with the exchange hook; both trees equal ONE process expanding
+    the same stream with G samples per round (same defer_steps): headers bit for bit, every node's rows on
+    its owner, the iteration count and the goal nodes appended (every rank's)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path), G, T, lag, rounds), nprocs=WORLD, join=True)
+    import clrrt
+    pl = _planner()
+    pl.set_option("defer_steps", T)
+    pl.set_option("nn_lag", lag)
+    st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
+    assert st["rounds"] == rounds and (T == 0 or st["deferred"] > 0), st
+    ref_raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
+    g = pl.nodes()
+    ranks = [np.load(tmp_path / f"shard{r}.npz") for r in range(WORLD)]
+    print(f"sharded G={G} T={T} lag {lag}: {ref_raw.shape[0]} nodes; owned {[len(r['own']) for r in ranks]}; "
+          f"deferred {[int(r['deferred']) for r in ranks]} (single {st['deferred']}); exchanges "
+          f"{[int(r['ex_rounds']) for r in ranks]}")
+    assert ref_raw.shape[0] > 2000
+    for r in ranks:
+        assert np.array_equal(r["hdr"], ref_raw[:, :HDR])
+        assert int(r["rounds"]) == rounds and int(r["it"]) == rounds * G
+        assert int(r["goals"]) == st["goal_nodes_added"]
+    assert sum(int(r["deferred"]) for r in ranks) == st["deferred"]
+    assert sum(len(r["own"]) for r in ranks) == ref_raw.shape[0]
+    for rk, r in enumerate(ranks):
+        want = [pl.rows(int(g["row_offset"][i]), int(g["nrows"][i])) for i in r["own"]]
+        want = np.concatenate(want) if want else np.zeros((0, 10))
+        assert np.array_equal(r["rows"].view(np.uint64), want.view(np.uint64)), rk
+    pl.close()
