@@ -25,8 +25,10 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "clrrt.h")
 
 _lib = None
 P = C.POINTER
-# clrrt_exchange_fn (include/clrrt.h): (user, n_local, elapsed_ms, *dev_all, *n_all, *max_elapsed_ms) -> status
-EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_double, P(C.c_void_p), P(C.c_int32), P(C.c_double))
+# clrrt_exchange_fn (include/clrrt.h): (user, n_local, elapsed_ms, aux_local, *dev_all, *n_all, *max_elapsed_ms,
+# *aux_sum) -> status
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_double, C.c_int64, P(C.c_void_p), P(C.c_int32),
+                          P(C.c_double), P(C.c_int64))
 
 _SIGS = {
     "clrrt_abi_version": (C.c_int, []),
@@ -101,6 +103,8 @@ def lib():
                              "(or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("CLRRT_ABI_ANY") and not hasattr(L, name):  # (bisection builds)
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

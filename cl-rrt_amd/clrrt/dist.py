@@ -16,7 +16,8 @@ GOAL_OFFSET = 140  # clrrt_node.goal (int32)
 class RoundExchange:
     """All-gather of one round's accepted-node records, count-prefixed.
 
-    Row 0 of `buf` is a header (int64 record count, float64 elapsed query ms); clrrt_round_eval writes
+    Row 0 of `buf` is a header (int64 record count, float64 elapsed query ms, int64 aux value summed over the
+    ranks); clrrt_round_eval writes
     this rank's records from row 1 on (`records_ptr`).  One all-gather moves header + the first `bound`
     record rows of every rank, so no count exchange (and no host sync) precedes the data; the headers
     are read back once afterwards.  `bound` adapts to 1.25x the largest count seen; a round whose count
@@ -24,7 +25,7 @@ class RoundExchange:
     stages device buffers through the host.
     """
 
-    HDR = 16
+    HDR = 24
 
     def __init__(self, cap_records, device, group=None, first_bound=1024):
         self.group = group
@@ -50,18 +51,21 @@ class RoundExchange:
         dist.all_gather(parts, src, group=self.group)
         return parts
 
-    def exchange(self, n_local, elapsed_ms):
+    def exchange(self, n_local, elapsed_ms, aux=0):
         """Returns (records (total, 160) uint8 on the buffer's device in global sample order, counts
-        per rank, first row of this rank's records, max elapsed ms over ranks)."""
+        per rank, first row of this rank's records, max elapsed ms over ranks); the sum of `aux` over the
+        ranks is left in self.aux_sum."""
         import numpy as np
-        hdr = np.zeros(2, dtype=np.float64)
+        hdr = np.zeros(3, dtype=np.float64)
         hdr.view(np.int64)[0] = int(n_local)
         hdr[1] = float(elapsed_ms)
+        hdr.view(np.int64)[2] = int(aux)
         self.buf[0, :self.HDR].copy_(torch.from_numpy(hdr.view(np.uint8)))
         parts = self._gather(self.buf[:self.bound + 1])
         heads = torch.stack([q[0, :self.HDR] for q in parts]).cpu().numpy()
         counts = [int(c) for c in heads[:, :8].copy().view(np.int64)[:, 0]]
-        t_max = float(heads[:, 8:].copy().view(np.float64).max())
+        t_max = float(heads[:, 8:16].copy().view(np.float64).max())
+        self.aux_sum = int(heads[:, 16:24].copy().view(np.int64).sum())
         maxc = max(counts)
         extra = None
         if maxc > self.bound:
@@ -99,13 +103,14 @@ class ShardExchange:
         self._keep = None
         self.rounds = 0
 
-        def cb(user, n_local, elapsed_ms, dev_all, n_all, max_ms):
+        def cb(user, n_local, elapsed_ms, aux, dev_all, n_all, max_ms, aux_sum):
             try:
-                cat, counts, _, t_max = self.rx.exchange(n_local, elapsed_ms)
+                cat, counts, _, t_max = self.rx.exchange(n_local, elapsed_ms, aux)
                 self._keep = cat  # the engine reads it (stream-ordered) before the next exchange
                 dev_all[0] = ctypes.c_void_p(cat.data_ptr() if cat.shape[0] else None).value
                 n_all[0] = int(cat.shape[0])
                 max_ms[0] = float(t_max)
+                aux_sum[0] = self.rx.aux_sum
                 self.rounds += 1
                 return 0
             except Exception:  # reported to the engine, which returns CLRRT_EHIP

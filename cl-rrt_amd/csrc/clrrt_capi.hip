@@ -233,6 +233,9 @@ struct clrrt_ctx {
     clrrt_exchange_fn fn = nullptr;
     void* user = nullptr;
     double max_ms = 0;             // largest elapsed query time over the ranks at the last exchange
+    int64_t nd_global = 0;         // deferred samples pending on all ranks after the last exchange
+    int64_t rows_stop = 0;         // ranks whose arena cannot take another round (the same stop everywhere)
+    int last_nb = 0;               // this rank's slice of the last round
     clrrt_node* xbuf = nullptr;    // the exchanged records in commit order (deferred samples: by age)
     uint32_t* xkey = nullptr;      // [2 xcap] sort keys (age), [2 xcap] record indices
     void* xtmp = nullptr;
@@ -262,6 +265,7 @@ struct clrrt_ctx {
 static void pf_reset(clrrt_ctx* c);
 static int flush_replays(clrrt_ctx* c);
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n);
+static int watchdog_check(clrrt_ctx* c);
 static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped);
 static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app);
 static int ensure_slots(clrrt_ctx* c);
@@ -1633,10 +1637,45 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
     }
+    static unsigned long long* dbg_host = nullptr;  // diagnostics heartbeat (host-mapped)
+    if (getenv("CLRRT_DEBUG_SYNC")) {  // diagnostics: which kernel of the round does not finish
+      if (!dbg_host) HIPC(c, hipHostMalloc((void**)&dbg_host, sizeof(unsigned long long) * 8 * 4096, hipHostMallocMapped));
+      memset(dbg_host, 0, sizeof(unsigned long long) * 8 * 4096);
+      HIPC(c, hipHostGetDevicePointer((void**)&a.dbg, dbg_host, 0));
+      HIPC(c, hipStreamSynchronize(rst));
+      fprintf(stderr, "[dbg] pre-rollout work done (n %d, nrep %d, ncarry %d)\n", n, a.nrep, a.ncarry);
+    }
     if (persistent)
       HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, defer ? c->def.best : c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
+    if (getenv("CLRRT_DEBUG_SYNC")) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hipStreamQuery(rst) == hipErrorNotReady) {
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 10.0) {
+          fprintf(stderr, "[dbg] rollout kernel not done after 10 s; waves (iterations, busy, parked, qdone|first "
+                          "busy lane, j|pass, steps|chain, wp|N, t):\n");
+          unsigned long long tmax = 0;
+          for (int w = 0; w < 4096; w++) tmax = std::max(tmax, dbg_host[w * 8 + 7]);
+          int shown = 0;
+          for (int w = 0; w < 4096 && shown < 40; w++) {
+            const unsigned long long* d = dbg_host + w * 8;
+            if (d[7] == 0 || tmax - d[7] < 100000000ull) continue;  // still beating in the last second
+            if (d[1] == 0 && d[2] == 0 && (d[3] >> 32)) continue;      // finished
+            fprintf(stderr, "  wave %d: it %llu busy %016llx parked %016llx qdone %llu lane %d j %d pass %d steps %d "
+                            "chain %d wp %d N %d age %.3f s\n", w, d[0], d[1], d[2], d[3] >> 32, (int)(uint32_t)d[3],
+                    (int)(d[4] >> 32), (int)(uint32_t)d[4], (int)(d[5] >> 32), (int)(uint32_t)d[5], (int)(d[6] >> 32),
+                    (int)(uint32_t)d[6], (double)(tmax - d[7]) * 1e-8);
+            shown++;
+          }
+          int alive = 0;
+          for (int w = 0; w < 4096; w++) alive += dbg_host[w * 8 + 7] != 0 && tmax - dbg_host[w * 8 + 7] < 100000000ull;
+          fprintf(stderr, "  waves still beating: %d\n", alive);
+          abort();
+        }
+      }
+      fprintf(stderr, "[dbg] rollout kernel done: %s\n", hipGetErrorString(hipStreamQuery(rst)));
+    }
     if (deferred) c->rep_n = 0;
     c->eval_deferred = deferred;
   }
@@ -1655,6 +1694,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
   if (defer) {  // views: the deferred samples of earlier rounds, then this round's
     auto& d = c->def;
     s.cand = d.cand; s.ncand = d.ncand; s.res = d.res; s.res_gb = d.res_gb;
+    s.ckey = nullptr;  // the round's keys are not in the rings (EXACT's conflict threshold only)
     s.view = d.dlist[d.cur_dl];
     s.nd = d.nd;
     s.sbase = d.slot * (int)c->cap.max_batch;
@@ -1708,6 +1748,10 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
     HIPC(c, hipMemcpyAsync(c->h_int + 2, (const char*)(c->work_ctr + 62), sizeof(int), hipMemcpyDeviceToHost, st));
   }
   HIPC(c, hipStreamSynchronize(st));
+  {
+    const int rw = watchdog_check(c);
+    if (rw != CLRRT_OK) return rw;
+  }
   if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   if (defer) {
     if (c->h_int[2] != 0 || c->h_int[1] > d.carry_cap)
@@ -1853,6 +1897,19 @@ static int ensure_slots(clrrt_ctx* c) {
   return CLRRT_OK;
 }
 
+// k_roll_run's watchdog (work counters 56..59): a wave that loops far past any correct launch exits and
+// records its state; reported as an error.
+static int watchdog_check(clrrt_ctx* c) {
+  unsigned long long h[4];
+  HIPC(c, hipMemcpy(h, c->work_ctr + 56, sizeof(h), hipMemcpyDeviceToHost));
+  if (h[0] == 0) return CLRRT_OK;
+  char msg[256];
+  snprintf(msg, sizeof(msg), "rollout kernel watchdog: %llu waves; j %d fin %d steps %d chain %d qdone %d busy %d",
+           h[0], (int)(h[1] >> 32), (int)(uint32_t)h[1], (int)(h[2] >> 32), (int)(uint32_t)h[2], (int)(h[3] >> 32),
+           (int)(uint32_t)h[3]);
+  return fail(c, CLRRT_EHIP, msg);
+}
+
 // Every replay must run exactly as many steps as its committed node has rows (k_roll_run counts the
 // ones that do not in work counter 61 and stores no row past the node's count).  Nonzero means the
 // arena's rows are not the committed rollouts': reported as an error instead of a silently wrong tree.
@@ -1861,7 +1918,7 @@ static int replay_check(clrrt_ctx* c) {
                          c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   if (c->h_int[2] != 0) return fail(c, CLRRT_EHIP, "a deferred-row replay diverged from its committed rollout");
-  return CLRRT_OK;
+  return watchdog_check(c);
 }
 
 // Run the pending replays (the last commit's accepted rollouts, deferred rows) on their own: before
@@ -1911,7 +1968,7 @@ static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
     if (d.nd > 0 || sharded) {
       SelArgs s;
       memset(&s, 0, sizeof(s));
-      s.p = c->dp; s.tree = c->tree; s.cand = d.cand; s.ckey = c->ckey; s.ncand = d.ncand; s.res = d.res;
+      s.p = c->dp; s.tree = c->tree; s.cand = d.cand; s.ckey = nullptr; s.ncand = d.ncand; s.res = d.res;
       s.res_gb = d.res_gb; s.regnodes = c->regnodes; s.gbnodes = c->gbnodes; s.so = c->so;
       s.view = d.dlist[d.cur_dl]; s.nd = d.nd; s.sbase = 0; s.gv = d.gv; s.pend = d.pend; s.B = d.nd;
       if (d.nd > 0) {
@@ -2065,9 +2122,18 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
   void* all = nullptr;
   int32_t n_all = 0;
   double mx = elapsed_ms;
-  if (h.fn(h.user, nn, elapsed_ms, &all, &n_all, &mx) != 0 || n_all < 0 || (n_all > 0 && !all))
+  // aux: this rank's pending deferred samples (low 32 bits) and whether its arena can take another round of
+  // its slice (+ its deferred samples) -- summed over the ranks, so every rank takes the same stop decision
+  const int64_t nd_loc = c->def.active ? c->def.nd : 0;
+  const bool rows_full =
+      c->n_rows + nn + 2 * ((int64_t)h.last_nb + nd_loc) * (c->dp.n_steps_max + 1) > c->cap.max_rows;
+  const int64_t aux = nd_loc + (rows_full ? (1ll << 32) : 0);
+  int64_t aux_sum = aux;
+  if (h.fn(h.user, nn, elapsed_ms, aux, &all, &n_all, &mx, &aux_sum) != 0 || n_all < 0 || (n_all > 0 && !all))
     return fail(c, CLRRT_EHIP, "the exchange of the round's records failed");
   h.max_ms = mx;
+  h.nd_global = aux_sum & 0xffffffffll;
+  h.rows_stop = aux_sum >> 32;
   if (n_all > 0) {
     if (n_all > h.xcap) {
       HIPC(c, hipStreamSynchronize(c->stream));
@@ -2192,6 +2258,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   const int cur = batch;  // samples per round, all ranks
   const bool sharded = c->sh.world > 1;
   c->sh.max_ms = 0;
+  c->sh.nd_global = 0;
+  c->sh.rows_stop = 0;
   if (sharded && (rc = shard_goal_reset(c)) != CLRRT_OK) return rc;
   const int64_t nodes_before = c->n_nodes;
   hipStream_t sides[2] = {c->side, c->side2};
@@ -2285,11 +2353,12 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     int64_t f0 = 0;
     int nb = (int)gb;
     if (sharded) shard_slice(c, gb, &f0, &nb);
+    c->sh.last_nb = nb;
     // (a commit also takes the deferred samples that resolve; sharded, the stop decision must be the same
     // on every rank: node counts only, the deferred samples bounded by the ring's rounds)
-    const int64_t nc = sharded ? gb * std::max(1, c->def.active ? c->def.R : 1) : gb + (int64_t)c->def.nd;
+    const int64_t nc = gb + (sharded ? c->sh.nd_global : (int64_t)c->def.nd);
     if (c->n_nodes + 2 * nc > c->cap.max_nodes ||
-        (!sharded && c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
+        (sharded ? c->sh.rows_stop > 0 : c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;
@@ -2455,6 +2524,8 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   int64_t nodes_before = c->n_nodes;
   int rc = defer_begin(c, !exact);
   c->sh.max_ms = 0;
+  c->sh.nd_global = 0;
+  c->sh.rows_stop = 0;
   if (rc == CLRRT_OK && sharded) rc = shard_goal_reset(c);
   bool have_next = false;  // this round's samples and lists were prepared by the previous round
   double last_round_ms = 0;
@@ -2479,11 +2550,12 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
     int64_t f0 = 0;
     int nb = (int)gb;
     if (sharded) shard_slice(c, gb, &f0, &nb);
+    c->sh.last_nb = nb;
     // a round appends at most 2 nodes and 2 full-horizon trajectories per sample (+ the deferred samples;
     // sharded, the same decision on every rank: node counts only, deferred samples bounded by the ring)
-    const int64_t nc = sharded ? gb * std::max(1, c->def.active ? c->def.R : 1) : gb + (int64_t)c->def.nd;
+    const int64_t nc = gb + (sharded ? c->sh.nd_global : (int64_t)c->def.nd);
     if (c->n_nodes + 2 * nc > c->cap.max_nodes ||
-        (!sharded && c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
+        (sharded ? c->sh.rows_stop > 0 : c->n_rows + 2 * nc * (c->dp.n_steps_max + 1) > c->cap.max_rows)) {
       if (n_iters > 0) { rc = fail(c, CLRRT_ECAPACITY, "tree capacity exhausted"); break; }
       st.capacity_stop = 1;
       break;

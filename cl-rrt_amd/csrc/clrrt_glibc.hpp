@@ -699,5 +699,76 @@ CLRRT_HD inline __attribute__((always_inline)) double atan2(double y, double x) 
   return copysign_(z, y);
 }
 
+// exp (sysdeps/ieee754/dbl-64/e_exp.c, glibc 2.35, as its FMA ifunc variant __exp_fma evaluates it): x =
+// k ln2/128 + r, exp(x) = 2^(k/128) exp(r) with 2^(k/128) = scale (1 + tail) from __exp_data.tab and a degree-5
+// polynomial; the FMA build contracts the reduction, the polynomial and the final scale + scale * tmp, not the
+// out-of-line specialcase (|x| >= 512).  Checked against the host libm bit for bit on 4e7 arguments
+// (development check) and on the device by tests/test_gpu_math.py.  Used by the W2 obstacle-cost term
+// Wcost[2] exp(-Wcost[3] Dobs) (simulation.cpp:91, rrtplanner.cpp:112).
+#if defined(__HIPCC__)
+static __device__ __constant__ uint64_t d_exp_tab[256] = CLRRT_GLIBC_EXP_TAB;
+#endif
+static const uint64_t h_exp_tab[256] = CLRRT_GLIBC_EXP_TAB;
+CLRRT_HD inline double from_bits(uint64_t u) {
+  double r;
+  memcpy(&r, &u, 8);
+  return r;
+}
+CLRRT_HD inline uint64_t exp_tab(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return d_exp_tab[i];
+#else
+  return h_exp_tab[i];
+#endif
+}
+CLRRT_HD inline double exp_specialcase(double tmp, uint64_t sbits, uint64_t ki) {
+  double scale, y;
+  if ((ki & 0x80000000) == 0) {  // k > 0: the exponent of scale might have overflowed by <= 460
+    sbits -= 1009ull << 52;
+    scale = from_bits(sbits);
+    y = 0x1p1009 * (scale + scale * tmp);
+    return y;
+  }
+  // k < 0: the result may be subnormal; avoid double rounding
+  sbits += 1022ull << 52;
+  scale = from_bits(sbits);
+  y = scale + scale * tmp;
+  if (y < 1.0) {
+    double lo = scale - y + scale * tmp;
+    const double hi = 1.0 + y;
+    lo = 1.0 - hi + y + lo;
+    y = (hi + lo) - 1.0;
+    if (y == 0) y = 0.0;  // -0 -> +0
+  }
+  return 0x1p-1022 * y;
+}
+CLRRT_HD inline double exp(double x) {
+  uint32_t abstop = (uint32_t)(bits(x) >> 52) & 0x7ff;
+  const uint32_t t_tiny = 0x3c9, t_512 = 0x408, t_1024 = 0x409;  // top12 of 2^-54, 512, 1024
+  if (abstop - t_tiny >= t_512 - t_tiny) {
+    if ((int32_t)(abstop - t_tiny) < 0) return 1.0 + x;  // tiny x (0 included)
+    if (abstop >= t_1024) {
+      if (bits(x) == 0xfff0000000000000ull) return 0.0;  // -inf
+      if (abstop >= 0x7ff) return 1.0 + x;               // +inf, NaN
+      return (bits(x) >> 63) ? 0.0 : from_bits(0x7ff0000000000000ull);  // underflow / overflow
+    }
+    abstop = 0;  // large |x|: specialcase below
+  }
+  const double z = exp_invln2N * x;
+  double kd = z + exp_shift;
+  const uint64_t ki = bits(kd);
+  kd -= exp_shift;
+  const double r = fma_(kd, exp_negln2loN, fma_(kd, exp_negln2hiN, x));
+  const int idx = 2 * (int)(ki % 128);
+  const uint64_t top = ki << 45;
+  const double tail = from_bits(exp_tab(idx));
+  const uint64_t sbits = exp_tab(idx + 1) + top;
+  const double r2 = r * r;
+  const double tmp = fma_(r2 * r2, fma_(r, exp_C5, exp_C4), fma_(r2, fma_(r, exp_C3, exp_C2), tail + r));
+  if (abstop == 0) return exp_specialcase(tmp, sbits, ki);
+  const double scale = from_bits(sbits);
+  return fma_(scale, tmp, scale);
+}
+
 }  // namespace glibc
 }  // namespace clrrt

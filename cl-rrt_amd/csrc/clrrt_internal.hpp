@@ -131,6 +131,7 @@ struct RollArgs {
   int* ncarry_out;
   int carry_cap;
   int jbase, sbase;
+  unsigned long long* dbg;  // diagnostics (CLRRT_DEBUG_SYNC): per-wave heartbeat in host-mapped memory, or null
 };
 
 // k_select over B "views": view v < nd is the still unresolved sample view[v] of an earlier round (deferred

@@ -864,7 +864,7 @@ __device__ __forceinline__ int roll_step_post(Roll& r, const DevParams& p, doubl
   r.costE += r.x4 * p.dt;
   double kappa = r.t3 / p.L;
   double term = p.W0 * r.x4 * p.dt + p.W1 * fabs(kappa);
-  if (p.use_exp) term = term + p.W2 * exp(-p.W3 * Dobs);
+  if (p.use_exp) term = term + p.W2 * glibc::exp(-p.W3 * Dobs);  // glibc's exp, restated
   r.costS += term;
   if (p.bend) r.costS += p.W4 * dist_to_lane(r.x0, r.x1, p.lane_shift0, p.Cxy1, p.Cxy2);
   // lateral acceleration limit (simulation.cpp:98-104)
@@ -1373,9 +1373,12 @@ __global__ void __launch_bounds__(256) k_roll_flag(RollArgs a) {
 #ifndef CLRRT_ROLL_WAVES
 #define CLRRT_ROLL_WAVES 1
 #endif
+constexpr int kFinSuspend = 1000;  // k_roll_run: `fin` of a lane whose chain reached its cap (defer_steps)
 // COOP: the collision check is obs_distance_coop (OBB collision without the gap value, static grid built,
 // the per-wave LDS scratch after the obstacle tables at a.coop_off)
-template <bool NEED_GAP, bool COOP>
+// CARRY: the launch resumes / suspends chains (deferred samples, option defer_steps); the instantiation without
+// it has none of that code (the step loop's register allocation is that of the plain kernel)
+template <bool NEED_GAP, bool COOP, bool CARRY>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_ROLL_WAVES))) k_roll_run(RollArgs a,
                                                   int* __restrict__ qnext, int* __restrict__ best, int B) {
   extern __shared__ float4 lds[];
@@ -1408,7 +1411,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   const Carry* __restrict__ cin = (const Carry*)a.carry_in;
   Carry* __restrict__ cout = (Carry*)a.carry_out;
   // queue: the suspended chains of the previous launch, the replays, then the round's jobs
-  const int nq = a.ncarry + a.nrep + a.njobs;
+  const int ncarry = CARRY ? a.ncarry : 0;
+  const int nq = ncarry + a.nrep + a.njobs;
   double* rows = nullptr;
   bool rp = false;
   int nrows_rp = 0;
@@ -1444,6 +1448,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   // idle lanes, so the long divergent end-of-rollout code runs once per batch instead of almost
   // every step for one or two lanes.
   auto finish_parked = [&]() {
+    if (CARRY && fin == kFinSuspend) {  // a chain at its cap: suspended into carry_out, resumed by the next launch
+      const int slot_c = atomicAdd(a.ncarry_out, 1);
+      if (slot_c < a.carry_cap) {
+        Carry& co = cout[slot_c];
+        co.r = r;
+        co.c7 = c7; co.c8 = c8; co.c9 = c9;
+        co.row_off = rows ? (int64_t)((rows - a.arena) / 10) : -1;
+        co.j = j; co.bs = bs; co.k = k; co.pass = pass; co.steps = steps; co.chain = chain;
+        co.rp = rp ? 1 : 0;
+        co.nrows_rp = nrows_rp;
+        if (!rp) {  // the sample's result waits for this rollout (k_select: pending)
+          if (pass == 0) a.res[j].outcome = CLRRT_ROLL_PENDING;
+          else a.res_gb[j].outcome = CLRRT_ROLL_PENDING;
+        }
+      } else if (a.ctr) {  // no carry slot left: reported by the host (the round is void)
+        atomicAdd(&a.ctr[62], 1ull);
+      }
+      rp = false;
+      rows = nullptr;
+      j = -1;
+      fin = -1;
+    }
     if (fin >= 0) {
       if (rp) {  // a replay: its rows are written; check it ran as long as the committed rollout
         n_rep++;
@@ -1495,10 +1521,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       iq = false;
     }
   };
+  // watchdog: every wave reaches an exit even if something goes wrong (a step always advances, so no
+  // correct launch comes near the bound); a trip is counted and reported by the host
+  uint32_t guard = 0;
+  const uint64_t t_guard = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
   for (;;) {
+    if ((++guard & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t_guard > 300000000ull) {  // 3 s
+      if (a.ctr && lane == 0) {
+        atomicAdd(&a.ctr[56], 1ull);
+        atomicMax(&a.ctr[57], (unsigned long long)(((uint64_t)(uint32_t)j << 32) | (uint32_t)fin));
+        atomicMax(&a.ctr[58], (unsigned long long)(((uint64_t)(uint32_t)steps << 32) | (uint32_t)chain));
+        atomicMax(&a.ctr[59], (unsigned long long)(((uint64_t)qdone << 32) | (uint32_t)__popcll(__ballot(j >= 0))));
+      }
+      break;
+    }
     if (pc) pc->mark(0);
     const uint64_t parked = __ballot(fin >= 0);
     const uint64_t busy0 = __ballot(j >= 0 && fin < 0);
+    if (a.dbg && (guard & 63) == 0) {  // diagnostics heartbeat: the wave's state every 64 iterations
+      const int fl = __ffsll((unsigned long long)busy0) - 1;
+      const int wv = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+      unsigned long long* d = a.dbg + (size_t)wv * 8;
+      const int fj = __shfl(j, fl < 0 ? 0 : fl, 64), fs = __shfl(steps, fl < 0 ? 0 : fl, 64);
+      const int fc = __shfl(chain, fl < 0 ? 0 : fl, 64), fw = __shfl(r.wp, fl < 0 ? 0 : fl, 64);
+      const int fn = __shfl(r.R.N, fl < 0 ? 0 : fl, 64), fp = __shfl(pass, fl < 0 ? 0 : fl, 64);
+      if (lane == 0) {
+        __atomic_store_n(&d[0], (unsigned long long)guard, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[1], (unsigned long long)busy0, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[2], (unsigned long long)parked, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[3], ((unsigned long long)qdone << 32) | (uint32_t)fl, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[4], ((unsigned long long)(uint32_t)fj << 32) | (uint32_t)fp, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[5], ((unsigned long long)(uint32_t)fs << 32) | (uint32_t)fc, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[6], ((unsigned long long)(uint32_t)fw << 32) | (uint32_t)fn, __ATOMIC_RELAXED);
+        __atomic_store_n(&d[7], (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED);
+      }
+    }
     const uint64_t m0 = __ballot(j < 0 && !qdone && lane_on);
     // once the queue is empty, finish parked rollouts at once: a goal-biased follow-up (up to the whole
     // horizon) must not wait for other lanes to end
@@ -1517,7 +1574,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           const int q0 = base + __popcll(m & ((1ull << lane) - 1));
           if (q0 >= nq) {
             exhausted = true;
-          } else if (q0 < a.ncarry) {  // a chain suspended by the previous launch: resumed where it stopped
+          } else if (CARRY && q0 < ncarry) {  // a chain suspended by the previous launch: resumed where it stopped
             const Carry& cr = cin[q0];
             r = cr.r;
             c7 = cr.c7; c8 = cr.c8; c9 = cr.c9;
@@ -1531,8 +1588,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
               a.res_gb[j].outcome = -1;
               j = -1;
             }
-          } else if (q0 - a.ncarry < a.nrep) {  // replay of a committed rollout: rows into the arena
-            const Replay& rq = reps[q0 - a.ncarry];
+          } else if (q0 - ncarry < a.nrep) {  // replay of a committed rollout: rows into the arena
+            const Replay& rq = reps[q0 - ncarry];
             rp = true;
             nrows_rp = rq.nrows;
             rows = a.arena + rq.row_off * 10;
@@ -1542,7 +1599,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
             src = rq.src;
             iq = true;
           } else {
-            const int qj = q0 - a.ncarry - a.nrep;
+            const int qj = q0 - ncarry - a.nrep;
             const int q = a.perm ? a.perm[qj] : qj;
             k = q / B;
             const int s = q - k * B;
@@ -1583,39 +1640,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       if (parked == 0 && qdone) break;
       continue;
     }
-    // a chain at its cap (defer_steps) is suspended before it takes another step: its lane state goes to
-    // carry_out (one slot reservation per wave), the lane turns idle and refills
-    {
-      const bool at_cap = j >= 0 && fin < 0 && chain >= cap_at;
-      const uint64_t cm = __ballot(at_cap);
-      if (cm) {
-        const int leader = __ffsll((unsigned long long)cm) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(a.ncarry_out, __popcll(cm));
-        base = __shfl(base, leader, 64);
-        if (at_cap) {
-          const int slot_c = base + __popcll(cm & ((1ull << lane) - 1));
-          if (slot_c < a.carry_cap) {
-            Carry& co = cout[slot_c];
-            co.r = r;
-            co.c7 = c7; co.c8 = c8; co.c9 = c9;
-            co.row_off = rows ? (int64_t)((rows - a.arena) / 10) : -1;
-            co.j = j; co.bs = bs; co.k = k; co.pass = pass; co.steps = steps; co.chain = chain;
-            co.rp = rp ? 1 : 0;
-            co.nrows_rp = nrows_rp;
-            if (!rp) {  // the sample's result waits for this rollout (k_select: pending)
-              if (pass == 0) a.res[j].outcome = CLRRT_ROLL_PENDING;
-              else a.res_gb[j].outcome = CLRRT_ROLL_PENDING;
-            }
-          } else {  // no carry slot left: the host reports it (the chain is dropped, the round is void)
-            if (a.ctr) atomicAdd(&a.ctr[62], 1ull);
-          }
-          rp = false;
-          rows = nullptr;
-          j = -1;
-        }
-      }
-    }
+    // a chain at its cap (defer_steps) takes no further step: it parks with fin = kFinSuspend and the next
+    // batch (finish_parked) moves its lane state to carry_out
+    if (CARRY && j >= 0 && fin < 0 && chain >= cap_at) fin = kFinSuspend;
     // the lanes with a rollout in flight take a step; with the cooperative collision check (COOP) the
     // whole wave takes part in its SAT tests, so the check sits outside the lanes' divergent region
     const bool act = j >= 0 && fin < 0;
@@ -1779,7 +1806,9 @@ __global__ void k_select(SelArgs a) {
   if (a.gv) a.gv[v] = g;
   if (a.pend) a.pend[v] = 0;
   // EXACT-mode conflict threshold: the key a new node must beat (<=) to be tried before the result.
-  o.thr = o.k >= 0 ? a.ckey[g0 + o.k] : (nc == a.p.sort_limit ? a.ckey[g0 + nc - 1] : __builtin_inff());
+  // (keys are kept for the round's own samples only: null for views into the rings, BATCH needs no threshold)
+  o.thr = !a.ckey ? __builtin_inff()
+          : o.k >= 0 ? a.ckey[g0 + o.k] : (nc == a.p.sort_limit ? a.ckey[g0 + nc - 1] : __builtin_inff());
   o.gb_ok = 0;
   if (o.k >= 0) {
     const int pid = a.cand[g0 + o.k];
@@ -2211,7 +2240,7 @@ __global__ void __launch_bounds__(256) k_tree_reinit(ReinitArgs a) {
       if (Dobs == 0) s_coll = 1;
       const double kappa = glibc::tan(x[3]) / p.L;
       double term = p.W0 * x[4] * p.dt + p.W1 * fabs(kappa);
-      if (p.use_exp) term = term + p.W2 * exp(-p.W3 * Dobs);
+      if (p.use_exp) term = term + p.W2 * glibc::exp(-p.W3 * Dobs);  // glibc's exp, restated
       double* t = a.terms + (a.koff[k] + i) * 2;
       t[0] = term;
       t[1] = p.bend ? p.W4 * dist_to_lane(x[0], x[1], p.lane_shift0, p.Cxy1, p.Cxy2) : 0.0;
@@ -2282,7 +2311,7 @@ __global__ void k_selftest_math(int fn, const double* __restrict__ a, const doub
     case 3: r = sqrt(x); break;
     case 4: r = fmod(x, y); break;
     case 5: r = glibc::atan2(x, y); break;
-    case 6: r = exp(x); break;
+    case 6: r = glibc::exp(x); break;
     case 7: r = x / y; break;
     case 8: { float sf, cf; glibc::sincosf(xf, sf, cf); r = (double)cf; } break;
     case 9: r = (double)glibc::sinf(xf); break;
@@ -2654,9 +2683,10 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
                     obs_lds + 4 * kCoopLdsPerWave <= 148 * 1024;
   a.coop_off = (int)obs_lds;
   const size_t lds = obs_lds + (coop ? 4 * kCoopLdsPerWave : 0);
-  const void* fn = a.p.need_gap ? (const void*)&k_roll_run<true, false>
-                   : coop       ? (const void*)&k_roll_run<false, true>
-                                : (const void*)&k_roll_run<false, false>;
+  const bool carry = a.cap > 0 || a.ncarry > 0;  // deferred samples: the CARRY instantiation
+  const void* fn = a.p.need_gap ? (carry ? (const void*)&k_roll_run<true, false, true> : (const void*)&k_roll_run<true, false, false>)
+                   : coop       ? (carry ? (const void*)&k_roll_run<false, true, true> : (const void*)&k_roll_run<false, true, false>)
+                                : (carry ? (const void*)&k_roll_run<false, false, true> : (const void*)&k_roll_run<false, false, false>);
   if (lds > 64 * 1024 && (e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
     return e;
   const int nqueue = a0.njobs + a0.nrep + a0.ncarry;
@@ -2676,12 +2706,20 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   } else {
     a.perm = nullptr;
   }
-  if (a.p.need_gap)
-    hipLaunchKernelGGL((k_roll_run<true, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
-  else if (coop)
-    hipLaunchKernelGGL((k_roll_run<false, true>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
-  else
-    hipLaunchKernelGGL((k_roll_run<false, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  if (carry) {
+    if (a.p.need_gap)
+      hipLaunchKernelGGL((k_roll_run<true, false, true>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+    else if (coop)
+      hipLaunchKernelGGL((k_roll_run<false, true, true>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+    else
+      hipLaunchKernelGGL((k_roll_run<false, false, true>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  } else if (a.p.need_gap) {
+    hipLaunchKernelGGL((k_roll_run<true, false, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  } else if (coop) {
+    hipLaunchKernelGGL((k_roll_run<false, true, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  } else {
+    hipLaunchKernelGGL((k_roll_run<false, false, false>), dim3(nb), dim3(256), lds, st, a, qnext, best, B);
+  }
   LAUNCH_CHECK();
   return hipSuccess;
 }

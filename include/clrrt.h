@@ -286,13 +286,14 @@ int clrrt_expand(clrrt_ctx* ctx, clrrt_rng* rng, int64_t n_iters, double budget_
  * accepted-node records (clrrt_node, owner = rank, rows in this rank's arena) to dev_local, and calls
  * `exchange` once per round, which must return in *dev_all the records of every rank concatenated in
  * rank order (device memory, valid until the next call; a collective such as one all-gather over RCCL) and
- * in *n_all their count, and in *max_elapsed_ms the largest `elapsed_ms` over the ranks -- the budget is
- * checked against it, so every rank runs the same rounds.  Every rank then appends the same records in
+ * in *n_all their count, in *max_elapsed_ms the largest `elapsed_ms` over the ranks -- the budget is
+ * checked against it, so every rank runs the same rounds -- and in *aux_sum the sum of `aux_local` over the
+ * ranks (the engine's capacity bookkeeping: pending deferred samples, ranks whose arena is full).  Every rank then appends the same records in
  * the same order (deferred samples: the oldest round first), so the trees stay identical.  The caller
  * chooses weak scaling (batch = world x per-GPU samples) or strong scaling (batch fixed).  world = 1 turns
  * sharding off.  dev_local holds cap_local records (>= 2 x the slice, + the deferred samples). */
-typedef int32_t (*clrrt_exchange_fn)(void* user, int32_t n_local, double elapsed_ms, void** dev_all,
-                                     int32_t* n_all, double* max_elapsed_ms);
+typedef int32_t (*clrrt_exchange_fn)(void* user, int32_t n_local, double elapsed_ms, int64_t aux_local,
+                                     void** dev_all, int32_t* n_all, double* max_elapsed_ms, int64_t* aux_sum);
 int clrrt_set_shards(clrrt_ctx* ctx, int32_t rank, int32_t world, void* dev_local, int32_t cap_local,
                      clrrt_exchange_fn exchange, void* user);
 

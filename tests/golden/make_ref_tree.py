@@ -24,7 +24,7 @@ from oracle_binding import Oracle, lib as olib  # noqa: E402
 
 SEED = 20261017
 SORT_SIZES = {"a": (3000, 400, 512), "b": (9000, 1500, 256)}  # nodes, root copies, samples
-SIM_SETS = {"stub": (0, (0, 0)), "obb": (1, (200, 0)), "moving": (1, (200, 20))}
+SIM_SETS = {tag: (c, o) for tag, (c, o, _) in T.SIM_CASES.items()}
 N_PARENTS, N_JOBS, FULL_ROWS = 48, 480, 8
 SORT_COLS = [0, 1, 2, 4, 6, 11, 16, 17, 18, 19, 20]  # header columns the candidate lists read (+ v, t)
 
@@ -94,7 +94,7 @@ def main():
         Hp = T.sim_parents(rng, N_PARENTS)
         J = T.sim_jobs(rng, Hp, N_JOBS)
         obs = T.scene(ns_, nm_)
-        p = T.params(coll)
+        p = T.sim_params(tag)
         T.ref_configure(L, p, obs)
         rmeta, rrows = T.ref_simulate(L, Hp, J)
         o = Oracle(p, obs if len(obs) else None)

@@ -38,7 +38,35 @@ EXPAND_CASES = [
     ("stub_goal_s5", 0, (0, 0), 5, 250, (30.0, -6.0, -0.4, 2.0)),
     ("obb200_goal_s9", 1, (200, 0), 9, 250, (45.0, 8.0, 0.5, 1.0)),
 ]
+# round 4: a reference tree of >= 2000 nodes at cfg3's scene (the bench's EXACT query appends ~4.4 k)
+EXPAND_CASES.append(("obb200_s11_4k", 1, (200, 0), 11, 4000, (40.0, 0.0, 0.0, 0.0)))
 SAMPLE_GOALS = [(40.0, 0.0, 0.0, 0.0), (30.0, -6.0, -0.4, 2.0), (-12.0, 25.0, 2.0, 0.0)]
+# Simulation sets: tag -> (collision mode, (static, moving) obstacles, parameter overrides).
+#   stub_w2  : the obstacle-gap cost term Wcost[2] exp(-Wcost[3] Dobs) (simulation.cpp:91) on, with the shipped
+#              stub (Dobs = 100): exp(-1) per step, glibc's exp restated on the device (clrrt_glibc.hpp)
+#   obb_bend : the lane-deviation cost Wcost[4] getDistToLane (simulation.cpp:92-95, :49-53) with a sloped
+#              lane (Cxy[1] = 0.05, Cxy[2] = -1, laneShifts[0] = 0.5), 200 obstacles
+# (The gap term with the OBB check is not pinned to the reference: its gap reads the OBB normal
+# normsY[3] that setNorms leaves unset, old_collisioncheck.cpp:74-75; tests/test_gpu_parity.py pins the
+# device to the oracle's canonical normal there.)
+SIM_CASES = {"stub": (0, (0, 0), {}), "obb": (1, (200, 0), {}), "moving": (1, (200, 20), {}),
+             "stub_w2": (0, (0, 0), {"Wcost2": 1.0, "Wcost3": 0.01}),
+             "obb_bend": (1, (200, 0), {"bend": 1, "lane_shift0": 0.5, "Cxy": (0.0, 0.05, -1.0)})}
+
+
+def sim_params(tag):
+    coll, _, ov = SIM_CASES[tag]
+    p = params(coll)
+    if "Wcost2" in ov:
+        p.Wcost[2] = ov["Wcost2"]
+    if "Wcost3" in ov:
+        p.Wcost[3] = ov["Wcost3"]
+    if "bend" in ov:
+        p.bend = ov["bend"]
+        p.lane_shift0 = ov["lane_shift0"]
+        for i in range(3):
+            p.Cxy[i] = ov["Cxy"][i]
+    return p
 SAMPLE_SEEDS = [1, 3, 12345]
 
 

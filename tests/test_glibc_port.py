@@ -63,3 +63,16 @@ def test_glibc_atan2_bit_exact():
         out = subprocess.run([exe, "4000000"], capture_output=True, text=True)
         assert out.returncode == 0, out.stdout + out.stderr
         assert "mismatches 0" in out.stdout
+
+
+def test_glibc_exp_bit_exact():
+    """clrrt::glibc::exp (the W2 obstacle-cost term Wcost[2] exp(-Wcost[3] Dobs), simulation.cpp:91) against
+    the host libm's exp (its FMA variant) on special values and 4*10^6 arguments incl. the subnormal range
+    (4*10^7: 0 mismatches)."""
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "exp_check")
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe,
+                        os.path.join(HERE, "native", "exp_check.cpp")], check=True)
+        out = subprocess.run([exe, "4000000"], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "exp mismatches 0" in out.stdout

@@ -70,7 +70,29 @@ def _pair(kind, seed=1, iters=40):
 
 @pytest.mark.parametrize("kind", ["empty", "obb200", "moving"])
 def test_rollout_parity(kind):
+    _rollout_parity(kind)
+
+
+@pytest.mark.parametrize("kind", ["obb200", "moving"])
+def test_rollout_parity_obstacle_gap_cost(kind):
+    """Wcost[2] != 0 (simulation.cpp:91; parameters.launch:15 sets 0): the device keeps every obstacle's
+    separating gap (the NEED_GAP path of the collision check) and evaluates glibc's exp, restated
+    (clrrt_glibc.hpp); rollouts, rows and costS equal the oracle's bit for bit.  The reference itself reads
+    the OBB normal normsY[3] that setNorms leaves unset (old_collisioncheck.cpp:74-75) in that gap; the oracle
+    and the device use the edge normal, so this path is pinned to the oracle here and
+    to the reference build with the stub check (tests/test_ref_tree.py, set stub_w2)."""
+    def w2(p):
+        p.Wcost[2] = 1.0
+        return p
+    _rollout_parity(kind, w2)
+
+
+def _rollout_parity(kind, modify=None):
     o, pl = _pair(kind, seed=2, iters=40)
+    if modify is not None:
+        mode, _ = _scene(kind)
+        o.set_params(modify(abi.default_params(collision_mode=mode)))
+        pl.set_params(modify(clrrt.default_params(collision_mode=mode)))
     r = clrrt.Rng(11)
     smp = r.draw_samples(pl.params, 120)
     jobs = []

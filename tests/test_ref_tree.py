@@ -80,13 +80,13 @@ def test_oracle_candidate_lists_match_reference(tag):
         assert m == cnt[j] and np.array_equal(oi[:m], ids[j, :m]), j
 
 
-@pytest.mark.parametrize("tag", ["stub", "obb", "moving"])
+@pytest.mark.parametrize("tag", list(T.SIM_CASES))
 def test_oracle_rollouts_match_reference(tag):
     from oracle_binding import Oracle
     Hp, J = FIX[f"sim_{tag}_parents"], FIX[f"sim_{tag}_jobs"]
-    coll, (ns, nm) = {"stub": (0, (0, 0)), "obb": (1, (200, 0)), "moving": (1, (200, 20))}[tag]
+    coll, (ns, nm), _ = T.SIM_CASES[tag]
     obs = T.scene(ns, nm)
-    o = Oracle(T.params(coll), obs if len(obs) else None)
+    o = Oracle(T.sim_params(tag), obs if len(obs) else None)
     o.L.orc_load_tree(o.h, T.node_array(Hp), len(Hp))
     meta, rows = T.oracle_simulate(o, J)
     assert len(RU.mismatches(meta[:, T.SIM_META_COLS], FIX[f"sim_{tag}_meta"][:, T.SIM_META_COLS])) == 0
@@ -217,14 +217,15 @@ def test_device_candidate_lists_match_reference(tag, strategy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["stub", "obb", "moving"])
+@pytest.mark.parametrize("tag", list(T.SIM_CASES))
 def test_device_rollouts_match_reference(tag):
     """Simulation (simulation.cpp:36-143) from loaded parents: outcome, rows, costs, reference end and
-    every trajectory row equal the reference's."""
+    every trajectory row equal the reference's (stub_w2: the exp cost term; obb_bend: the lane cost)."""
     Hp, J = FIX[f"sim_{tag}_parents"], FIX[f"sim_{tag}_jobs"]
-    coll, (ns, nm) = {"stub": (0, (0, 0)), "obb": (1, (200, 0)), "moving": (1, (200, 20))}[tag]
+    coll, (ns, nm), _ = T.SIM_CASES[tag]
     pl = _planner(coll)
     try:
+        pl.set_params(T.sim_params(tag))
         pl.set_obstacles(T.scene(ns, nm))
         pl.tree_load(T.node_array(Hp))
         meta, rows = T.device_simulate(pl, J)

@@ -57,6 +57,9 @@ XFG = (0xC15C0, 186)
 # sysdeps/ieee754/flt-32 (sincosf.h, sincosf_data.c): __sincosf_table[2] (sign[4], hpi_inv, hpi, c0, c1,
 # s1, c2, s2, c3, s3, c4: 14 doubles each) and __inv_pio4[24] (32-bit windows of the bits of 2/pi)
 SINCOSF_TABLE = (0xB30C0, 2 * 14)
+# sysdeps/ieee754/dbl-64 (e_exp.c, e_exp_data.c; the FMA ifunc variant __exp_fma): struct exp_data __exp_data =
+# invln2N, shift, negln2hiN, negln2loN, poly[4], exp2_shift, exp2_poly[5], tab[2 * 128] (uint64)
+EXP_DATA = (0xAF960, 14, 256)
 INV_PIO4 = (0xB3060, 24)
 
 
@@ -183,11 +186,28 @@ def main():
         if not (abs(x * 256 - (i + 16)) <= 0.5 and abs(t1 - math.atan(x)) <= 2 * abs(t1) * 2.0 ** -52
                 and abs(t2 - 1 / (1 + x * x)) <= 4 * t2 * 2.0 ** -52):
             sys.exit(f"atan2 cij row {i}: {cij[7 * i:7 * i + 7]}")
+    # exp: __exp_data's constants, and tab[2k], tab[2k+1] with 2^(k/128) = asdouble(tab[2k+1] + (k << 45)) *
+    # (1 + asdouble(tab[2k])) to 2^-100 relative (derived with 60-digit arithmetic)
+    ex = [dbl(b, EXP_DATA[0] + 8 * i) for i in range(EXP_DATA[1])]
+    etab = list(struct.unpack_from(f"<{EXP_DATA[2]}Q", b, EXP_DATA[0] + 8 * EXP_DATA[1]))
+    if ex[0] != float.fromhex("0x1.71547652b82fep+7") or ex[1] != 1.5 * 2.0 ** 52:
+        sys.exit("__exp_data invln2N / shift")
+    decimal.getcontext().prec = 60
+    ln2 = decimal.Decimal(2).ln()
+    if abs(decimal.Decimal(ex[2]) + decimal.Decimal(ex[3]) + ln2 / 128) > ln2 / 128 * decimal.Decimal(2) ** -90:
+        sys.exit("__exp_data negln2hiN + negln2loN != -ln2 / 128")
+    for k in range(128):
+        want = (decimal.Decimal(2) ** (decimal.Decimal(k) / 128))
+        scale = struct.unpack("<d", struct.pack("<Q", (etab[2 * k + 1] + (k << 45)) & 0xFFFFFFFFFFFFFFFF))[0]
+        tail = struct.unpack("<d", struct.pack("<Q", etab[2 * k]))[0]
+        got = decimal.Decimal(scale) * (1 + decimal.Decimal(tail))
+        if abs(got - want) > want * decimal.Decimal(2) ** -100:
+            sys.exit(f"__exp_data tab row {k}")
     lines = [
         "// clrrt_glibc_data.hpp — GENERATED by tools/gen_glibc_libm.py; do not edit.",
         "// Provenance: glibc 2.35 libm's data (the IBM Accurate Mathematical Library, (C) IBM Corp. and the Free",
         "// Software Foundation), distributed by glibc under the GNU Lesser General Public License v2.1 or later.",
-        "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c), tan (s_tan.c) and atan2 (e_atan2.c)",
+        "// Constants and tables of glibc 2.35's double sin/cos (s_sin.c), tan (s_tan.c), atan2 (e_atan2.c) and exp (e_exp.c)",
         "// as loaded by its FMA variants, read from the libm image the CPU oracle links (hash-checked);",
         "// __sincostab cross-checked against 60-digit sin/cos(k/128).",
         "#pragma once",
@@ -217,6 +237,14 @@ def main():
     lines.append("#define CLRRT_GLIBC_ATAN2_CIJ { \\")
     for i in range(0, len(cij), 7):
         lines.append("  " + ", ".join(hexf(v) for v in cij[i:i + 7]) + ", \\")
+    lines.append("}")
+    lines.append("// double exp (dbl-64/e_exp.c, ARM optimized-routines algorithm in glibc): __exp_data")
+    for n, v in zip(("exp_invln2N", "exp_shift", "exp_negln2hiN", "exp_negln2loN", "exp_C2", "exp_C3", "exp_C4",
+                     "exp_C5"), ex[:8]):
+        lines.append(f"constexpr double {n} = {hexf(v)};")
+    lines.append("#define CLRRT_GLIBC_EXP_TAB { \\")
+    for i in range(0, len(etab), 4):
+        lines.append("  " + ", ".join(f"{v:#018x}ull" for v in etab[i:i + 4]) + ", \\")
     lines.append("}")
     lines.append("#define CLRRT_GLIBC_INV_PIO4 { \\")
     for i in range(0, len(inv), 8):
