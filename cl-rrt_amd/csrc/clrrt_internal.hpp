@@ -191,6 +191,7 @@ struct WalkBufs {
   // its search to nch waves over interleaved super-tile subsets with the list's 11th entry as the
   // bound, then a merge wave (k_walk_split / k_walk_merge); budget 0 = off
   int bud_tiles, bud_ex, max_over, nch;
+  int half_max = 4096;  // fp16 LDS bounds up to this many super-tiles, coded bytes (+ inside bracket) beyond
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists

@@ -52,11 +52,15 @@ namespace clrrt {
 #define NN_K (CAND_K + 1)
 #define WALK_TILE 32
 #define WALK_SUPER 32  // tiles per super-tile
+#define WALK_FMT_STATE 0  // k_walk_search LDS formats: float bound + visited mask per super-tile,
+#define WALK_FMT_HALF 1   // fp16 bound (stateless),
+#define WALK_FMT_CODED 2  // one log-coded byte (stateless; large trees)
+#define WALK_TQ 68      // tile stack entries (a super-tile pair adds <= 64 to <= 3 pending)
 #ifndef WALK_APBINS
 #define WALK_APBINS 8  // ang_par sectors (top key bits)
 #endif
 #ifndef WALK_SECTOR_BITS
-#define WALK_SECTOR_BITS 3
+#define WALK_SECTOR_BITS 3  // 2^WALK_SECTOR_BITS >= WALK_APBINS
 #endif
 
 #define LAUNCH_CHECK3()                          \
@@ -96,7 +100,8 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   const float a = (float)nodes[i].ang_par;
   int bin = (int)floorf((a + 3.14159265f) * (WALK_APBINS / 6.2831853f));
   bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
-  keys[i] = ((uint64_t)bin << 61) | ((uint64_t)k << 29) | (__float_as_uint(nodes[i].costE) >> 3);
+  keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | ((uint64_t)k << (32 - WALK_SECTOR_BITS)) |
+            (__float_as_uint(nodes[i].costE) >> WALK_SECTOR_BITS);
   vals[i] = i;
 }
 
@@ -301,15 +306,35 @@ __device__ __forceinline__ float atan2_apx(float y, float x) {
 // it), so moving the offset by pos_err moves the key by at most pos_err; the margin also covers the
 // float evaluation here and in the reference (checked by tests/test_nnwalk_bounds.py).
 // The same margin bounds the key from above: lo <= key <= hi (lo = -inf, hi = +inf when undecided).
+template <bool BRK>
 __device__ __forceinline__ void walk_key_range(float tx, float ty, float pos_err, float& lo, float& hi) {
   const float rho = 4.77f;
   const float t2 = tx * tx + ty * (ty - 2.f * rho);  // dc^2 - rho^2
   if (t2 <= -0.01f) {
     // surely inside the circle: dubins_key's inside branch, rho (alpha + asin(qx / df) - asin(rho sin(alpha)
     // / df)) with alpha = 2 pi - acos((5 rho^2 - df^2) / (4 rho^2)), is >= rho pi = 14.98 anywhere
-    // (a tighter bracket cut exact keys 3x but cost more in the visits: cfg3 0.94 -> 0.89 M nodes/s)
     lo = 14.9f;
     hi = __builtin_inff();
+    if constexpr (BRK) {
+      // BRK (large trees, where the inside records' exact keys dominate): a bracket of that branch, restated
+      // with atan2: asin(qx / df) = atan2(qx, qy + rho), sin(alpha) = -sqrt(1 - c^2).  Its gradient grows
+      // like 1 / sqrt(1 - c^2) and df / sqrt(df^2 - (rho sin alpha)^2): the margin carries those factors,
+      // and near their poles the plain rho pi bound stays (tests/test_nnwalk_bounds.py, jittered offsets).
+      // On bench-size trees it costs the visits more than it saves (cfg3 0.94 -> 0.89 M nodes/s, round 2).
+      const float df2 = tx * tx + (ty + rho) * (ty + rho);
+      const float cA = fminf(fmaxf((5.f * rho * rho - df2) * (1.f / (4.f * rho * rho)), -1.f), 1.f);
+      const float sA = fsqrt(fmaxf((1.f - cA) * (1.f + cA), 0.f));
+      const float u = rho * sA;
+      const float w = fsqrt(fmaxf(df2 - u * u, 0.f));
+      const float cw = w * frcp(fsqrt(df2));
+      if (sA >= 0.05f && cw >= 0.05f) {
+        const float alpha = 6.28318531f - atan2_apx(sA, cA);
+        const float L = rho * (alpha + atan2_apx(tx, ty + rho) + atan2_apx(u, w));
+        const float m = 2e-3f + 1e-4f * L + pos_err * (8.f + 8.f * frcp(sA) + 8.f * frcp(cw));
+        lo = fmaxf(L - m, 14.9f);
+        hi = L + m;
+      }
+    }
     return;
   }
   if (!(t2 > -0.01f)) {  // NaN
@@ -426,19 +451,40 @@ __device__ __forceinline__ void walk_emit(float lk, int li, int lane, int s, int
   }
 }
 
-// One wave per sample.  LDS per super-tile: s_lb = a lower bound (fp16, rounded down) of the keys in
+// Stateless bounds in LDS: one byte per super-tile, a lower bound on a log scale (16 codes per octave from
+// 2^-4 to 2^12; code 0: no bound, 255: nothing left).  Decoding is monotone, so a bound is compared with a
+// threshold in the code domain (lc_le: the largest code that decodes to <= the threshold).
+__device__ __forceinline__ float lc_dec(int c) {
+  return c == 0 ? -__builtin_inff() : (c == 255 ? __builtin_inff() : exp2f((float)(c - 64) * 0.0625f));
+}
+__device__ __forceinline__ int lc_enc(float b) {  // the largest code whose value is <= b
+  if (b == __builtin_inff()) return 255;
+  if (!(b >= lc_dec(1))) return 0;
+  int c = (int)floorf(log2f(b) * 16.f) + 64;
+  c = c < 1 ? 1 : (c > 254 ? 254 : c);
+  while (c > 1 && lc_dec(c) > b) c--;
+  while (c < 254 && lc_dec(c + 1) <= b) c++;
+  return c;
+}
+__device__ __forceinline__ int lc_le(float v) {  // the largest code c with lc_dec(c) <= v
+  return v == __builtin_inff() ? 255 : lc_enc(v);
+}
+
+// One wave per sample.  LDS per super-tile: s_lb = a lower bound (one log-coded byte, rounded down) of the keys in
 // its tiles not yet visited.  Pass k visits the tiles whose bound lies in (T_{k-1}, min(T_k, kth)]
 // (T_k grows geometrically from the smallest bound; a tile's bound is max(tile bound, super-tile
 // bound), so the intervals of successive passes partition the tiles and no per-tile state is kept),
 // two tiles of 32 nodes per step (lanes 0-31 / 32-63), so nodes are visited roughly in the order of
 // their bounds and the list's 11th key prunes the rest.  The search ends after the first pass whose
-// threshold reaches kth: every tile with a bound <= kth has then been visited.  LDS is 2 bytes per
-// super-tile (12 KB at 6 M nodes).
+// threshold reaches kth: every tile with a bound <= kth has then been visited.  LDS is 1 byte per
+// super-tile (16 KB at 16 M nodes: LDS, not registers, sets the walk's occupancy on large trees).
+// Tiles taken by the super-tile visits go to a small LDS stack and are visited four at a time (128
+// records over the 64 lanes), so the visits' lanes stay busy however few tiles each super-tile gives.
 #ifndef CLRRT_WALK_WAVES
 #define CLRRT_WALK_WAVES 4
 #endif
 // STATE = true (trees up to ~1.3 M nodes): per super-tile a float bound and a visited-tile mask
-// (8 bytes) instead of the stateless fp16 interval scheme, which spends an extra bound per visit.
+// (8 bytes) instead of the stateless coded interval scheme, which spends an extra bound per visit.
 //
 // Overflow.  A round's search lasts as long as its slowest samples, and a few samples need 10-100x
 // the median work (optimize samples near the root, where the costE bound is weak: 1e5 exact keys).
@@ -449,7 +495,7 @@ __device__ __forceinline__ void walk_emit(float lk, int li, int lane, int s, int
 // k_walk_merge takes the 11 smallest (key, node) pairs of the nch partial lists.  Every pair of the
 // sample's true list precedes that 11th entry, each wave's list is exact over its super-tiles, so the
 // merged list equals the walk's (and the brute force's).  Records beyond max_over: the walk goes on.
-template <bool STATE, bool SPLIT>
+template <int FMT, bool SPLIT, bool BRK>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_WALK_WAVES))) k_walk_search(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                     const float4* __restrict__ Q, const float* __restrict__ CE,
@@ -465,12 +511,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
                                                     int max_over, int nch, float* __restrict__ pk,
                                                     int* __restrict__ pi, int nloc_max) {
   // LDS is indexed by the wave's local super-tile index l (super-tile gst(l))
-  extern __shared__ __half s_lb[];  // [nloc] bounds of the super-tiles' remaining tiles (stateless)
+  constexpr bool STATE = FMT == WALK_FMT_STATE, CODED = FMT == WALK_FMT_CODED;
+  extern __shared__ uint8_t s_lb[];  // [nloc] bounds of the super-tiles' remaining tiles (stateless) ...
+  __half* s_lbh = (__half*)s_lb;             // ... fp16, rounded down, or (CODED) one log-coded byte
   float* s_lbf = (float*)s_lb;               // STATE: [nloc] float bounds ...
   uint32_t* s_vis = (uint32_t*)(s_lbf + nloc_max);  // ... and [nloc] visited / discarded tile masks
-  auto lds_lb = [&](int t) -> float { return STATE ? s_lbf[t] : __half2float(s_lb[t]); };
   __shared__ int s_q2[64];  // records past stage 1 (stage 2: exact keys) ...
   __shared__ float s_b2[64];  // ... and their key lower bounds
+  __shared__ int s_tq[WALK_TQ];    // tile queue: tiles taken by the super-tile visits ...
+  __shared__ float s_tb[WALK_TQ];  // ... and their bounds
   const int lane = threadIdx.x;
   int s, ch = 0, nloc = nsup;
   float kb = __builtin_inff();  // SPLIT: the pairs sought precede (kb, ib)
@@ -512,6 +561,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   // feasible; 11 nodes have keys <= uk[10], so no pair with a larger key enters the list
   float uk = __builtin_inff();
   float kth = __builtin_inff();
+  int kth_c = 255;    // stateless: lc_le(kth - base)
+  float base = 0.f;   // the smallest super-tile bound (pass thresholds and stateless codes are relative to it)
   int idk = 0x7fffffff;
   float lim = __builtin_inff();  // explore: (prune radius + delta)^2
   float cb0 = -2.f;             // explore: cos of the largest heading-to-sample angle a node may have
@@ -535,6 +586,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     if (SPLIT && w_less(kb, ib, kth, idk)) { kth = kb; idk = ib; }
     const float u10 = uni(__shfl(uk, NN_K - 1, 64));
     if (u10 < kth) { kth = u10; idk = 0x7fffffff; }
+    if constexpr (CODED) kth_c = uni(lc_le(kth - base));
     if (kth < __builtin_inff()) {
       const float R = (kth + 2e-4f) * (1.0f / 0.9999f);
       lim = uni(R < 0.f ? -1.f : (R + dl) * (R + dl));
@@ -634,7 +686,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     const float qx = rsx - pp.x, qy = rsy - pp.y;
     const float tx = pp.z * qx - pp.w * qy, ty = fabsf(pp.w * qx + pp.z * qy);
     float lo, hi;
-    walk_key_range(tx, ty, 4.f * dl + 1e-6f * (fabsf(tx) + ty), lo, hi);
+    walk_key_range<BRK>(tx, ty, 4.f * dl + 1e-6f * (fabsf(tx) + ty), lo, hi);
     const float cst = ex ? 0.f : ce;  // explore keys carry no cost
     const float tlo = cst + lo, thi = cst + hi;
     lbt = tlo - 1e-6f * fabsf(tlo);
@@ -718,7 +770,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   };
   // nodes of up to four tiles: t0 / t1 on lanes 0-31 / 32-63 (first set), t2 / t3 (second set);
   // -1 = none.  Both sets' records are loaded before either is tested.
-  auto visit4 = [&](int t0, int t1, int t2, int t3) {
+  auto visit4 = [&](int t0, int t1, int t2, int t3) __attribute__((always_inline)) {
     const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     n_tile += (t0 >= 0) + (t1 >= 0) + (t2 >= 0) + (t3 >= 0);
     const int ta = lane < 32 ? t0 : t1, tb = lane < 32 ? t2 : t3;
@@ -759,6 +811,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   auto run_out = [&](int tl) -> bool {
     const int2 tr = trun[tl];
     return tr.x >= 0 && tr.x == hc && !w_less(kc, tr.y, kth, idk);
+  };
+  // Tile stack (LDS, WALK_TQ entries: tile, bound), wave-uniform depth.  Tiles the list has pruned since
+  // they were pushed are skipped.
+  int qn = 0;
+  auto next_q = [&]() __attribute__((always_inline)) -> int {
+    while (qn > 0) {
+      qn--;
+      const int t = uni(s_tq[qn]);
+      if (!(uni(s_tb[qn]) > kth)) return t;
+    }
+    return -1;
+  };
+  auto visit_queue = [&]() __attribute__((always_inline)) {
+    const int t0 = next_q();
+    const int t1 = next_q();
+    const int t2 = next_q();
+    const int t3 = next_q();
+    if (t0 >= 0) visit4(t0, t1, t2, t3);
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto flush_queue = [&]() __attribute__((always_inline)) {
+    while (qn > 0) visit_queue();
   };
   // visit the tiles of super-tiles sa (lanes 0-31) and sb (lanes 32-63, -1: none) whose bounds lie in
   // (Tp, min(T, kth)] (STATE: not visited yet and <= min(T, kth)); the super-tiles' LDS bounds become
@@ -816,25 +890,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       const bool take = st >= 0 && (first || lb > Tp) && lb <= T && !(lb > kth);
       tm = __ballot(take);
       const float rest = hmin(st >= 0 && lb > T ? lb : __builtin_inff());
-      if ((lane & 31) == 0 && st >= 0) s_lb[lo] = __float2half_rd(rest);
-    }
-    // tiles that the list has pruned since they were selected are skipped
-    auto next_tile = [&]() -> int {
-      while (tm) {
-        const int a = __ffsll((unsigned long long)tm) - 1;
-        tm &= tm - 1;
-        if (!(__shfl(lb, a, 64) > kth)) return (a < 32 ? sa : sb) * WALK_SUPER + (a & 31);
+      if ((lane & 31) == 0 && st >= 0) {
+        if constexpr (CODED) s_lb[lo] = (uint8_t)lc_enc(rest - base);
+        else s_lbh[lo] = __float2half_rd(rest);
       }
-      return -1;
-    };
-    while (tm) {
-      const int t0 = next_tile();
-      const int t1 = next_tile();
-      const int t2 = next_tile();
-      const int t3 = next_tile();
-      if (t0 >= 0) visit4(t0, t1, t2, t3);
     }
+    // the taken tiles join the wave's tile queue; full sets of four are visited at once (the lanes of a
+    // visit stay busy however few tiles each super-tile gives)
+    const bool tk = (tm >> lane) & 1ull;
+    if (tk) {
+      const int pos = qn + __popcll(tm & ((1ull << lane) - 1));
+      s_tq[pos] = st * WALK_SUPER + (lane & 31);
+      s_tb[pos] = lb;
+    }
+    qn += __popcll(tm);
     __builtin_amdgcn_wave_barrier();
+    while (qn >= 4) visit_queue();
     if (prof) cyc[1] += __builtin_amdgcn_s_memtime() - c0;
   };
 
@@ -871,17 +942,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
       if constexpr (STATE) {
         s_lbf[t] = lb;
         s_vis[t] = 0u;
-      } else {
-        s_lb[t] = __float2half_rd(lb);
+      } else if constexpr (!CODED) {
+        s_lbh[t] = __float2half_rd(lb);
       }
       mlb = fminf(mlb, lb);
     }
   }
   mlb = wmin(mlb);
+  base = mlb > 0.f && mlb < __builtin_inff() ? mlb : 0.f;
+  if constexpr (CODED) {
+    // codes relative to the smallest bound: their resolution (1/16 octave of the distance above it) then
+    // follows the pass thresholds' geometric spacing; the bounds are recomputed rather than kept
+    for (int t0 = 0; t0 < nloc; t0 += 64) {
+      const int t = t0 + lane;
+      if (t < nloc) s_lb[t] = (uint8_t)lc_enc(walk_lb(sup[gst(t)], rsx, rsy, ex, flen_t, dsR) - base);
+    }
+  }
   __builtin_amdgcn_wave_barrier();
   if (prof) cyc[0] += __builtin_amdgcn_s_memtime() - ct0;
   // 2. passes of growing threshold
-  const float base = mlb > 0.f && mlb < __builtin_inff() ? mlb : 0.f;
 #ifndef WALK_T0
 #define WALK_T0 0.5f
 #endif
@@ -892,17 +971,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   bool budget = !SPLIT && (bud_tiles > 0 || bud_ex > 0);
   for (int pass = 0;; pass++) {
     const float lim_t = fminf(T, kth);
+    const int lim_c = CODED ? uni(lc_le(lim_t - base)) : 0;
     for (int t0 = 0; t0 < nloc; t0 += 64) {
       const int t = t0 + lane;
-      const float lb = t < nloc ? lds_lb(t) : __builtin_inff();
-      uint64_t m = __ballot(lb < __builtin_inff() && lb <= lim_t);
+      bool want;
+      if constexpr (CODED) {
+        const int c = t < nloc ? s_lb[t] : 255;
+        want = c != 255 && c <= lim_c;
+      } else {
+        const float lb = t < nloc ? (STATE ? s_lbf[t] : __half2float(s_lbh[t])) : __builtin_inff();
+        want = lb < __builtin_inff() && lb <= lim_t;
+      }
+      uint64_t m = __ballot(want);
       while (m) {
         // two super-tiles per visit (one per half wave)
         int sa = -1, sb = -1;
         while (m && sb < 0) {
           const int st = t0 + __ffsll((unsigned long long)m) - 1;
           m &= m - 1;
-          if (lds_lb(st) > kth) continue;
+          if (CODED ? (int)s_lb[st] > kth_c : (STATE ? s_lbf[st] : __half2float(s_lbh[st])) > kth) continue;
           if (sa < 0) sa = st; else sb = st;
         }
         if (sa >= 0) visit_supers(sa, sb, Tp, T, pass == 0);
@@ -921,6 +1008,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         }
       }
     }
+    flush_queue();
     drain();
     if (T == __builtin_inff() || kth <= T) break;
     Tp = T;
@@ -1160,12 +1248,16 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   const double scale = span > 0 ? 65535.0 / span : 1.0;
   hipError_t e = hipSuccess;
   size_t bytes = 0;
-  // per-sample LDS: 8 B per super-tile with state, 2 B without; state while it costs no occupancy
-  const bool state = nsup <= 1280 && !stateless;
-  const size_t lds = (state ? 2 * sizeof(float) : sizeof(__half)) * (size_t)nsup;
+  // per-sample LDS: 8 B per super-tile with state (while it costs no occupancy), 2 B (fp16) while that costs
+  // none, then one coded byte (+ the inside-circle key bracket: on such trees exact keys dominate)
+  const int fmt = nsup <= 1280 && !stateless ? WALK_FMT_STATE : (nsup <= w.half_max ? WALK_FMT_HALF : WALK_FMT_CODED);
+  const bool brk = fmt == WALK_FMT_CODED;
+  const size_t lds = (fmt == WALK_FMT_STATE ? 2 * sizeof(float) : fmt == WALK_FMT_HALF ? sizeof(__half) : 1) * (size_t)nsup;
+  const void* kfn = fmt == WALK_FMT_STATE ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false>
+                    : fmt == WALK_FMT_HALF ? (const void*)&k_walk_search<WALK_FMT_HALF, false, false>
+                                           : (const void*)&k_walk_search<WALK_FMT_CODED, false, true>;
   if (lds > 64 * 1024) {
-    e = hipFuncSetAttribute(state ? (const void*)&k_walk_search<true, false> : (const void*)&k_walk_search<false, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const bool split = (w.bud_tiles > 0 || w.bud_ex > 0) && w.max_over > 0 && w.nch > 0 && w.ovf_n;
@@ -1180,28 +1272,33 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
   if (e != hipSuccess) return e;
   const int bt = split ? w.bud_tiles : 0, be = split ? w.bud_ex : 0;
-  if (state)
-    hipLaunchKernelGGL((k_walk_search<true, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, w.Q,
-                       w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder,
-                       stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
-  else
-    hipLaunchKernelGGL((k_walk_search<false, false>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P,
-                       w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,
-                       w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup);
+#define WALK_LAUNCH(F, BK)                                                                                       \
+  hipLaunchKernelGGL((k_walk_search<F, false, BK>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, \
+                     w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,  \
+                     w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup)
+  if (fmt == WALK_FMT_STATE) WALK_LAUNCH(WALK_FMT_STATE, false);
+  else if (fmt == WALK_FMT_HALF) WALK_LAUNCH(WALK_FMT_HALF, false);
+  else WALK_LAUNCH(WALK_FMT_CODED, true);
+#undef WALK_LAUNCH
   LAUNCH_CHECK3();
   if (split) {
     // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
     // claimed records exit at once) and the merge
     const int nl = (nsup + w.nch - 1) / w.nch;
+    const void* sfn = brk ? (const void*)&k_walk_search<WALK_FMT_STATE, true, true>
+                          : (const void*)&k_walk_search<WALK_FMT_STATE, true, false>;
     if (2 * sizeof(float) * (size_t)nl > 64 * 1024) {
-      e = hipFuncSetAttribute((const void*)&k_walk_search<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(2 * sizeof(float) * (size_t)nl));
+      e = hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * sizeof(float) * (size_t)nl));
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((k_walk_search<true, true>), dim3(w.max_over * w.nch), dim3(64), 2 * sizeof(float) * (size_t)nl,
-                       st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand,
-                       ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
-                       nl);
+#define WALK_SPLIT(BK)                                                                                           \
+  hipLaunchKernelGGL((k_walk_search<WALK_FMT_STATE, true, BK>), dim3(w.max_over * w.nch), dim3(64),               \
+                     2 * sizeof(float) * (size_t)nl, st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, \
+                     ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf,  \
+                     w.max_over, w.nch, w.pk, w.pi, nl)
+    if (brk) WALK_SPLIT(true);
+    else WALK_SPLIT(false);
+#undef WALK_SPLIT
     LAUNCH_CHECK3();
     hipLaunchKernelGGL(k_walk_merge, dim3(w.max_over), dim3(64), 0, st, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi,
                        p.sort_limit, cand, ckey, ncand, ctie);

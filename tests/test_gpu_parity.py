@@ -44,7 +44,10 @@ def _nn_strategy(pl, name):
     so that its own path runs."""
     pl.set_option("nn_exact_fused", name == "fused")
     pl.set_option("nn_walk_min", 0 if name.startswith("walk") else 1 << 40)
-    pl.set_option("nn_walk_stateless", name.endswith("stateless"))
+    # 'coded': the large-tree walk (one log-coded LDS byte per super-tile + the inside-circle key bracket)
+    coded = "coded" in name
+    pl.set_option("nn_walk_stateless", name.endswith("stateless") or coded)
+    pl.set_option("nn_walk_half_max", 0 if coded else 4096)
     split = name.startswith("walk_split")
     pl.set_option("nn_walk_budget_tiles", 1 if split else 2048)
     pl.set_option("nn_walk_budget_keys", 1 if split else 4096)
@@ -356,7 +359,7 @@ def test_walk_matches_brute_force_large_tree():
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    for strategy in ("walk", "walk_stateless"):
+    for strategy in ("walk", "walk_stateless", "walk_coded", "walk_split_coded"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")

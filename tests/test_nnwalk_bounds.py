@@ -11,6 +11,7 @@ relies on, with the margins it uses:
     the walk's drains) below / above the key of every offset within pos_err of its own.
 """
 import numpy as np
+import pytest
 
 RHO = np.float32(4.77)
 
@@ -86,8 +87,9 @@ def atan2_apx(y, x):
     return np.where(y < 0, -a, a).astype(F)
 
 
-def walk_key_range(tx, ty, pos_err):
-    """walk_key_range of clrrt_nnwalk.hip in float32 (inside the turning circle: the rho pi floor)."""
+def walk_key_range(tx, ty, pos_err, inside_bracket=False):
+    """walk_key_range of clrrt_nnwalk.hip in float32 (inside the turning circle: the rho pi floor, or with
+    inside_bracket -- walk_key_range<true>, the large-tree walk -- a bracket of the inside branch)."""
     tx, ty = tx.astype(F), ty.astype(F)
     rho = RHO
     t2 = tx * tx + ty * (ty - F(2) * rho)
@@ -100,6 +102,20 @@ def walk_key_range(tx, ty, pos_err):
     m = F(2) * pos_err + F(2e-4) + F(2e-5) * L
     lo = np.where(out, L - m, np.where(near, np.minimum(L - m - F(1e-4), F(14.9)), F(14.9)))
     hi = np.where(out, L + m, np.inf)
+    # surely inside: the inside branch restated with atan2 (clrrt_nnwalk.hip walk_key_range<true>)
+    ins = t2 <= F(-0.01)
+    df2 = tx * tx + (ty + rho) * (ty + rho)
+    cA = np.clip((F(5) * rho * rho - df2) * (F(1) / (F(4) * rho * rho)), F(-1), F(1))
+    sA = np.sqrt(np.maximum((F(1) - cA) * (F(1) + cA), F(0)))
+    u = rho * sA
+    w = np.sqrt(np.maximum(df2 - u * u, F(0)))
+    cw = w / np.sqrt(df2)
+    use = ins & (sA >= F(0.05)) & (cw >= F(0.05)) & inside_bracket
+    with np.errstate(all="ignore"):
+        Li = rho * ((F(6.28318531) - atan2_apx(sA, cA)) + atan2_apx(tx, ty + rho) + atan2_apx(u, w))
+        mi = F(2e-3) + F(1e-4) * Li + pos_err * (F(8) + F(8) / sA + F(8) / cw)
+    lo = np.where(use, np.maximum(Li - mi, F(14.9)), lo)
+    hi = np.where(use, Li + mi, hi)
     return lo.astype(np.float64), hi.astype(np.float64)
 
 
@@ -160,9 +176,11 @@ def test_stage1_bound_near_turning_circle():
         assert (ub[okh] - key[okh]).min() >= 0, band
 
 
-def test_stage1_bound_inside_turning_circle():
+@pytest.mark.parametrize("bracket", [False, True])
+def test_stage1_bound_inside_turning_circle(bracket):
     """Offsets uniformly inside the turning circle, jittered by up to 6e-4 (beyond the frame error of
-    any bench tree): the walk's lower bound (the rho pi floor there) never exceeds the float key."""
+    any bench tree): the walk's bounds (the rho pi floor there, or the large-tree walk's bracket of the
+    inside branch) bracket the float key."""
     rng = np.random.default_rng(14)
     rho = float(RHO)
     n = 2_000_000
@@ -176,8 +194,10 @@ def test_stage1_bound_inside_turning_circle():
         rr = pos * np.sqrt(rng.uniform(0, 1, n))
         jx = (tx + rr * np.cos(ang)).astype(F)
         jy = np.abs(ty + rr * np.sin(ang)).astype(F)
-        lb, ub = walk_key_range(jx, jy, F(pos) + F(1e-6) * (np.abs(jx) + jy))
+        lb, ub = walk_key_range(jx, jy, F(pos) + F(1e-6) * (np.abs(jx) + jy), inside_bracket=bracket)
         ok = np.isfinite(key)
         assert (key[ok] - lb[ok]).min() >= 0, (pos, (key[ok] - lb[ok]).min())
         okh = ok & np.isfinite(ub)
         assert not okh.any() or (ub[okh] - key[okh]).min() >= 0, pos
+        if bracket:  # and it is a bracket: most inside offsets get a finite upper bound
+            assert okh.mean() > 0.5, okh.mean()
