@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
 
 CONFIGS = {
     # name: static obstacles, moving obstacles, samples per batch (per GPU), horizon ms
-    "cfg2": dict(obstacles=50, moving=0, batch=4096, horizon_ms=200.0,
+    "cfg2": dict(obstacles=50, moving=0, batch=4096, horizon_ms=200.0, defer_steps=64,
                  desc="cfg2: 50-obstacle static urban scene, 4096 samples/batch, 0.2 s horizon"),
     "cfg3": dict(obstacles=200, moving=0, batch=16384, horizon_ms=2000.0,
                  desc="cfg3: 200-obstacle static urban scene, 16384 samples/batch per GPU, 2 s horizon"),
@@ -44,7 +44,7 @@ PEAK_HBM_GBS = 8000.0
 # point scanned by findClosestPoint; FP32 per OBB box test = 36.
 FLOP_STEP, FLOP_SCAN, FLOP_BOX = 160, 6, 36
 FLOP_KEY = 40  # FP32 FLOP per nearest-node (Dubins) key
-# BATCH option defer_steps of the headline run
+# BATCH option defer_steps of the headline run (a config may set its own)
 DEFER_STEPS = 128
 
 
@@ -63,9 +63,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-exact", action="store_true", help="skip the secondary EXACT-mode figure")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--defer-steps", type=int, default=DEFER_STEPS,
+    ap.add_argument("--defer-steps", type=int, default=-1,
                     help="BATCH deferred samples: rollout chains run at most this many steps per round's launch, "
-                         "longer ones resume in the next and their sample commits in a later round (0: off)")
+                         "longer ones resume in the next and their sample commits in a later round (0: off; "
+                         "default: the config's, else DEFER_STEPS)")
     ap.add_argument("--no-sync", action="store_true", help="skip the secondary figure without deferred samples")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N > 1: weak = batch samples per GPU per round (N x batch per round), strong = batch "
@@ -269,7 +270,7 @@ def main():
     B_rank = -(-G // world)
     pl = clrrt.Planner(params, device=local % max(1, ndev), max_nodes=max_nodes, max_rows=max_rows, max_batch=B_rank,
                        max_obstacles=max(1, len(obs)))
-    defer = args.defer_steps
+    defer = args.defer_steps if args.defer_steps >= 0 else cfg.get("defer_steps", DEFER_STEPS)
     pl.set_option("defer_steps", defer)
     for kv in args.opt:
         k, v = kv.split("=", 1)

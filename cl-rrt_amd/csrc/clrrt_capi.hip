@@ -107,6 +107,7 @@ struct clrrt_ctx {
   // with lag 2: 3072 tiles 1.039 vs 2048 1.031 M nodes/s, 8192 keys 1.008, 12 chunks 1.030)
   int nnw_bud_tiles = 3072, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
+  int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
   // pipelined rounds: a second index set, so the next round's index is built while the side stream's
@@ -1234,6 +1235,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) c->nnw_bud_tiles = (int)value;
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
+  else if (k == "nn_walk_lds_floor" && value >= 0 && value <= 65536) c->nnw_lds_floor = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
@@ -1391,6 +1393,7 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.max_over = c->nnw_max_over;
   w.nch = c->nnw_chunks;
   w.half_max = c->nnw_half_max;
+  w.lds_floor = c->nnw_lds_floor;
   return alloc_walk(c, w);
 }
 static int ensure_walk(clrrt_ctx* c) { return ensure_walk_set(c, c->nnw); }

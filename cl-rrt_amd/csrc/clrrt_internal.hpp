@@ -192,6 +192,7 @@ struct WalkBufs {
   // bound, then a merge wave (k_walk_split / k_walk_merge); budget 0 = off
   int bud_tiles, bud_ex, max_over, nch;
   int half_max = 4096;  // fp16 LDS bounds up to this many super-tiles, coded bytes (+ inside bracket) beyond
+  int lds_floor = 0;    // bytes of LDS each walk wave reserves at least (caps the walk's waves per CU)
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists

@@ -55,6 +55,9 @@ namespace clrrt {
 #define WALK_FMT_STATE 0  // k_walk_search LDS formats: float bound + visited mask per super-tile,
 #define WALK_FMT_HALF 1   // fp16 bound (stateless),
 #define WALK_FMT_CODED 2  // one log-coded byte (stateless; large trees)
+#ifndef WALK_STAGE1_QUEUE
+#define WALK_STAGE1_QUEUE 1
+#endif
 #define WALK_TQ 68      // tile stack entries (a super-tile pair adds <= 64 to <= 3 pending)
 #ifndef WALK_APBINS
 #define WALK_APBINS 8  // ang_par sectors (top key bits)
@@ -518,6 +521,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   uint32_t* s_vis = (uint32_t*)(s_lbf + nloc_max);  // ... and [nloc] visited / discarded tile masks
   __shared__ int s_q2[64];  // records past stage 1 (stage 2: exact keys) ...
   __shared__ float s_b2[64];  // ... and their key lower bounds
+#if WALK_STAGE1_QUEUE
+  __shared__ int s_q1[192];        // records past the prefilter (stage 1 queue)
+#endif
   __shared__ int s_tq[WALK_TQ];    // tile queue: tiles taken by the super-tile visits ...
   __shared__ float s_tb[WALK_TQ];  // ... and their bounds
   const int lane = threadIdx.x;
@@ -768,6 +774,34 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     }
     return !ang_bad && !in_bad && !turn_bad;
   };
+#if WALK_STAGE1_QUEUE
+  // Records past the prefilter wait in an LDS stack (their place-order index) and run stage 1 in full
+  // waves of 64: most visited records fail the prefilter (84% of an explore sample's on a 16 M-node tree),
+  // so stage 1 on the visits' own lanes would run its key brackets for a few lanes at a time.
+  int n1 = 0;
+  auto push1 = [&](bool ok, int j) __attribute__((always_inline)) {
+    const uint64_t m = __ballot(ok);
+    if (ok) s_q1[n1 + __popcll(m & ((1ull << lane) - 1))] = j;
+    n1 += __popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto run_stage1 = [&](int cnt) __attribute__((always_inline)) {  // the top cnt (<= 64) entries
+    const int b0 = n1 - cnt;
+    const bool v = lane < cnt;
+    const int j = v ? s_q1[b0 + lane] : -1;
+    __builtin_amdgcn_wave_barrier();
+    n1 = b0;
+    float4 pp = make_float4(0.f, 0.f, 1.f, 0.f), qq = pp;
+    float ce = 0.f;
+    if (v) { pp = P[j]; qq = Q[j]; ce = CE[j]; }
+    float lt, ut;
+    stage1(v, pp, qq, ce, lt, ut);
+    n_und += __popcll(__ballot(lt == -__builtin_inff()));
+    n_sure += __popcll(__ballot(ut < __builtin_inff()));
+    if (ub_insert(ut)) refresh();
+    enqueue(v, lt, j);
+  };
+#endif
   // nodes of up to four tiles: t0 / t1 on lanes 0-31 / 32-63 (first set), t2 / t3 (second set);
   // -1 = none.  Both sets' records are loaded before either is tested.
   auto visit4 = [&](int t0, int t1, int t2, int t3) __attribute__((always_inline)) {
@@ -784,6 +818,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     const bool oka = prefilter(ida, ha, pa, qa, ca);
     const bool okb = prefilter(idb, hb, pb, qb, cb);
     n_q += __popcll(__ballot(oka)) + __popcll(__ballot(okb));
+#if WALK_STAGE1_QUEUE
+    push1(oka, ja);
+    push1(okb, jb);
+    while (n1 >= 64) run_stage1(64);
+#else
     float la, ua, lb, ub;
     stage1(oka, pa, qa, ca, la, ua);
     stage1(okb, pb, qb, cb, lb, ub);
@@ -794,6 +833,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     if (ia || ib2) refresh();
     enqueue(oka, la, ja);
     enqueue(okb, lb, jb);
+#endif
     if (prof) cyc[2] += __builtin_amdgcn_s_memtime() - c0;
   };
   // visit the tiles of super-tile st whose bounds lie in (Tp, min(T, kth)] (pass 0: <= min(T, kth));
@@ -833,6 +873,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   };
   auto flush_queue = [&]() __attribute__((always_inline)) {
     while (qn > 0) visit_queue();
+#if WALK_STAGE1_QUEUE
+    while (n1 > 0) run_stage1(n1 < 64 ? n1 : 64);
+#endif
   };
   // visit the tiles of super-tiles sa (lanes 0-31) and sb (lanes 32-63, -1: none) whose bounds lie in
   // (Tp, min(T, kth)] (STATE: not visited yet and <= min(T, kth)); the super-tiles' LDS bounds become
@@ -1252,7 +1295,10 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   // none, then one coded byte (+ the inside-circle key bracket: on such trees exact keys dominate)
   const int fmt = nsup <= 1280 && !stateless ? WALK_FMT_STATE : (nsup <= w.half_max ? WALK_FMT_HALF : WALK_FMT_CODED);
   const bool brk = fmt == WALK_FMT_CODED;
-  const size_t lds = (fmt == WALK_FMT_STATE ? 2 * sizeof(float) : fmt == WALK_FMT_HALF ? sizeof(__half) : 1) * (size_t)nsup;
+  // (a floor on it caps the walk's waves per CU, leaving room for the main stream's kernels beside it)
+  const size_t lds = std::max<size_t>((size_t)w.lds_floor,
+                                      (fmt == WALK_FMT_STATE ? 2 * sizeof(float) : fmt == WALK_FMT_HALF ? sizeof(__half) : 1) *
+                                          (size_t)nsup);
   const void* kfn = fmt == WALK_FMT_STATE ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false>
                     : fmt == WALK_FMT_HALF ? (const void*)&k_walk_search<WALK_FMT_HALF, false, false>
                                            : (const void*)&k_walk_search<WALK_FMT_CODED, false, true>;

@@ -35,7 +35,7 @@ def timed(sub):
     pl.sort_nodes_batch(sub, exact=False)  # warm: index built for this tree
     best = 1e9
     for _ in range(3):
-        pl.reset_counters()
+        pl.reset_counters()  # the counters below are those of the last repetition
         t0 = time.perf_counter()
         pl.sort_nodes_batch(sub, exact=False)
         best = min(best, time.perf_counter() - t0)
@@ -56,8 +56,10 @@ for tgt in targets:
         w = pl.search_work()
         dc = pl.debug_counters()
         ns = max(1, w["samples"])
+        q = pl.nn_stats()
         line = (f"   {lab:8s} {len(sub):5d} samples: {best * 1e3:7.2f} ms; tiles/sample {w['tiles'] / ns:.0f}, "
-                f"exact keys/sample {w['exact_keys'] / ns:.0f}, overflow records/round {dc[32] / 3:.0f}")
+                f"exact keys/sample {w['exact_keys'] / ns:.0f}, overflow records/round {dc[32]:.0f}; per sample: "
+                f"super visits {q['walk_supers'] / len(sub):.0f}, prefilter passes {q['walk_queued'] / len(sub):.0f}")
         if phases:
             pl.set_option("nn_debug", 2)
             pl.reset_counters()
