@@ -77,6 +77,16 @@ __device__ __forceinline__ float prune_r(float slack) {
 // Survivors are queued per lane; a second pass runs nn_prefilter, the exact Dubins key and
 // feasibleNode on the queue, so lanes stay converged instead of diverging node by node.
 #define NN_QCAP 32
+// block sizes of the commit-path kernels that run beside the lag-2 walk (k_select; the appended-node search):
+// one-wave blocks would fit the single wave slots the walk frees, but measured (round 4, tools/ab_bench.sh)
+// k_select's block size does not matter and one-wave appended-node search blocks (4x the tile staging) cost
+// 3% of cfg3's throughput
+#ifndef CLRRT_SEL_BLK
+#define CLRRT_SEL_BLK 256
+#endif
+#ifndef CLRRT_PATH_BLK
+#define CLRRT_PATH_BLK 256
+#endif
 __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, NnFrame fr, float* __restrict__ pk,
@@ -2572,19 +2582,21 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
                            float* ckey, int* ncand, int* ctie, float* seed) {
   if (count <= 0 || B <= 0) return hipSuccess;
-  const int groups = (B + 255) / 256;
+  // (the seed / merge kernels and the index build run one-wave blocks: they run beside the lag-2 walk, whose
+  // waves fill the CUs and free one slot at a time; priorities order dispatch but do not preempt)
+  const int groups = (B + CLRRT_PATH_BLK - 1) / CLRRT_PATH_BLK;
   int nchunks = (count + 255) / 256;
   const int want = max(1, 2048 / max(1, groups));
   nchunks = max(1, min(nchunks, min(want, max_chunks)));
   int chunk = (count + nchunks - 1) / nchunks;
   chunk = (chunk + 255) & ~255;
   nchunks = (count + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 255) / 256), dim3(256), 0, st, B, p.sort_limit, ckey, ncand, seed);
+  hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, p.sort_limit, ckey, ncand, seed);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(256), 0, st, S, B, nodes + first, count, chunk,
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(CLRRT_PATH_BLK), 0, st, S, B, nodes + first, count, chunk,
                      nchunks, p, fr, pk, pi, seed, nullptr);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
+  hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 63) / 64), dim3(64), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      first, cand, ckey, ncand, ctie);
   LAUNCH_CHECK();
   return hipSuccess;
@@ -2663,7 +2675,7 @@ static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
   size_t bytes = roll_order_scratch_bytes(a.njobs);
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, a.pflag, ppos, a.njobs, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_roll_order, dim3((a.njobs + 255) / 256), dim3(256), 0, st, a.pflag, ppos, a.njobs, a.perm);
+  hipLaunchKernelGGL(k_roll_order, dim3((a.njobs + 63) / 64), dim3(64), 0, st, a.pflag, ppos, a.njobs, a.perm);
   return hipGetLastError();
 }
 
@@ -2700,7 +2712,7 @@ hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, 
   a.lanes_per_wave = lpw;
   const int nb = blocks < (nqueue + 4 * lpw - 1) / (4 * lpw) ? blocks : (nqueue + 4 * lpw - 1) / (4 * lpw);
   if (a.njobs > 0 && a.perm && a.pflag) {  // queue order: the likely-long jobs first
-    hipLaunchKernelGGL(k_roll_flag, dim3((a.njobs + 255) / 256), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_roll_flag, dim3((a.njobs + 63) / 64), dim3(64), 0, st, a);
     LAUNCH_CHECK();
     if ((e = roll_order(st, a)) != hipSuccess) return e;
   } else {
@@ -2732,7 +2744,7 @@ hipError_t launch_rollout(hipStream_t st, int src, const RollArgs& a) {
 }
 
 hipError_t launch_select(hipStream_t st, const SelArgs& a) {
-  hipLaunchKernelGGL(k_select, dim3((a.B + 255) / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_select, dim3((a.B + CLRRT_SEL_BLK - 1) / CLRRT_SEL_BLK), dim3(CLRRT_SEL_BLK), 0, st, a);
   LAUNCH_CHECK();
   return hipSuccess;
 }

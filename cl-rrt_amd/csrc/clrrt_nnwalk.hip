@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) k_walk_tiles(const float4* __restrict__ P
                                                     WalkTile* __restrict__ out) {
   // R = node 0's position in the frame (any fixed point gives a valid bound; the root gives a tight one)
   const float Rx = (float)(nodes[0].x - ox), Ry = (float)(nodes[0].y - oy);
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // one wave per tile
   const int lane = threadIdx.x & 63;
   if (t >= ntiles) return;
   const int b = t * size;
@@ -1222,7 +1222,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   if (incremental) {
     const int n0 = (int)prev->sorted_n, nn = N - n0;
     if (nn > 0) {
-      hipLaunchKernelGGL(k_walk_keys, dim3((nn + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale,
+      hipLaunchKernelGGL(k_walk_keys, dim3((nn + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
                          (uint64_t*)w.keys, w.vals, n0);
       LAUNCH_CHECK3();
       size_t bytes = w.tmp_bytes;
@@ -1241,7 +1241,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
         return e;
     }
   } else {
-    hipLaunchKernelGGL(k_walk_keys, dim3((N + 255) / 256), dim3(256), 0, st, nodes, N, x0, y0, scale,
+    hipLaunchKernelGGL(k_walk_keys, dim3((N + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
                        (uint64_t*)w.keys, w.vals, 0);
     LAUNCH_CHECK3();
     size_t bytes = w.tmp_bytes;
@@ -1253,7 +1253,8 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   w.sorted_x0 = x0;
   w.sorted_y0 = y0;
   w.sorted_scale = scale;
-  hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 255) / 256), dim3(256), 0, st, nodes, N, Npad, w.sids, fr.ox, fr.oy,
+  // one-wave blocks (see launch_nn_delta)
+  hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 63) / 64), dim3(64), 0, st, nodes, N, Npad, w.sids, fr.ox, fr.oy,
                      w.P, w.Q, w.CE, w.ID, w.vals);
   LAUNCH_CHECK3();
   // HEAD[j] = first record of j's run of equal key inputs (inclusive max-scan of dup markers)
@@ -1269,10 +1270,10 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   }
   hipLaunchKernelGGL(k_walk_trun, dim3((ntiles + 255) / 256), dim3(256), 0, st, w.HEAD, w.ID, ntiles, w.trun);
   LAUNCH_CHECK3();
-  hipLaunchKernelGGL(k_walk_tiles, dim3((ntiles + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
+  hipLaunchKernelGGL(k_walk_tiles, dim3(ntiles), dim3(64), 0, st, w.P, w.Q, w.CE, w.ID, ntiles, WALK_TILE,
                      fr.delta, nodes, fr.ox, fr.oy, w.tiles);
   LAUNCH_CHECK3();
-  hipLaunchKernelGGL(k_walk_tiles, dim3((nsup + 3) / 4), dim3(256), 0, st, w.P, w.Q, w.CE, w.ID, nsup,
+  hipLaunchKernelGGL(k_walk_tiles, dim3(nsup), dim3(64), 0, st, w.P, w.Q, w.CE, w.ID, nsup,
                      WALK_TILE * WALK_SUPER, fr.delta, nodes, fr.ox, fr.oy, w.supers);
   LAUNCH_CHECK3();
   return hipSuccess;
