@@ -49,6 +49,15 @@ for tgt in targets:
             break
     n = pl.size()[0]
     print(f"{n / 1e6:6.2f} M nodes (grown in {time.perf_counter() - t_grow:5.1f} s)", flush=True)
+    ab = [x for x in os.environ.get("CLRRT_OPTS_AB", "").split(";") if x]  # option sets timed one after another
+    for kv in ab:
+        for o in kv.split(","):
+            k, v = o.split("=")
+            pl.set_option(k, int(v))
+        best = timed(kinds[0][1])
+        w = pl.search_work()
+        print(f"   [{kv}] mixed: {best * 1e3:7.2f} ms; tiles/sample {w['tiles'] / max(1, w['samples']):.0f}, exact keys/sample "
+              f"{w['exact_keys'] / max(1, w['samples']):.0f}, overflow records {pl.debug_counters()[32]}", flush=True)
     for lab, sub in kinds:
         if phases:
             pl.set_option("nn_debug", 0)
