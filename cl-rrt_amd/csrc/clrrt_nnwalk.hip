@@ -56,7 +56,10 @@ namespace clrrt {
 #define WALK_FMT_HALF 1   // fp16 bound (stateless),
 #define WALK_FMT_CODED 2  // one log-coded byte (stateless; large trees)
 #ifndef WALK_STAGE1_QUEUE
-#define WALK_STAGE1_QUEUE 1
+#define WALK_STAGE1_QUEUE 0  // measured neutral (round 4); off saves 768 B of LDS per wave
+#endif
+#ifndef WALK_HALF_SUPER
+#define WALK_HALF_SUPER 1  // HALF format: keep each super-tile's phase-1 bound in LDS (2 more bytes per super-tile)
 #endif
 #define WALK_TQ 68      // tile stack entries (a super-tile pair adds <= 64 to <= 3 pending)
 #ifndef WALK_APBINS
@@ -517,6 +520,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   constexpr bool STATE = FMT == WALK_FMT_STATE, CODED = FMT == WALK_FMT_CODED;
   extern __shared__ uint8_t s_lb[];  // [nloc] bounds of the super-tiles' remaining tiles (stateless) ...
   __half* s_lbh = (__half*)s_lb;             // ... fp16, rounded down, or (CODED) one log-coded byte
+  __half* s_sh = s_lbh + nloc_max;           // HALF: the super-tiles' own bounds (phase 1), fp16 rounded down
   float* s_lbf = (float*)s_lb;               // STATE: [nloc] float bounds ...
   uint32_t* s_vis = (uint32_t*)(s_lbf + nloc_max);  // ... and [nloc] visited / discarded tile masks
   __shared__ int s_q2[64];  // records past stage 1 (stage 2: exact keys) ...
@@ -915,9 +919,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         s_lbf[lo] = rest;
       }
     } else {
-      float sl = __builtin_inff();
-      if ((lane & 31) == 0 && st >= 0) sl = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
-      const float slb = __shfl(sl, lane & 32, 64);
+      float slb;
+      if constexpr (FMT == WALK_FMT_HALF && WALK_HALF_SUPER) {
+        // the super-tile's own bound, kept from phase 1 (rounded down: still <= every tile's effective bound)
+        slb = st >= 0 ? __half2float(s_sh[lo]) : __builtin_inff();
+      } else {
+        float sl = __builtin_inff();
+        if ((lane & 31) == 0 && st >= 0) sl = walk_lb(sup[st], rsx, rsy, ex, flen_t, dsR);
+        slb = __shfl(sl, lane & 32, 64);
+      }
 #ifdef WALK_CHEAP_STATELESS
       // the distance-only bound first; the full one only for tiles it does not place beyond min(T, kth)
       // (the weaker value still bounds the super-tile's rest)
@@ -987,6 +997,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
         s_vis[t] = 0u;
       } else if constexpr (!CODED) {
         s_lbh[t] = __float2half_rd(lb);
+        if constexpr (WALK_HALF_SUPER) s_sh[t] = s_lbh[t];
       }
       mlb = fminf(mlb, lb);
     }
@@ -1298,7 +1309,9 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   const bool brk = fmt == WALK_FMT_CODED;
   // (a floor on it caps the walk's waves per CU, leaving room for the main stream's kernels beside it)
   const size_t lds = std::max<size_t>((size_t)w.lds_floor,
-                                      (fmt == WALK_FMT_STATE ? 2 * sizeof(float) : fmt == WALK_FMT_HALF ? sizeof(__half) : 1) *
+                                      (fmt == WALK_FMT_STATE ? 2 * sizeof(float)
+                                       : fmt == WALK_FMT_HALF ? (WALK_HALF_SUPER ? 2 : 1) * sizeof(__half)
+                                                              : 1) *
                                           (size_t)nsup);
   const void* kfn = fmt == WALK_FMT_STATE ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false>
                     : fmt == WALK_FMT_HALF ? (const void*)&k_walk_search<WALK_FMT_HALF, false, false>
