@@ -824,14 +824,28 @@ __device__ __forceinline__ double obs_distance(const Roll& r, const DevParams& p
   return best;
 }
 
-// Diagnostics (built with -DCLRRT_ROLL_PROFILE only): wave time per phase of k_roll_run, from the
-// shader clock, accumulated into work counters 32..39.
+// Diagnostics (built with -DCLRRT_ROLL_PROFILE only): time per phase of the rollout kernels, from the
+// shader clock, accumulated into work counters 40..47.  k_rollout (one lane per job) keeps it per lane.
+// k_roll_run keeps it per WAVE (wq: the wave's LDS slot, [0] the last mark, [1 + k] phase k): a mark closes
+// the interval since the previous mark of ANY of the wave's lanes, so a phase that runs on some lanes while
+// the others idle is charged to that phase (round 3's per-lane clocks, read from lane 0, charged everything
+// lane 0 sat out -- 45-80% of the wave time -- to "loop top").
 struct PhaseClk {
   uint64_t last;
   uint64_t t[8];
+  uint64_t* wq = nullptr;
   __device__ __forceinline__ void mark(int k) {
 #ifdef CLRRT_ROLL_PROFILE
     const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (wq) {
+      const uint64_t m = __ballot(1);
+      if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) {
+        wq[1 + k] += now - wq[0];
+        wq[0] = now;
+      }
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
     t[k] += now - last;
     last = now;
 #endif
@@ -1433,8 +1447,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   RollSrc src;
   PhaseClk pclk{};
 #ifdef CLRRT_ROLL_PROFILE
+  __shared__ uint64_t s_phase[4][9];  // per wave of the block: last mark, phases 0..7
   PhaseClk* pc = &pclk;
-  pclk.last = __builtin_amdgcn_s_memtime();
+  pclk.wq = s_phase[threadIdx.x >> 6];
+  if ((threadIdx.x & 63) == 0) {
+    pclk.wq[0] = __builtin_amdgcn_s_memtime();
+    for (int q = 1; q < 9; q++) pclk.wq[q] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
 #else
   PhaseClk* pc = nullptr;
 #endif
@@ -1722,7 +1742,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   }
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && lane == 0)
-    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.t[q]);
+    for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.wq[1 + q]);
   if (a.ctr) {
     // load balance: wave lifetimes (sum, max), the longest chain (max), waves; the queue drain (first
     // step after a fetch found it empty) of the wave, the busiest lane's steps after it
