@@ -392,7 +392,11 @@ def test_pipelined_batch_rounds_identical():
                 dict(nn_lag=2, stream_prio=0), dict(roll_priority=0, roll_blocks=512),
                 dict(roll_coop=0), dict(rows_deferred=0),
                 dict(nn_walk_double=0), dict(nn_walk_budget_tiles=0, nn_walk_budget_keys=0),
-                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5)]
+                dict(nn_walk_budget_tiles=1, nn_walk_budget_keys=1, nn_walk_chunks=5),
+                # scheduling / placement options (CU-masked rollout stream, walk streams off 2/8 of the CUs,
+                # 32 job lanes per wave, an LDS floor per walk wave) and the large-tree walk format
+                dict(cu_split=2), dict(walk_cu_reserve=2), dict(roll_lanes=32), dict(nn_walk_lds_floor=16384),
+                dict(nn_walk_stateless=1, nn_walk_half_max=0)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
@@ -412,6 +416,26 @@ def test_pipelined_batch_rounds_identical():
     assert trees[0][2] > 20000
     for t in trees[1:]:
         assert trees[0][0] == t[0] and trees[0][1] == t[1]
+
+
+@pytest.mark.gpu
+def test_exact_min_width_identical():
+    """EXACT trees do not depend on the speculation width (option exact_min_width): the committed prefix of
+    every round is the reference's sequential order, whatever the number of samples speculated."""
+    mode, obs = _scene("obb200")
+    trees = []
+    for width in (8, 64, 1):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 22,
+                           max_batch=256)
+        pl.set_option("exact_min_width", width)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(21), n_iters=300, mode=clrrt.CLRRT_MODE_EXACT, batch=256)
+        assert st["iterations"] == 300
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes()))
+        pl.close()
+    assert trees[0] == trees[1] == trees[2]
 
 
 @pytest.mark.gpu
