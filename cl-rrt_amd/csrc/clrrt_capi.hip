@@ -108,6 +108,12 @@ struct clrrt_ctx {
   int nnw_bud_tiles = 3072, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
+  // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
+  // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
+  // beside the lag-2 walk (the commit's k_select waited ~1.2 ms per round for slots behind ~1 ms walk waves)
+  // and balances the walk's own tail: cfg3 1.164 -> 1.203 M nodes/s (round 4 sweep: 1024 / 1536 / 2048 /
+  // 2560 waves -> 1.07 / 1.17 / 1.202 / 1.203 M), the 16 M-node search alone 62 -> 58 ms at 3072
+  int nnw_waves = -1;
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
   // pipelined rounds: a second index set, so the next round's index is built while the side stream's
@@ -501,7 +507,7 @@ static void free_all(clrrt_ctx* c) {
                   c->ncand3, c->ctie3, c->nnw3.keys, c->nnw3.keys2, c->nnw3.vals, c->nnw3.vals2, c->nnw3.tmp, c->nnw3.P,
                   c->nnw3.Q, c->nnw3.CE, c->nnw3.ID, c->nnw3.tiles, c->nnw3.supers, c->nnw3.sorder, c->nnw3.HEAD,
                   c->nnw3.ovf_n, c->nnw3.ovf, c->nnw3.pk, c->nnw3.pi, c->nnw3.skeys, c->nnw3.sids,
-                  c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun};
+                  c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun, c->nnw.wctr, c->nnw_alt.wctr, c->nnw3.wctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
   void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal};
@@ -1236,6 +1242,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
   else if (k == "nn_walk_lds_floor" && value >= 0 && value <= 65536) c->nnw_lds_floor = (int)value;
+  else if (k == "nn_walk_waves" && value >= -1 && value <= 1 << 20) c->nnw_waves = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
   else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
@@ -1372,6 +1379,7 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
   HIPC(c, dalloc(&w.supers, walk_super_count(c->cap.max_nodes) + 1));
   HIPC(c, dalloc(&w.ovf_n, 1));
   HIPC(c, dalloc(&w.ovf, kWalkMaxOver));
+  HIPC(c, dalloc(&w.wctr, 8));
   HIPC(c, dalloc(&w.pk, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
   HIPC(c, dalloc(&w.pi, (int64_t)kWalkMaxOver * kWalkMaxChunks * 11));
   HIPC(c, dalloc(&w.skeys, Mp));
@@ -1394,6 +1402,7 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.nch = c->nnw_chunks;
   w.half_max = c->nnw_half_max;
   w.lds_floor = c->nnw_lds_floor;
+  w.waves = c->nnw_waves < 0 ? 10 * c->n_cu : c->nnw_waves;
   return alloc_walk(c, w);
 }
 static int ensure_walk(clrrt_ctx* c) { return ensure_walk_set(c, c->nnw); }

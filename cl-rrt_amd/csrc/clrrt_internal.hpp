@@ -193,6 +193,8 @@ struct WalkBufs {
   int bud_tiles, bud_ex, max_over, nch;
   int half_max = 4096;  // fp16 LDS bounds up to this many super-tiles, coded bytes (+ inside bracket) beyond
   int lds_floor = 0;    // bytes of LDS each walk wave reserves at least (caps the walk's waves per CU)
+  int waves = 0;        // > 0: a persistent walk grid of this many waves (samples from per-XCD counters)
+  int* wctr = nullptr;  // [8] the per-XCD sample counters
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists

@@ -502,7 +502,7 @@ __device__ __forceinline__ int lc_le(float v) {  // the largest code c with lc_d
 // sample's true list precedes that 11th entry, each wave's list is exact over its super-tiles, so the
 // merged list equals the walk's (and the brute force's).  Records beyond max_over: the walk goes on.
 template <int FMT, bool SPLIT, bool BRK>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_WALK_WAVES))) k_walk_search(const clrrt_sample* __restrict__ S, int B,
+__device__ __forceinline__ void walk_one(const clrrt_sample* __restrict__ S, int B,
                                                     const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                     const float4* __restrict__ Q, const float* __restrict__ CE,
                                                     const int* __restrict__ ID, const int* __restrict__ HEAD,
@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
                                                     unsigned long long* __restrict__ stats, int bud_tiles,
                                                     int bud_ex, int* __restrict__ ovf_n, int4* __restrict__ ovf,
                                                     int max_over, int nch, float* __restrict__ pk,
-                                                    int* __restrict__ pi, int nloc_max) {
+                                                    int* __restrict__ pi, int nloc_max, int s, int ch, int nloc, float kb, int ib, int o_sp) {
   // LDS is indexed by the wave's local super-tile index l (super-tile gst(l))
   constexpr bool STATE = FMT == WALK_FMT_STATE, CODED = FMT == WALK_FMT_CODED;
   extern __shared__ uint8_t s_lb[];  // [nloc] bounds of the super-tiles' remaining tiles (stateless) ...
@@ -531,26 +531,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   __shared__ int s_tq[WALK_TQ];    // tile queue: tiles taken by the super-tile visits ...
   __shared__ float s_tb[WALK_TQ];  // ... and their bounds
   const int lane = threadIdx.x;
-  int s, ch = 0, nloc = nsup;
-  float kb = __builtin_inff();  // SPLIT: the pairs sought precede (kb, ib)
-  int ib = 0x7fffffff;
-  if constexpr (SPLIT) {
-    const int o = (int)blockIdx.x / nch;
-    ch = (int)blockIdx.x % nch;
-    if (o >= min(*ovf_n, max_over)) return;
-    const int4 rec = ovf[o];
-    s = rec.x;
-    kb = __int_as_float(rec.y);
-    ib = rec.z;
-    nloc = ch < nsup ? (nsup - ch + nch - 1) / nch : 0;
-  } else {
-    // XCD-aware: consecutive blocks go to the 8 XCDs in turn; XCD x takes the x-th eighth of the
-    // place-ordered samples, so its L2 holds the tree region those samples search
-    const int per = (B + 7) >> 3;
-    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (t >= B) return;
-    s = sorder[t];
-  }
+  // SPLIT: the pairs sought precede (kb, ib); ch / nloc: the wave's interleaved super-tile subset
   auto gst = [&](int l) -> int { return SPLIT ? ch + l * nch : l; };  // super-tile of local index l
   const double sx = S[s].x, sy = S[s].y;
   const bool ex = S[s].explore != 0;
@@ -1071,7 +1052,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
   }
   // 3. output (k_nn_merge's format); SPLIT: the wave's partial list
   if constexpr (SPLIT) {
-    const int o = (int)blockIdx.x / nch;
+    const int o = o_sp;
     if (lane < NN_K) {
       pk[((size_t)o * nch + ch) * NN_K + lane] = lk;
       pi[((size_t)o * nch + ch) * NN_K + lane] = li;
@@ -1080,6 +1061,63 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_W
     walk_emit(lk, li, lane, s, p.sort_limit, cand, ckey, ncand, ctie);
   }
   flush_stats();
+}
+
+// One wave per sample (or, with wctr, a persistent grid of waves taking samples from per-XCD counters: the
+// walk then holds a fixed number of wave slots and leaves the rest to the kernels beside it); SPLIT: the
+// overflow records' waves.
+template <int FMT, bool SPLIT, bool BRK, bool PERS = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CLRRT_WALK_WAVES))) k_walk_search(const clrrt_sample* __restrict__ S, int B,
+                                                    const NnRec* __restrict__ nodes, const float4* __restrict__ P,
+                                                    const float4* __restrict__ Q, const float* __restrict__ CE,
+                                                    const int* __restrict__ ID, const int* __restrict__ HEAD,
+                                                    const int2* __restrict__ trun,
+                                                    const WalkTile* __restrict__ tiles, int ntiles,
+                                                    const WalkTile* __restrict__ sup, int nsup, DevParams p,
+                                                    NnFrame fr, int* __restrict__ cand, float* __restrict__ ckey,
+                                                    int* __restrict__ ncand, int* __restrict__ ctie,
+                                                    const int* __restrict__ sorder,
+                                                    unsigned long long* __restrict__ stats, int bud_tiles,
+                                                    int bud_ex, int* __restrict__ ovf_n, int4* __restrict__ ovf,
+                                                    int max_over, int nch, float* __restrict__ pk,
+                                                    int* __restrict__ pi, int nloc_max, int* __restrict__ wctr) {
+  if constexpr (SPLIT) {
+    const int o = (int)blockIdx.x / nch;
+    const int ch = (int)blockIdx.x % nch;
+    if (o >= min(*ovf_n, max_over)) return;
+    const int4 rec = ovf[o];
+    const int nloc = ch < nsup ? (nsup - ch + nch - 1) / nch : 0;
+    walk_one<FMT, SPLIT, BRK>(S, B, nodes, P, Q, CE, ID, HEAD, trun, tiles, ntiles, sup, nsup, p, fr, cand, ckey, ncand, ctie, sorder, stats, bud_tiles, bud_ex, ovf_n, ovf, max_over, nch, pk, pi, nloc_max, rec.x, ch, nloc, __int_as_float(rec.y), rec.z, o);
+  } else {
+    // XCD-aware: consecutive blocks go to the 8 XCDs in turn; XCD x takes the x-th eighth of the
+    // place-ordered samples, so its L2 holds the tree region those samples search (persistent waves then
+    // help the other XCDs' eighths)
+    const int per = (B + 7) >> 3;
+    const int x0 = (int)(blockIdx.x & 7);
+    if constexpr (!PERS) {
+      const int t = x0 * per + (int)(blockIdx.x >> 3);
+      if (t >= B) return;
+      walk_one<FMT, SPLIT, BRK>(S, B, nodes, P, Q, CE, ID, HEAD, trun, tiles, ntiles, sup, nsup, p, fr, cand, ckey, ncand,
+                                ctie, sorder, stats, bud_tiles, bud_ex, ovf_n, ovf, max_over, nch, pk, pi, nloc_max,
+                                sorder[t], 0, nsup, __builtin_inff(), 0x7fffffff, 0);
+      return;
+    }
+    int k = 0;
+    for (;;) {
+      int t = -1;
+      while (k < 8) {
+        const int x = (x0 + k) & 7;
+        int i = 0;
+        if (threadIdx.x == 0) i = atomicAdd(&wctr[x], 1);
+        i = __shfl(i, 0, 64);
+        if (i < per && x * per + i < B) { t = x * per + i; break; }
+        k++;
+      }
+      if (t < 0) break;
+      walk_one<FMT, SPLIT, BRK>(S, B, nodes, P, Q, CE, ID, HEAD, trun, tiles, ntiles, sup, nsup, p, fr, cand, ckey, ncand, ctie, sorder, stats, bud_tiles, bud_ex, ovf_n, ovf, max_over, nch, pk, pi, nloc_max, sorder[t], 0, nsup, __builtin_inff(), 0x7fffffff, 0);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
 }
 
 // The 11 smallest (key, node) pairs of an overflow sample's nch partial lists (one wave per record);
@@ -1313,9 +1351,14 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                        : fmt == WALK_FMT_HALF ? (WALK_HALF_SUPER ? 2 : 1) * sizeof(__half)
                                                               : 1) *
                                           (size_t)nsup);
-  const void* kfn = fmt == WALK_FMT_STATE ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false>
-                    : fmt == WALK_FMT_HALF ? (const void*)&k_walk_search<WALK_FMT_HALF, false, false>
-                                           : (const void*)&k_walk_search<WALK_FMT_CODED, false, true>;
+  const bool pers_k = w.waves > 0 && w.wctr;
+  const void* kfn =
+      fmt == WALK_FMT_STATE ? (pers_k ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false, true>
+                                      : (const void*)&k_walk_search<WALK_FMT_STATE, false, false, false>)
+      : fmt == WALK_FMT_HALF ? (pers_k ? (const void*)&k_walk_search<WALK_FMT_HALF, false, false, true>
+                                       : (const void*)&k_walk_search<WALK_FMT_HALF, false, false, false>)
+                             : (pers_k ? (const void*)&k_walk_search<WALK_FMT_CODED, false, true, true>
+                                       : (const void*)&k_walk_search<WALK_FMT_CODED, false, true, false>);
   if (lds > 64 * 1024) {
     e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1332,14 +1375,28 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
   if (e != hipSuccess) return e;
   const int bt = split ? w.bud_tiles : 0, be = split ? w.bud_ex : 0;
-#define WALK_LAUNCH(F, BK)                                                                                       \
-  hipLaunchKernelGGL((k_walk_search<F, false, BK>), dim3(((B + 7) >> 3) * 8), dim3(64), lds, st, S, B, nodes, w.P, \
+  // persistent waves (option nn_walk_waves): a fixed grid taking samples from per-XCD counters
+  const bool pers = pers_k;
+  const int grid = pers ? std::min(((B + 7) >> 3) * 8, std::max(8, w.waves & ~7)) : ((B + 7) >> 3) * 8;
+  if (pers) {
+    e = hipMemsetAsync(w.wctr, 0, 8 * sizeof(int), st);
+    if (e != hipSuccess) return e;
+  }
+  int* wctr = pers ? w.wctr : nullptr;
+#define WALK_LAUNCH1(F, BK, PS)                                                                                  \
+  hipLaunchKernelGGL((k_walk_search<F, false, BK, PS>), dim3(grid), dim3(64), lds, st, S, B, nodes, w.P,          \
                      w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,  \
-                     w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup)
+                     w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup, wctr)
+#define WALK_LAUNCH(F, BK)            \
+  do {                                \
+    if (pers) WALK_LAUNCH1(F, BK, true);  \
+    else WALK_LAUNCH1(F, BK, false);  \
+  } while (0)
   if (fmt == WALK_FMT_STATE) WALK_LAUNCH(WALK_FMT_STATE, false);
   else if (fmt == WALK_FMT_HALF) WALK_LAUNCH(WALK_FMT_HALF, false);
   else WALK_LAUNCH(WALK_FMT_CODED, true);
 #undef WALK_LAUNCH
+#undef WALK_LAUNCH1
   LAUNCH_CHECK3();
   if (split) {
     // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
@@ -1355,7 +1412,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   hipLaunchKernelGGL((k_walk_search<WALK_FMT_STATE, true, BK>), dim3(w.max_over * w.nch), dim3(64),               \
                      2 * sizeof(float) * (size_t)nl, st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, \
                      ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf,  \
-                     w.max_over, w.nch, w.pk, w.pi, nl)
+                     w.max_over, w.nch, w.pk, w.pi, nl, nullptr)
     if (brk) WALK_SPLIT(true);
     else WALK_SPLIT(false);
 #undef WALK_SPLIT

@@ -429,7 +429,7 @@ int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
  * persistent waves with a job queue, default; 0: one lane per candidate), "roll_blocks" (persistent
  * blocks of 256 lanes; 0: by tree size), "nn_walk_min" (trees of at least this many nodes use the
  * walk search, default 8192; below it the brute force), "nn_walk_stateless", "nn_walk_budget_tiles",
- * "nn_walk_budget_keys", "nn_walk_chunks", "nn_walk_max_over", "nn_walk_half_max", "nn_walk_double", "nn_pipeline",
+ * "nn_walk_budget_keys", "nn_walk_chunks", "nn_walk_max_over", "nn_walk_half_max", "nn_walk_waves", "nn_walk_lds_floor", "nn_walk_double", "nn_pipeline",
  * "nn_lag" (0: by query length, 1, 2), "nn_exact_fused", "nn_debug" (diagnostics; changes results),
  * "roll_priority", "roll_coop", "roll_spread", "roll_lanes", "rows_deferred", "exact_min_width",
  * "cu_split", "walk_cu_reserve", "stream_prio", "side_priority" (see clrrt_capi.hip). */

@@ -48,6 +48,8 @@ def _nn_strategy(pl, name):
     coded = "coded" in name
     pl.set_option("nn_walk_stateless", name.endswith("stateless") or coded)
     pl.set_option("nn_walk_half_max", 0 if coded else 4096)
+    # 'persistent': a fixed grid of 1024 walk waves taking samples from per-XCD counters
+    pl.set_option("nn_walk_waves", 1024 if "persistent" in name else 0)  # others: one wave per sample
     split = name.startswith("walk_split")
     pl.set_option("nn_walk_budget_tiles", 1 if split else 2048)
     pl.set_option("nn_walk_budget_keys", 1 if split else 4096)
@@ -359,7 +361,8 @@ def test_walk_matches_brute_force_large_tree():
     smp = list(clrrt.Rng(33).draw_samples(pl.params, 16384))
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
-    for strategy in ("walk", "walk_stateless", "walk_coded", "walk_split_coded"):
+    for strategy in ("walk", "walk_stateless", "walk_coded", "walk_split_coded", "walk_persistent",
+                     "walk_coded_persistent"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
@@ -396,7 +399,7 @@ def test_pipelined_batch_rounds_identical():
                 # scheduling / placement options (CU-masked rollout stream, walk streams off 2/8 of the CUs,
                 # 32 job lanes per wave, an LDS floor per walk wave) and the large-tree walk format
                 dict(cu_split=2), dict(walk_cu_reserve=2), dict(roll_lanes=32), dict(nn_walk_lds_floor=16384),
-                dict(nn_walk_stateless=1, nn_walk_half_max=0)]
+                dict(nn_walk_stateless=1, nn_walk_half_max=0), dict(nn_walk_waves=0), dict(nn_walk_waves=512)]
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
