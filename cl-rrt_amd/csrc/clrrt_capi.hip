@@ -112,7 +112,8 @@ struct clrrt_ctx {
   // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
   // beside the lag-2 walk (the commit's k_select waited ~1.2 ms per round for slots behind ~1 ms walk waves)
   // and balances the walk's own tail: cfg3 1.164 -> 1.203 M nodes/s (round 4 sweep: 1024 / 1536 / 2048 /
-  // 2560 waves -> 1.07 / 1.17 / 1.202 / 1.203 M), the 16 M-node search alone 62 -> 58 ms at 3072
+  // 2560 waves -> 1.07 / 1.17 / 1.202 / 1.203 M), the 16 M-node search alone 62 -> 58 ms at 3072; the default
+  // grid is used for batches of >= 4x its waves (below, one wave per sample)
   int nnw_waves = -1;
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
@@ -1403,6 +1404,9 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.half_max = c->nnw_half_max;
   w.lds_floor = c->nnw_lds_floor;
   w.waves = c->nnw_waves < 0 ? 10 * c->n_cu : c->nnw_waves;
+  // the default grid serves batches of >= 4x its waves (cfg2's 4096-sample rounds run 4% faster with one
+  // wave per sample: 1.237 vs 1.188 M nodes/s)
+  w.waves_min_batch = c->nnw_waves < 0 ? 4 * w.waves : 0;
   return alloc_walk(c, w);
 }
 static int ensure_walk(clrrt_ctx* c) { return ensure_walk_set(c, c->nnw); }

@@ -194,6 +194,7 @@ struct WalkBufs {
   int half_max = 4096;  // fp16 LDS bounds up to this many super-tiles, coded bytes (+ inside bracket) beyond
   int lds_floor = 0;    // bytes of LDS each walk wave reserves at least (caps the walk's waves per CU)
   int waves = 0;        // > 0: a persistent walk grid of this many waves (samples from per-XCD counters)
+  int waves_min_batch = 0;  // ... used for batches of at least this many samples
   int* wctr = nullptr;  // [8] the per-XCD sample counters
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)

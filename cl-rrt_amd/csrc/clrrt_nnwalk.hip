@@ -1351,7 +1351,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                        : fmt == WALK_FMT_HALF ? (WALK_HALF_SUPER ? 2 : 1) * sizeof(__half)
                                                               : 1) *
                                           (size_t)nsup);
-  const bool pers_k = w.waves > 0 && w.wctr;
+  const bool pers_k = w.waves > 0 && w.wctr && B >= w.waves_min_batch;
   const void* kfn =
       fmt == WALK_FMT_STATE ? (pers_k ? (const void*)&k_walk_search<WALK_FMT_STATE, false, false, true>
                                       : (const void*)&k_walk_search<WALK_FMT_STATE, false, false, false>)
