@@ -362,7 +362,7 @@ def test_walk_matches_brute_force_large_tree():
     _nn_strategy(pl, "brute")
     ids_b, keys_b = pl.sort_nodes_batch(smp, exact=False)
     for strategy in ("walk", "walk_stateless", "walk_coded", "walk_split_coded", "walk_persistent",
-                     "walk_coded_persistent"):
+                     "walk_coded_persistent", "walk_split_persistent"):
         _nn_strategy(pl, strategy)
         ids_g, keys_g = pl.sort_nodes_batch(smp, exact=False)
         print(f"tree {n_nodes} nodes; {strategy} lists equal: {np.array_equal(ids_b, ids_g)}")
