@@ -78,6 +78,35 @@ def parse():
     return ap.parse_args()
 
 
+def walk_wave_state(config):
+    """Hardware view of the walk search (verdict item 2): how the main k_walk_search grid's wave time splits
+    into issuing instructions, parked on s_waitcnt (memory / LDS) and issue stalls, from the newest committed SQ
+    pass of this config (profiles/r*_<config>_walk_sq.json, tools/pmc_walk_bench.sh; the counters cannot be
+    collected inside bench.py).  Returns a dict or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_walk_sq.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        tot = {}
+        for k, v in d.items():
+            # the main grid: k_walk_search<FMT, SPLIT = false, ...>
+            if k.startswith("void clrrt::k_walk_search<") and k.split(",")[1].strip() == "false":
+                for c, x in v["total"].items():
+                    tot[c] = tot.get(c, 0.0) + x
+        wc = tot.get("SQ_WAVE_CYCLES", 0.0)
+        if wc <= 0:
+            return None
+        return {"kernel": "k_walk_search (main grid)", "bound": "latency: wave time parked on memory / LDS waits",
+                "frac": tot["SQ_ACTIVE_INST_ANY"] / wc, "unit": "fraction of wave time issuing",
+                "parked_frac": tot["SQ_WAIT_ANY"] / wc, "issue_stall_frac": tot["SQ_WAIT_INST_ANY"] / wc,
+                "valu_insts_per_wave": tot["SQ_INSTS_VALU"] / max(1.0, tot["SQ_WAVES"]),
+                "source": f"{os.path.basename(files[-1])} ({d.get('_build', 'unrecorded build')})"}
+    except (KeyError, OSError, ValueError, IndexError):
+        return None
+
+
 def measured_traffic(config):
     """HBM bytes per rollout launch from the committed rocprofv3 PMC passes of THIS config
     (profiles/r*_<config>_pmc_{fetch,write}.json: FETCH_SIZE and WRITE_SIZE collected in separate runs,
@@ -497,6 +526,9 @@ def main():
             "note": "outcome 0 empty, 1 all erased, 2 committed path collides, 3 re-initialised from the path"}
     if sync_line:
         line["batch_sync"] = sync_line
+    ww = walk_wave_state(args.config)
+    if ww:
+        line["roofline_walk"] = ww
     if exact_line:
         line["exact_mode"] = exact_line
     if cpu_line:
