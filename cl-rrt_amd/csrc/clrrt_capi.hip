@@ -106,6 +106,9 @@ struct clrrt_ctx {
   // "nn_walk_max_over" records <= 2048); defaults from the cfg3 bench sweeps (round 3
   // with lag 2: 3072 tiles 1.039 vs 2048 1.031 M nodes/s, 8192 keys 1.008, 12 chunks 1.030)
   int nnw_bud_tiles = 3072, nnw_bud_ex = 4096, nnw_chunks = 16, nnw_max_over = 1024;
+  // "nn_walk_max_over" unset: 1024 records, 2048 on trees of >= 6 Mi nodes (at 8 M nodes 1024 records ran out
+  // and the samples past them searched alone: 31.7 -> 24.1 ms per 16384-sample round, profiles/r04u)
+  bool nnw_max_over_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
@@ -1245,7 +1248,10 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_lds_floor" && value >= 0 && value <= 65536) c->nnw_lds_floor = (int)value;
   else if (k == "nn_walk_waves" && value >= -1 && value <= 1 << 20) c->nnw_waves = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
-  else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) c->nnw_max_over = (int)value;
+  else if (k == "nn_walk_max_over" && value >= 1 && value <= kWalkMaxOver) {
+    c->nnw_max_over = (int)value;
+    c->nnw_max_over_set = true;
+  }
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
@@ -1399,7 +1405,7 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   // sweeps: 4096 best at <= 1.6 M nodes, 8192 at 4.7 M, where 4096 overflows more samples than there
   // are records)
   w.bud_ex = c->nnw_bud_ex > 0 ? (int)std::max<int64_t>(c->nnw_bud_ex, c->n_nodes >> 9) : 0;
-  w.max_over = c->nnw_max_over;
+  w.max_over = c->nnw_max_over_set || c->n_nodes < (6 << 20) ? c->nnw_max_over : kWalkMaxOver;
   w.nch = c->nnw_chunks;
   w.half_max = c->nnw_half_max;
   w.lds_floor = c->nnw_lds_floor;
