@@ -109,6 +109,9 @@ struct clrrt_ctx {
   // "nn_walk_max_over" unset: 1024 records, 2048 on trees of >= 6 Mi nodes (at 8 M nodes 1024 records ran out
   // and the samples past them searched alone: 31.7 -> 24.1 ms per 16384-sample round, profiles/r04u)
   bool nnw_max_over_set = false;
+  // "nn_walk_budget_tiles" unset: max(3072, N / 2048) tiles (16 M nodes: 3072 overflowed 2048 samples per
+  // round, 8192 -> 45.6 vs 58-59 ms; 8 M: 3072 stays best, 25.8 vs 29.9 ms at 8192, profiles/r04as)
+  bool nnw_bud_tiles_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
@@ -1242,7 +1245,10 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   if (k == "roll_persistent") c->roll_persistent = value != 0;
   else if (k == "nn_walk_min" && value >= 0) c->nnw_min_nodes = value;
   else if (k == "nn_walk_stateless") c->nnw_stateless = value != 0;
-  else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) c->nnw_bud_tiles = (int)value;
+  else if (k == "nn_walk_budget_tiles" && value >= 0 && value < INT_MAX) {
+    c->nnw_bud_tiles = (int)value;
+    c->nnw_bud_tiles_set = true;
+  }
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
   else if (k == "nn_walk_lds_floor" && value >= 0 && value <= 65536) c->nnw_lds_floor = (int)value;
@@ -1400,7 +1406,9 @@ static int alloc_walk(clrrt_ctx* c, WalkBufs& w) {
 
 // Walk-search configuration of a set (+ its buffers on first use).
 static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
-  w.bud_tiles = c->nnw_bud_tiles;
+  w.bud_tiles = c->nnw_bud_tiles_set || c->nnw_bud_tiles == 0
+                    ? c->nnw_bud_tiles
+                    : (int)std::max<int64_t>(c->nnw_bud_tiles, c->n_nodes >> 11);
   // the exact-key budget grows with the tree (denser trees: more near-tied keys per sample; the cfg3
   // sweeps: 4096 best at <= 1.6 M nodes, 8192 at 4.7 M, where 4096 overflows more samples than there
   // are records)
