@@ -78,17 +78,57 @@ def parse():
     return ap.parse_args()
 
 
+def source_fingerprint():
+    """sha256 (16 hex) of the engine's sources (cl-rrt_amd/csrc, include/clrrt.h): the build a committed PMC pass
+    was collected on records it as "_src" (tools/summarize_pmc.py), so the bench line can name a pass of THIS
+    build (the GPU box has no git history to compare commits against)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "cl-rrt_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "cl-rrt_amd", "csrc", "*.hpp")) + [os.path.join(ROOT, "include", "clrrt.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _tag_key(path):
+    """Profile tags sort by round, then by suffix length, then alphabetically: r04q < r04z < r04aa < r04ah."""
+    import re
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
+def pick_profile(paths, need=None):
+    """The committed pass of the current sources if there is one (its "_src" field), else the newest by tag.
+    Returns (path, json, same_build) or (None, None, False).  need(path) filters candidates."""
+    fp = source_fingerprint()
+    cands = sorted((p for p in paths if need is None or need(p)), key=_tag_key)
+    loaded = []
+    for p in cands:
+        try:
+            loaded.append((p, json.load(open(p))))
+        except (OSError, ValueError):
+            pass
+    for p, d in reversed(loaded):
+        if d.get("_src") == fp:
+            return p, d, True
+    if loaded:
+        return loaded[-1][0], loaded[-1][1], False
+    return None, None, False
+
+
 def walk_wave_state(config):
     """Hardware view of the walk search (verdict item 2): how the main k_walk_search grid's wave time splits
     into issuing instructions, parked on s_waitcnt (memory / LDS) and issue stalls, from the newest committed SQ
     pass of this config (profiles/r*_<config>_walk_sq.json, tools/pmc_walk_bench.sh; the counters cannot be
     collected inside bench.py).  Returns a dict or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_walk_sq.json")))
-    if not files:
+    path, d, same = pick_profile(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_walk_sq.json")))
+    if not path:
         return None
     try:
-        d = json.load(open(files[-1]))
         tot = {}
         for k, v in d.items():
             # the main grid: k_walk_search<FMT, SPLIT = false, ...>
@@ -102,7 +142,8 @@ def walk_wave_state(config):
                 "frac": tot["SQ_ACTIVE_INST_ANY"] / wc, "unit": "fraction of wave time issuing",
                 "parked_frac": tot["SQ_WAIT_ANY"] / wc, "issue_stall_frac": tot["SQ_WAIT_INST_ANY"] / wc,
                 "valu_insts_per_wave": tot["SQ_INSTS_VALU"] / max(1.0, tot["SQ_WAVES"]),
-                "source": f"{os.path.basename(files[-1])} ({d.get('_build', 'unrecorded build')})"}
+                "source": f"{os.path.basename(path)} ({d.get('_build', 'unrecorded build')})",
+                "same_build": same}
     except (KeyError, OSError, ValueError, IndexError):
         return None
 
@@ -114,14 +155,13 @@ def measured_traffic(config):
     both files is used and named in the note.  Returns (bytes or None, note)."""
     import glob
     prof = os.path.join(ROOT, "profiles")
-    fetch = sorted(glob.glob(os.path.join(prof, f"r*_{config}_pmc_fetch.json")))
     write = {os.path.basename(w).split("_")[0]: w for w in glob.glob(os.path.join(prof, f"r*_{config}_pmc_write.json"))}
-    fetch = [f for f in fetch if os.path.basename(f).split("_")[0] in write]
-    if not fetch:
+    fpath, f, same = pick_profile(glob.glob(os.path.join(prof, f"r*_{config}_pmc_fetch.json")),
+                                  need=lambda p: os.path.basename(p).split("_")[0] in write)
+    if not fpath:
         return None, f"no PMC profile committed for {config}"
-    tag = os.path.basename(fetch[-1]).split("_")[0]
+    tag = os.path.basename(fpath).split("_")[0]
     try:
-        f = json.load(open(fetch[-1]))
         w = json.load(open(write[tag]))
 
         def per_dispatch(summary, prefix, counter):
@@ -143,7 +183,8 @@ def measured_traffic(config):
                 if name.endswith("k_roll_run"):
                     raise
         build = f.get("_build", "unrecorded build")
-        return kb * 1024.0, (f"{os.path.basename(fetch[-1])} + {os.path.basename(write[tag])} ({build}): "
+        which = "this build's sources" if same else "an EARLIER build (no pass of these sources is committed)"
+        return kb * 1024.0, (f"{os.path.basename(fpath)} + {os.path.basename(write[tag])} ({build}; {which}): "
                              "(2 x FETCH_SIZE [gfx950 half-count correction] + WRITE_SIZE) KiB per launch")
     except (KeyError, OSError, ValueError) as e:
         return None, f"PMC profile unreadable: {e}"
@@ -313,7 +354,7 @@ def main():
         # one code path for 1 and N GPUs: clrrt_expand runs the sharded rounds itself (this rank's slice of
         # every round, lag-2 pipeline, deferred samples) and calls back once per round for the all-gather
         from clrrt import dist as cdist
-        ex = cdist.ShardExchange(pl, cdist.exchange_capacity(B_rank, defer), "cuda")
+        ex = cdist.ShardExchange(pl, cdist.exchange_capacity(B_rank, defer), "cuda", slice_size=B_rank)
 
     replanning = bool(cfg.get("replan"))
     if replanning:

@@ -103,12 +103,10 @@ def lib():
                              "(or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            if os.environ.get("CLRRT_ABI_ANY") and not hasattr(L, name):  # (bisection builds)
-                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.clrrt_abi_version() != abi.CLRRT_ABI_VERSION and not os.environ.get("CLRRT_ABI_ANY"):  # (bisection builds)
+        if L.clrrt_abi_version() != abi.CLRRT_ABI_VERSION:
             raise ClrrtError(f"{LIB_PATH}: ABI version {L.clrrt_abi_version()} != {abi.CLRRT_ABI_VERSION}; rebuild")
         _lib = L
     return _lib

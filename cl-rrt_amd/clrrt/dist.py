@@ -20,9 +20,11 @@ class RoundExchange:
     ranks); clrrt_round_eval writes
     this rank's records from row 1 on (`records_ptr`).  One all-gather moves header + the first `bound`
     record rows of every rank, so no count exchange (and no host sync) precedes the data; the headers
-    are read back once afterwards.  `bound` adapts to 1.25x the largest count seen; a round whose count
-    exceeds it (rare) moves the excess with a second all-gather.  gloo (CPU rehearsal of the path)
-    stages device buffers through the host.
+    are read back once afterwards (the engine appends the union, so it needs the counts on the host).
+    `bound` starts at `first_bound` (the sharded expansion passes this rank's slice size: a round commits
+    about 0.4 records per sample) and adapts to 1.25x the largest count seen; a round whose count exceeds it
+    (rare) moves the excess with a second all-gather (`second_gathers`; `collectives` counts them all).
+    gloo (CPU rehearsal of the path) stages device buffers through the host.
     """
 
     HDR = 24
@@ -37,6 +39,8 @@ class RoundExchange:
         self.bound = min(self.cap, first_bound)
         self.host = dist.get_backend(group) == "gloo" and self.dev.type != "cpu"
         self.second_gathers = 0
+        self.collectives = 0
+        self.exchanges = 0
 
     def records_ptr(self):
         """Device address where this rank's clrrt_round_eval output goes (row 1 of the buffer)."""
@@ -46,6 +50,7 @@ class RoundExchange:
         return self.buf[1:]
 
     def _gather(self, t):
+        self.collectives += 1
         src = t.cpu() if self.host else t.contiguous()
         parts = [torch.empty_like(src) for _ in range(self.world)]
         dist.all_gather(parts, src, group=self.group)
@@ -56,6 +61,7 @@ class RoundExchange:
         per rank, first row of this rank's records, max elapsed ms over ranks); the sum of `aux` over the
         ranks is left in self.aux_sum."""
         import numpy as np
+        self.exchanges += 1
         hdr = np.zeros(3, dtype=np.float64)
         hdr.view(np.int64)[0] = int(n_local)
         hdr[1] = float(elapsed_ms)
@@ -83,7 +89,12 @@ class RoundExchange:
         cat = torch.cat(pieces, 0) if total else self.buf[1:1]
         if self.host and total:
             cat = cat.to(self.dev)
-        return cat.contiguous(), counts, sum(counts[:self.rank]), t_max
+        cat = cat.contiguous()
+        if self.dev.type == "cuda":
+            # the engine reads the records on its own stream, which does not order after torch's (a non-blocking
+            # HIP stream unless clrrt_set_stream made them one): the gather and the concatenation must be done
+            torch.cuda.current_stream(self.dev).synchronize()
+        return cat, counts, sum(counts[:self.rank]), t_max
 
 
 class ShardExchange:
@@ -94,10 +105,14 @@ class ShardExchange:
     the largest elapsed query time over the ranks (the engine's budget decision, identical on every rank).
     One code path for 1 and N GPUs: with world 1 the engine appends its records itself."""
 
-    def __init__(self, planner, cap_records, device, group=None, first_bound=1024):
+    def __init__(self, planner, cap_records, device, group=None, first_bound=None, slice_size=None):
         import ctypes
         import traceback
         from . import EXCHANGE_FN
+        if first_bound is None:
+            # a round commits ~0.4 records per sample of the slice (2 at most): one slice's worth of rows covers the
+            # first rounds without a second gather (then the bound follows the counts seen)
+            first_bound = int(slice_size) + 64 if slice_size else 1024
         self.rx = RoundExchange(cap_records, device, group, first_bound)
         self.rank, self.world = self.rx.rank, self.rx.world
         self._keep = None
@@ -123,6 +138,11 @@ class ShardExchange:
     @property
     def second_gathers(self):
         return self.rx.second_gathers
+
+    @property
+    def collectives(self):
+        """All-gathers issued (one per round unless a round's count passed the bound)."""
+        return self.rx.collectives
 
 
 def exchange_capacity(max_batch, defer_steps=0, sim_dt=0.04):

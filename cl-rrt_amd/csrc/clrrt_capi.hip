@@ -257,7 +257,20 @@ struct clrrt_ctx {
     size_t xtmp_bytes = 0;
     int64_t xcap = 0;
     unsigned long long* d_goal = nullptr;  // goal nodes among the appended records (device counter)
+    // errors are collective: a rank that fails sends an error flag through the exchange's aux word (bit 48) in
+    // the exchange the other ranks make next, so every rank leaves the expansion instead of waiting in a
+    // collective the failed rank never joins
+    bool poison_seen = false;      // an exchange of this expansion reported another rank's failure
+    bool fn_failed = false;        // the exchange hook itself failed (the collective is broken: no more calls)
+    bool final_exchanged = false;  // the expansion's last exchange (the drain's) is done
   } sh;
+  // option "fail_at_round" k (fault injection, tests): the k-th commit from now fails with CLRRT_ECAPACITY
+  // after the round's deferred-sample bookkeeping, as the "trajectory arena full" check does
+  int fail_at_round = 0;
+  // CLRRT_DEBUG_SYNC (diagnostics, read once at clrrt_create): a heartbeat buffer the rollout kernel's waves
+  // write, polled while waiting for the launch
+  bool debug_sync = false;
+  unsigned long long* dbg_host = nullptr;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -282,7 +295,7 @@ static int flush_replays(clrrt_ctx* c);
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n);
 static int watchdog_check(clrrt_ctx* c);
 static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped);
-static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app);
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, bool final_exchange = false);
 static int ensure_slots(clrrt_ctx* c);
 
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
@@ -547,6 +560,7 @@ static void free_all(clrrt_ctx* c) {
   if (c->h_totals) hipHostFree(c->h_totals);
   if (c->h_int) hipHostFree(c->h_int);
   if (c->h_bbox) hipHostFree(c->h_bbox);
+  if (c->dbg_host) hipHostFree(c->dbg_host);
   for (auto& pe : c->ev_pending) { hipEventDestroy(pe.second.first); hipEventDestroy(pe.second.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -561,6 +575,7 @@ int clrrt_create(const clrrt_params* p, const clrrt_capacity* cap, int device, c
   clrrt_ctx* c = new clrrt_ctx();
   c->device = device;
   c->params = *p;
+  c->debug_sync = getenv("CLRRT_DEBUG_SYNC") != nullptr;
   clrrt_capacity dc;
   dc.max_nodes = 1 << 20;
   dc.max_rows = 1 << 24;
@@ -1261,6 +1276,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
+  else if (k == "fail_at_round" && value >= 0 && value < INT_MAX) c->fail_at_round = (int)value;  // fault injection
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
@@ -1670,8 +1686,8 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       a.perm = c->roll_perm;
       a.pflag = c->roll_pflag;
     }
-    static unsigned long long* dbg_host = nullptr;  // diagnostics heartbeat (host-mapped)
-    if (getenv("CLRRT_DEBUG_SYNC")) {  // diagnostics: which kernel of the round does not finish
+    unsigned long long*& dbg_host = c->dbg_host;  // diagnostics heartbeat (host-mapped)
+    if (c->debug_sync) {  // diagnostics: which kernel of the round does not finish
       if (!dbg_host) HIPC(c, hipHostMalloc((void**)&dbg_host, sizeof(unsigned long long) * 8 * 4096, hipHostMallocMapped));
       memset(dbg_host, 0, sizeof(unsigned long long) * 8 * 4096);
       HIPC(c, hipHostGetDevicePointer((void**)&a.dbg, dbg_host, 0));
@@ -1682,7 +1698,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, defer ? c->def.best : c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
-    if (getenv("CLRRT_DEBUG_SYNC")) {
+    if (c->debug_sync) {
       const auto t0 = std::chrono::steady_clock::now();
       while (hipStreamQuery(rst) == hipErrorNotReady) {
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 10.0) {
@@ -1799,6 +1815,8 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   }
   int64_t nn = c->h_totals[0], nr = c->h_totals[1];
   if (c->n_rows + nr > c->cap.max_rows) return fail(c, CLRRT_ECAPACITY, "trajectory arena full");
+  if (c->fail_at_round > 0 && --c->fail_at_round == 0)
+    return fail(c, CLRRT_ECAPACITY, "injected failure (option fail_at_round)");
   c->counters.sim_count += c->h_totals[2];
   c->counters.fail_collision += c->h_totals[3];
   c->counters.fail_acclimit += c->h_totals[4];
@@ -1835,6 +1853,9 @@ static int ensure_defer(clrrt_ctx* c) {
   const int64_t B = c->cap.max_batch;
   const int n = std::max(1, c->dp.n_steps_max);
   const int R = (int)((2LL * n + d.T - 1) / d.T) + 2;
+  // sharded rounds carry a record's origin-round age in 8 bits (k_compact_scatter / k_xorder_keys)
+  if (c->sh.world > 1 && R > 256)
+    return fail(c, CLRRT_EINVAL, "defer_steps too small for sharded rounds (more than 256 rounds in flight)");
   if (!d.res || d.R < R) {
     HIPC(c, hipStreamSynchronize(c->stream));
     for (void* p : {(void*)d.res, (void*)d.res_gb, (void*)d.cand, (void*)d.ncand, (void*)d.samp, (void*)d.best})
@@ -1969,11 +1990,15 @@ static int flush_replays(clrrt_ctx* c) {
   a.nrep = c->rep_n;
   a.coop_enable = c->roll_coop;
   a.lanes_per_wave = c->roll_spread ? 0 : 64;
-  if (d.ncarry > 0) {  // suspended replays (or, after an error, chains) of a deferring expansion: run to their end
+  // chains resumed from the carry buffer index the ring's first-success flags (ring slot x max_batch), not
+  // roll_best's max_batch entries
+  int* best = c->roll_best;
+  if (d.ncarry > 0) {  // suspended replays of a deferring expansion: run to their end
     defer_roll_args(c, a, false);
+    best = d.best;
     d.ncarry = 0;
   }
-  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, c->roll_best, c->n_cu));
+  HIPC(c, launch_rollout_persistent(c->stream, a, 0, c->roll_q, best, c->n_cu));
   c->rep_n = 0;
   return replay_check(c);
 }
@@ -2011,7 +2036,7 @@ static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
       d.nd_eval = d.nd;
       int nn = 0, n_app = 0;
       int rc = compact_and_copy(c, 0, &nn, true);
-      if (rc == CLRRT_OK) rc = commit_round(c, nn, c->sh.max_ms, &n_app);
+      if (rc == CLRRT_OK) rc = commit_round(c, nn, c->sh.max_ms, &n_app, true);
       if (rc != CLRRT_OK) return rc;
       if (goal_nodes) *goal_nodes += c->last_goal_nodes;
       if (d.nd != 0 || d.ncarry != 0) return fail(c, CLRRT_EHIP, "deferred samples left after the drain");
@@ -2139,9 +2164,30 @@ static inline void shard_slice(const clrrt_ctx* c, int64_t g, int64_t* f, int* n
   *n = (int)(g * (r + 1) / W - *f);
 }
 
+// A sharded expansion that fails on this rank: unless the other ranks already know (they saw an error flag, or
+// the collective itself failed) or no exchange is left for them to make, take part in the exchange they make
+// next with an empty record set and the error flag (aux bit 48), so that they fail too instead of waiting.
+static void shard_expansion_end(clrrt_ctx* c, int rc) {
+  auto& h = c->sh;
+  if (h.world > 1 && rc != CLRRT_OK && !h.poison_seen && !h.fn_failed && !h.final_exchanged) {
+    void* all = nullptr;
+    int32_t n_all = 0;
+    double mx = 0;
+    int64_t aux_sum = 0;
+    h.fn(h.user, 0, 0.0, 1ll << 48, &all, &n_all, &mx, &aux_sum);
+  }
+  if (rc != CLRRT_OK) {  // the expansion's suspended chains and pending samples are dropped with its results
+    c->def.ncarry = 0;
+    c->def.nd = 0;
+  }
+}
+static void shard_expansion_begin(clrrt_ctx* c) {
+  c->sh.poison_seen = c->sh.fn_failed = c->sh.final_exchanged = false;
+}
+
 // The commit of a round's records (c->out_nodes[0 .. nn)): appended as they are (one rank), or exchanged
 // with the other ranks and the union appended in the same order on every rank.  *n_app = records appended.
-static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, bool final_exchange) {
   auto& h = c->sh;
   *n_app = 0;
   if (h.world <= 1) {
@@ -2149,6 +2195,7 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
     return append_nodes(c, c->out_nodes, nn);
   }
   if (nn > h.cap_local) return fail(c, CLRRT_ECAPACITY, "the round's records exceed the exchange buffer");
+  if (final_exchange) h.final_exchanged = true;
   if (nn > 0)
     HIPC(c, hipMemcpyAsync(h.dev_local, c->out_nodes, sizeof(clrrt_node) * nn, hipMemcpyDeviceToDevice, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));  // the caller's collective reads dev_local
@@ -2162,11 +2209,17 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
       c->n_rows + nn + 2 * ((int64_t)h.last_nb + nd_loc) * (c->dp.n_steps_max + 1) > c->cap.max_rows;
   const int64_t aux = nd_loc + (rows_full ? (1ll << 32) : 0);
   int64_t aux_sum = aux;
-  if (h.fn(h.user, nn, elapsed_ms, aux, &all, &n_all, &mx, &aux_sum) != 0 || n_all < 0 || (n_all > 0 && !all))
+  if (h.fn(h.user, nn, elapsed_ms, aux, &all, &n_all, &mx, &aux_sum) != 0 || n_all < 0 || (n_all > 0 && !all)) {
+    h.fn_failed = true;
     return fail(c, CLRRT_EHIP, "the exchange of the round's records failed");
+  }
+  if (aux_sum >> 48) {  // another rank failed (shard_poison): every rank leaves the expansion
+    h.poison_seen = true;
+    return fail(c, CLRRT_EHIP, "sharded expansion: " + std::to_string(aux_sum >> 48) + " rank(s) failed this round");
+  }
   h.max_ms = mx;
   h.nd_global = aux_sum & 0xffffffffll;
-  h.rows_stop = aux_sum >> 32;
+  h.rows_stop = (aux_sum >> 32) & 0xffff;
   if (n_all > 0) {
     if (n_all > h.xcap) {
       HIPC(c, hipStreamSynchronize(c->stream));
@@ -2293,6 +2346,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   c->sh.max_ms = 0;
   c->sh.nd_global = 0;
   c->sh.rows_stop = 0;
+  shard_expansion_begin(c);
   if (sharded && (rc = shard_goal_reset(c)) != CLRRT_OK) return rc;
   const int64_t nodes_before = c->n_nodes;
   hipStream_t sides[2] = {c->side, c->side2};
@@ -2517,6 +2571,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   // tree, so inside its time)
   if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
   st.deferred = c->def.deferred_total;
+  shard_expansion_end(c, rc);
   if (rc == CLRRT_OK) rc = flush_replays(c);
   c->def.active = false;
   if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);
@@ -2559,6 +2614,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   c->sh.max_ms = 0;
   c->sh.nd_global = 0;
   c->sh.rows_stop = 0;
+  shard_expansion_begin(c);
   if (rc == CLRRT_OK && sharded) rc = shard_goal_reset(c);
   bool have_next = false;  // this round's samples and lists were prepared by the previous round
   double last_round_ms = 0;
@@ -2665,6 +2721,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   // tree, so inside its time)
   if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
   st.deferred = c->def.deferred_total;
+  shard_expansion_end(c, rc);
   if (rc == CLRRT_OK) rc = flush_replays(c);
   c->def.active = false;
   if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);

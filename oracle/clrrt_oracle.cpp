@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -90,6 +91,10 @@ struct Oracle {
   vector<Obs> det;
   vector<Node> tree;
   vector<Node> best;  // MotionPlanner::bestNodes (motionplanner.h:23): the committed path
+  // test expansions only (orc_expand_batch_defer_mt): keys from cached node rotations without the by-value Node
+  // copy, and the stable order's prefix by partial sorts -- the same lists
+  bool keys_by_ref = false;
+  vector<float> rot;  // (sin, cos) of each node's dubinsDistance rotation angle
 };
 
 // ---------------------------------------------------------------- helpers (functions.h)
@@ -472,13 +477,10 @@ static Pt sample_around(Oracle& o) {  // :187-201
   return s;
 }
 
-static float dubins(Pt S, Node N, int dir) {  // dubinsDistance :371-406 (Node by value, as the reference)
+// dubinsDistance :371-406, after the rotation angle's sincosf: the key of offset (qx, qy) from a node whose
+// heading rotation is (sa, ca).
+static float dubins_rot(float qx, float qy, float sa, float ca) {
   float rho = 4.77;
-  float qx = S.x - N.state[0];
-  float qy = S.y - N.state[1];
-  float ang = -N.state[2] - M_PI * (dir != 1);
-  float sa, ca;
-  lm_sincosf(ang, &sa, &ca);
   float tmp = ca * qx - sa * qy;
   qy = std::abs(sa * qx + ca * qy);
   qx = tmp;
@@ -491,6 +493,34 @@ static float dubins(Pt S, Node N, int dir) {  // dubinsDistance :371-406 (Node b
                 (qx * qx + (qy - rho) * (qy - rho) <= rho * rho);
   if (!inside) return std::sqrt(dc * dc - rho * rho) + rho * (thc - std::acos(rho / dc));
   return rho * (alpha + std::asin(qx / df) - std::asin(rho * lm_sinf(alpha) / df));
+}
+
+// dubinsDistance :371-406 (Node by value, as the reference: the CPU baseline times that copy)
+static float dubins(Pt S, Node N, int dir) {
+  float qx = S.x - N.state[0];
+  float qy = S.y - N.state[1];
+  float ang = -N.state[2] - M_PI * (dir != 1);
+  float sa, ca;
+  lm_sincosf(ang, &sa, &ca);
+  return dubins_rot(qx, qy, sa, ca);
+}
+
+// the same key from a node's cached rotation (Oracle::rot, dir = 1): the multi-threaded test expansions
+// (orc_expand_batch_defer_mt), without the by-value copy of nodes that hold long trajectories
+static float dubins_cached(const Oracle& o, const Pt& S, size_t i) {
+  const Node& N = o.tree[i];
+  float qx = S.x - N.state[0];
+  float qy = S.y - N.state[1];
+  return dubins_rot(qx, qy, o.rot[2 * i], o.rot[2 * i + 1]);
+}
+static void cache_rotations(Oracle& o) {
+  for (size_t i = o.rot.size() / 2; i < o.tree.size(); i++) {
+    float ang = -o.tree[i].state[2] - M_PI * (1 != 1);
+    float sa, ca;
+    lm_sincosf(ang, &sa, &ca);
+    o.rot.push_back(sa);
+    o.rot.push_back(ca);
+  }
 }
 
 static bool feasible_node(Oracle& o, const Node& n, const Pt& s) {  // :271-289
@@ -508,13 +538,43 @@ static bool feasible_node(Oracle& o, const Node& n, const Pt& s) {  // :271-289
 static vector<int> sort_nodes(Oracle& o, const Pt& s, bool explore, size_t upto,
                               vector<float>* keys_out = nullptr, bool stable = false) {
   vector<std::pair<int, float>> dv;
-  for (size_t i = 0; i != upto; i++) {
-    float k = explore ? dubins(s, o.tree[i], 1) : o.tree[i].costE + dubins(s, o.tree[i], 1);
-    dv.push_back(std::make_pair((int)i, k));
-  }
   auto by_key = [](const std::pair<int, float>& a, const std::pair<int, float>& b) { return a.second < b.second; };
-  if (stable) std::stable_sort(dv.begin(), dv.end(), by_key);
-  else std::sort(dv.begin(), dv.end(), by_key);
+  if (o.keys_by_ref && stable && o.rot.size() >= 2 * upto && !keys_out) {
+    // test expansions: cached rotations, and the stable order's prefix by partial sorts on (key, id) -- the
+    // stable sort of an id-ordered list is the (key, id) order when no key is NaN (else the full sort below)
+    dv.reserve(upto);
+    bool nan = false;
+    for (size_t i = 0; i != upto; i++) {
+      const float d = dubins_cached(o, s, i);
+      float k = explore ? d : o.tree[i].costE + d;
+      nan |= k != k;
+      dv.push_back(std::make_pair((int)i, k));
+    }
+    if (!nan) {
+      auto by_key_id = [](const std::pair<int, float>& a, const std::pair<int, float>& b) {
+        return a.second < b.second || (a.second == b.second && a.first < b.first);
+      };
+      size_t K = std::min<size_t>(upto, 64), done = 0;
+      vector<int> out;
+      for (;;) {
+        std::partial_sort(dv.begin() + done, dv.begin() + K, dv.end(), by_key_id);
+        for (; done < K; done++) {
+          if (feasible_node(o, o.tree[dv[done].first], s)) out.push_back(dv[done].first);
+          if ((int)out.size() == o.p.sort_limit) return out;
+        }
+        if (K == upto) return out;
+        K = std::min<size_t>(upto, 8 * K);
+      }
+    }
+    std::stable_sort(dv.begin(), dv.end(), by_key);
+  } else {
+    for (size_t i = 0; i != upto; i++) {
+      float k = explore ? dubins(s, o.tree[i], 1) : o.tree[i].costE + dubins(s, o.tree[i], 1);
+      dv.push_back(std::make_pair((int)i, k));
+    }
+    if (stable) std::stable_sort(dv.begin(), dv.end(), by_key);
+    else std::sort(dv.begin(), dv.end(), by_key);
+  }
   vector<int> out;
   for (auto it = dv.begin(); it != dv.end(); ++it) {
     if (feasible_node(o, o.tree[it->first], s)) {
@@ -836,6 +896,61 @@ void orc_expand_batch_defer(void* h, long n_iters, int B, int stable, int T, lon
     round++;
   }
   for (auto& p : pend) append_result(*o, p.r);
+  if (deferred) *deferred = ndef;
+}
+
+// orc_expand_batch_defer with each round's samples evaluated on `threads` host threads (the frozen tree is
+// only read; counters are atomic; results are appended in the same order), so that whole trees at the
+// benchmarked sizes (16384 samples per round) can be checked.  Test infrastructure.
+void orc_expand_batch_defer_mt(void* h, long n_iters, int B, int stable, int T, int threads, long* deferred) {
+  Oracle* o = (Oracle*)h;
+  struct Pend { long due; IterResult r; };
+  std::vector<Pend> pend;
+  long done = 0, round = 0, ndef = 0;
+  const bool by_ref = o->keys_by_ref;
+  o->keys_by_ref = true;
+  while (done < n_iters) {
+    int nb = (int)std::min<long>(B, n_iters - done);
+    std::vector<Pt> ss(nb);
+    std::vector<char> ex(nb);
+    for (int j = 0; j < nb; j++) {
+      ss[j] = sample_around(*o);
+      double r = static_cast<double>(rand()) / (static_cast<double>(RAND_MAX / (1)));
+      ex[j] = r <= 0.7;
+    }
+    const size_t upto = o->tree.size();
+    cache_rotations(*o);
+    std::vector<IterResult> rs(nb);
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    const int nt = std::max(1, std::min(threads, nb));
+    for (int t = 0; t < nt; t++)
+      pool.emplace_back([&]() {
+        for (int j; (j = next.fetch_add(1, std::memory_order_relaxed)) < nb;)
+          rs[j] = evaluate_iteration(*o, ss[j], ex[j], upto, stable != 0);
+      });
+    for (auto& th : pool) th.join();
+    std::vector<Pend> keep;
+    for (auto& p : pend) {
+      if (p.due == round) append_result(*o, p.r);
+      else keep.push_back(std::move(p));
+    }
+    for (int j = 0; j < nb; j++) {
+      const long D = (T > 0 && rs[j].chain > 0) ? (rs[j].chain + T - 1) / T - 1 : 0;
+      if (D == 0) {
+        append_result(*o, rs[j]);
+      } else {
+        keep.push_back(Pend{round + D, std::move(rs[j])});
+        ndef++;
+      }
+    }
+    pend.swap(keep);
+    done += nb;
+    round++;
+  }
+  for (auto& p : pend) append_result(*o, p.r);
+  o->keys_by_ref = by_ref;
+  o->rot.clear();
   if (deferred) *deferred = ndef;
 }
 

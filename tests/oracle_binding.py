@@ -36,6 +36,7 @@ def lib():
             "orc_expand_budget": (l, [vp, d, i]),
             "orc_expand_batch": (None, [vp, l, i, i]),
             "orc_expand_batch_defer": (None, [vp, l, i, i, i, C.POINTER(C.c_long)]),
+            "orc_expand_batch_defer_mt": (None, [vp, l, i, i, i, i, C.POINTER(C.c_long)]),
             "orc_tree_size": (l, [vp]),
             "orc_get_nodes": (None, [vp, l, l, P(abi.Node)]),
             "orc_node_ref_len": (l, [vp, l]),
@@ -128,9 +129,15 @@ class Oracle:
     def expand(self, n):
         self.L.orc_expand(self.h, n)
 
-    def expand_batch(self, n, batch, stable=True, defer_steps=0):
+    def expand_batch(self, n, batch, stable=True, defer_steps=0, threads=0):
         """BATCH rounds (the engine's semantics); defer_steps T > 0: deferred samples (orc_expand_batch_defer).
-        Returns the number of samples deferred at least one round."""
+        threads > 0: each round's samples evaluated on that many host threads (orc_expand_batch_defer_mt, same
+        tree).  Returns the number of samples deferred at least one round."""
+        if threads > 0:
+            nd = C.c_long(0)
+            self.L.orc_expand_batch_defer_mt(self.h, n, batch, 1 if stable else 0, max(0, defer_steps), threads,
+                                             C.byref(nd))
+            return nd.value
         if defer_steps <= 0:
             self.L.orc_expand_batch(self.h, n, batch, 1 if stable else 0)
             return 0

@@ -34,11 +34,11 @@ def _free_port():
     return p
 
 
-def _planner():
+def _planner(world=WORLD):
     import clrrt
     from clrrt import abi, scenes
     pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), device=0, max_nodes=1 << 18,
-                       max_rows=1 << 25, max_batch=WORLD * B)
+                       max_rows=1 << 25, max_batch=world * B)
     pl.set_obstacles(scenes.urban_scene(200))
     pl.tree_init()
     return pl
@@ -121,65 +121,82 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
 # The engine's own sharded rounds (clrrt_set_shards + clrrt.dist.ShardExchange): clrrt_expand runs every round
 # on each rank -- its slice of the samples, the lag-1 / lag-2 pipelines, deferred samples -- and the exchange
 # hook all-gathers the records; the same code path as one GPU.
-SHARD_CASES = [  # (samples per round over both ranks, defer_steps, nn_lag, rounds)
-    (2 * B, 0, 1, 4),
-    (2 * B, 64, 2, 6),
-    (2 * B - 7, 48, 1, 4),   # uneven slices (shard_slice), deferred samples
+SHARD_CASES = [  # (ranks, samples per round over all ranks, defer_steps, nn_lag, rounds)
+    (2, 2 * B, 0, 1, 4),
+    (2, 2 * B, 64, 2, 6),
+    (2, 2 * B - 7, 48, 1, 4),   # uneven slices (shard_slice), deferred samples
+    (4, 4 * B, 128, 2, 5),      # four ranks, the cfg3 bench's defer_steps
+    (4, 4 * B - 5, 64, 1, 4),
 ]
 
 
-def _shard_worker(rank, port, out_dir, G, T, lag, rounds):
+def _shard_worker(rank, port, out_dir, world, G, T, lag, rounds, fail_rank=-1, fail_round=0):
     sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     import clrrt
     from clrrt import dist as cdist
-    pl = _planner()
+    pl = _planner(world)
     pl.set_option("defer_steps", T)
     pl.set_option("nn_lag", lag)
     pl.set_stream(torch.cuda.current_stream().cuda_stream)
-    ex = cdist.ShardExchange(pl, cdist.exchange_capacity(B, T), "cuda", first_bound=256)
-    st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
+    ex = cdist.ShardExchange(pl, cdist.exchange_capacity(-(-G // world), T), "cuda", slice_size=-(-G // world))
+    if rank == fail_rank:
+        pl.set_option("fail_at_round", fail_round)
+    err = ""
+    try:
+        st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
+    except clrrt.ClrrtError as e:
+        st, err = None, str(e)
+    if st is None:
+        np.savez(os.path.join(out_dir, f"shard{rank}.npz"), err=err, ex_rounds=ex.rounds)
+        dist.destroy_process_group()
+        pl.close()
+        return
     raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
     g = pl.nodes()
     own = np.nonzero(g["owner"] == rank)[0]
     rows = [pl.rows(int(g["row_offset"][i]), int(g["nrows"][i])) for i in own]
     np.savez(os.path.join(out_dir, f"shard{rank}.npz"), hdr=raw[:, :HDR], own=own,
              rows=np.concatenate(rows) if rows else np.zeros((0, 10)), rounds=st["rounds"], it=st["iterations"],
-             goals=st["goal_nodes_added"], deferred=st["deferred"], ex_rounds=ex.rounds)
+             goals=st["goal_nodes_added"], deferred=st["deferred"], ex_rounds=ex.rounds,
+             collectives=ex.collectives, err=err)
     dist.barrier()
     dist.destroy_process_group()
     pl.close()
 
 
-@pytest.mark.parametrize("G,T,lag,rounds", SHARD_CASES)
-def test_sharded_expand_matches_single_process(tmp_path, G, T, lag, rounds):
-    """Two ranks sharing GPU 0 run clrrt_expand with the exchange hook; both trees equal ONE process expanding
-    the same stream with G samples per round (same defer_steps): headers bit for bit, every node's rows on
-    its owner, the iteration count and the goal nodes appended (every rank's)."""
+@pytest.mark.parametrize("world,G,T,lag,rounds", SHARD_CASES)
+def test_sharded_expand_matches_single_process(tmp_path, world, G, T, lag, rounds):
+    """Two or four ranks sharing GPU 0 run clrrt_expand with the exchange hook; every tree equals ONE process
+    expanding the same stream with G samples per round (same defer_steps): headers bit for bit, every node's rows
+    on its owner, the iteration count and the goal nodes appended (every rank's).  One collective
+    per exchange (the gather bound starts at the slice size, so no round needs a second gather)."""
     import torch.multiprocessing as mp
-    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path), G, T, lag, rounds), nprocs=WORLD, join=True)
+    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path), world, G, T, lag, rounds), nprocs=world, join=True)
     import clrrt
-    pl = _planner()
+    pl = _planner(world)
     pl.set_option("defer_steps", T)
     pl.set_option("nn_lag", lag)
     st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
     assert st["rounds"] == rounds and (T == 0 or st["deferred"] > 0), st
     ref_raw = np.frombuffer(bytes(pl.nodes_raw()), dtype=np.uint8).reshape(-1, 160)
     g = pl.nodes()
-    ranks = [np.load(tmp_path / f"shard{r}.npz") for r in range(WORLD)]
-    print(f"sharded G={G} T={T} lag {lag}: {ref_raw.shape[0]} nodes; owned {[len(r['own']) for r in ranks]}; "
+    ranks = [np.load(tmp_path / f"shard{r}.npz") for r in range(world)]
+    print(f"sharded x{world} G={G} T={T} lag {lag}: {ref_raw.shape[0]} nodes; owned {[len(r['own']) for r in ranks]}; "
           f"deferred {[int(r['deferred']) for r in ranks]} (single {st['deferred']}); exchanges "
-          f"{[int(r['ex_rounds']) for r in ranks]}")
+          f"{[int(r['ex_rounds']) for r in ranks]}, collectives {[int(r['collectives']) for r in ranks]}")
     assert ref_raw.shape[0] > 2000
     for r in ranks:
+        assert str(r["err"]) == ""
         assert np.array_equal(r["hdr"], ref_raw[:, :HDR])
         assert int(r["rounds"]) == rounds and int(r["it"]) == rounds * G
         assert int(r["goals"]) == st["goal_nodes_added"]
+        assert int(r["collectives"]) == int(r["ex_rounds"]) >= rounds
     assert sum(int(r["deferred"]) for r in ranks) == st["deferred"]
     assert sum(len(r["own"]) for r in ranks) == ref_raw.shape[0]
     for rk, r in enumerate(ranks):
@@ -187,3 +204,42 @@ def test_sharded_expand_matches_single_process(tmp_path, G, T, lag, rounds):
         want = np.concatenate(want) if want else np.zeros((0, 10))
         assert np.array_equal(r["rows"].view(np.uint64), want.view(np.uint64)), rk
     pl.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fail_round", [1, 3])
+def test_sharded_failure_is_collective(tmp_path, fail_round):
+    """A failure on one rank only (option fail_at_round: its commit of that round fails, after the deferred-sample
+    bookkeeping) ends the expansion on every rank with an error, instead of leaving the others waiting in the
+    round's all-gather: the failed rank joins the exchange the others make with an error flag."""
+    import torch.multiprocessing as mp
+    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path), 2, 2 * B, 64, 2, 6, 1, fail_round), nprocs=2,
+             join=True)
+    r0, r1 = (np.load(tmp_path / f"shard{r}.npz") for r in range(2))
+    print(f"fail at round {fail_round}: rank 0 '{r0['err']}', rank 1 '{r1['err']}', exchanges "
+          f"{int(r0['ex_rounds'])} / {int(r1['ex_rounds'])}")
+    assert "injected failure" in str(r1["err"])
+    assert "rank(s) failed" in str(r0["err"])
+
+
+@pytest.mark.timeout(300)
+def test_deferred_error_then_flush(tmp_path):
+    """An expansion with deferred samples that fails mid-way (fault injection) leaves no suspended chains behind:
+    the rows flush, a fresh tree and a new expansion afterwards work and grow the tree a fresh context grows."""
+    import clrrt
+    trees = []
+    for inject in (True, False):
+        pl = _planner(1)
+        pl.set_option("defer_steps", 32)
+        if inject:
+            pl.set_option("fail_at_round", 3)
+            with pytest.raises(clrrt.ClrrtError, match="injected failure"):
+                pl.expand(clrrt.Rng(5), n_iters=6 * B, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+            pl.rows_flush()
+            pl.tree_init()
+        st = pl.expand(clrrt.Rng(SEED), n_iters=4 * B, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+        assert st["deferred"] > 0
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes()))
+        pl.close()
+    assert trees[0] == trees[1]

@@ -189,3 +189,52 @@ def test_cfg2_batch_tree_parity():
     oc, gc = o.counters(), pl.counters()
     assert oc["rollouts"] > 0 and gc["rollouts"] > 0
     pl.close()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config", ["cfg3", "cfg2"])
+def test_bench_settings_deferred_tree_matches_oracle(config):
+    """The exact settings bench.py measures, whole tree against the oracle (verdict r04 item 1): BATCH rounds at
+    the benchmarked batch with deferred samples (cfg3: 200 obstacles, B = 16384, defer_steps 128, the lag-2
+    pipeline a 2 s query runs, 8 rounds; cfg2: 50 obstacles, B = 4096, defer_steps 64, lag 1 as a 200 ms query
+    runs, 6 rounds) grow node for node, bit for bit (states, float costs, goal flags, parents, every trajectory row,
+    the reference's counters) the tree of orc_expand_batch_defer's rule (each sample evaluated against its own
+    round's frozen tree -- expandTree rrtplanner.cpp:123-174 -- and committed ceil(chain / T) - 1 rounds late,
+    oldest round first), evaluated here on 16 host threads."""
+    B, T, M, rounds, lag = {"cfg3": (16384, 128, 200, 8, 2), "cfg2": (4096, 64, 50, 6, 1)}[config]
+    obs = scenes.urban_scene(M)
+    seed = 31
+    o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+    Oracle.srand(seed)
+    o.init_tree()
+    ndef = o.expand_batch(B * rounds, B, stable=True, defer_steps=T, threads=16)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 20,
+                       max_rows=1 << 26, max_batch=B)
+    try:
+        pl.set_option("defer_steps", T)
+        pl.set_option("nn_lag", lag)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(seed), n_iters=B * rounds, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+        assert st["rounds"] == rounds and st["iterations"] == B * rounds, st
+        on, gn = o.nodes(), pl.nodes()
+        print(f"{config} bench settings: oracle {len(on['parent'])} nodes ({ndef} samples deferred), "
+              f"gpu {len(gn['parent'])} nodes ({st['deferred']} deferred)")
+        assert len(on["parent"]) == len(gn["parent"]) > rounds * B // 4
+        bad = np.nonzero((on["parent"] != gn["parent"]) | (on["goal"] != gn["goal"]) | (on["nrows"] != gn["nrows"])
+                         | (gn["state"].view(np.uint64) != on["state"].view(np.uint64)).any(axis=1)
+                         | (gn["costE"].view(np.uint32) != on["costE"].view(np.uint32))
+                         | (gn["costS"].view(np.uint32) != on["costS"].view(np.uint32)))[0]
+        assert bad.size == 0, f"{bad.size} nodes differ, first {bad[:5]}"
+        assert st["deferred"] == ndef > 0
+        oc, gc = o.counters(), pl.counters()
+        for k in ("sim_count", "fail_collision", "fail_acclimit", "fail_iterlimit", "rollouts"):
+            assert oc[k] == gc[k], (k, oc[k], gc[k])
+        nr = pl.size()[1]
+        arena = pl.rows(0, nr)
+        for i in range(1, len(on["parent"])):
+            off, cnt = int(gn["row_offset"][i]), int(gn["nrows"][i])
+            assert np.array_equal(arena[off:off + cnt].view(np.uint64), np.ascontiguousarray(o.rows(i)).view(np.uint64)), i
+        assert pl.debug_counters()[61] == 0
+    finally:
+        pl.close()

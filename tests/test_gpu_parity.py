@@ -443,7 +443,7 @@ def test_exact_min_width_identical():
 
 @pytest.mark.gpu
 def test_deferred_batch_rounds_identical():
-    """Full-size property of the deferred-sample rounds (defer_steps): the pipelines (none, lag 1, lag 2) and
+    """Full-size property of the deferred-sample rounds (defer_steps 128, as bench.py runs cfg3): the pipelines (none, lag 1, lag 2) and
     the scheduling options (grid width, queue order, per-lane collision checks) grow exactly the same tree --
     which samples are deferred, and by how many rounds, depends on their rollouts' step counts only -- and
     a sample is deferred in every variant; rows of every node replay exactly."""
@@ -454,7 +454,7 @@ def test_deferred_batch_rounds_identical():
     for opts in variants:
         pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 20, max_rows=1 << 26,
                            max_batch=16384)
-        pl.set_option("defer_steps", 64)
+        pl.set_option("defer_steps", 128)  # the cfg3 bench setting
         for k, v in opts.items():
             pl.set_option(k, v)
         pl.set_obstacles(obs)

@@ -99,3 +99,22 @@ def test_scene_generator_shape():
     assert s.shape == (220, 7)
     assert np.all(np.abs(s[:200, 1]) >= 3.0)
     assert np.all(s[:200, 5:] == 0) and np.any(s[200:, 5:] != 0)
+
+
+@pytest.mark.parametrize("T", [0, 24])
+def test_threaded_batch_defer_equals_sequential(T):
+    """orc_expand_batch_defer_mt (each round's samples on host threads, keys without the by-value Node copy) grows
+    the tree of the sequential orc_expand_batch_defer, bit for bit -- it is the checker the full-size deferred-sample
+    tests (tests/test_full_size_parity.py) run at the benchmarked batch sizes."""
+    obs = scenes.urban_scene(200)
+    trees = []
+    for threads in (0, 8):
+        o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+        Oracle.srand(7)
+        o.init_tree()
+        nd = o.expand_batch(6 * 128, 128, stable=True, defer_steps=T, threads=threads)
+        assert (nd > 0) == (T > 0)
+        trees.append((bytes(o.nodes_raw()), o.counters(), nd,
+                      b"".join(o.rows(i).tobytes() for i in range(1, o.size(), 5))))
+    assert trees[0] == trees[1]
+    assert len(trees[0][0]) > 160 * 100

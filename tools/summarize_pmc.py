@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --pmc counter_collection.csv per kernel: dispatches, sum and mean per dispatch
 of each counter.  Usage: summarize_pmc.py [--build COMMIT] run_counter_collection.csv [more.csv ...] > summary.json
-(--build records the profiled build's commit under "_build", which bench.py quotes in traffic_note)."""
+(--build records the profiled build's commit under "_build", which bench.py quotes in traffic_note; "_src" is the
+sources' fingerprint, by which bench.py picks the pass of the build it runs on)."""
 import collections
 import csv
 import json
@@ -28,4 +29,7 @@ for k, v in out.items():
               "total": dict(v["counters"])}
 if build:
     res["_build"] = build
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from bench import source_fingerprint  # noqa: E402
+res["_src"] = source_fingerprint()  # bench.py names the pass of the build it runs on
 json.dump(res, sys.stdout, indent=1, sort_keys=True)
