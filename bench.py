@@ -44,6 +44,10 @@ PEAK_HBM_GBS = 8000.0
 # point scanned by findClosestPoint; FP32 per OBB box test = 36.
 FLOP_STEP, FLOP_SCAN, FLOP_BOX = 160, 6, 36
 FLOP_KEY = 40  # FP32 FLOP per nearest-node (Dubins) key
+# the walk search's own work (hardware roofline of k_walk_search): per tile / super-tile lower bound (walk_lb: two
+# approximate acos, a square root, a reciprocal, the dot products: ~40 FP32 FLOP) and per record of a visited tile
+# through the prefilter (distance + turning-bound + feasibility-cone tests: ~12 FLOP)
+FLOP_TILE_BOUND, FLOP_PREFILTER = 40, 12
 # BATCH option defer_steps of the headline run (a config may set its own)
 DEFER_STEPS = 128
 
@@ -437,10 +441,11 @@ def main():
 
     roll_ms, roll_n = pl.kernel_time(1)
     nn_ms, nn_n = pl.kernel_time(0)
+    walk_ms, walk_n = pl.kernel_time(3)
     other_ms, other_n = pl.kernel_time(2)
     work = pl.work_counters()
     cnt = pl.counters()
-    sw = pl.search_work()
+    sw = pl.search_work_ex()
 
     sync_line = None
     if world == 1 and not replanning and not args.no_sync and defer > 0:
@@ -487,7 +492,12 @@ def main():
     peak_tf = (fp64 + fp32) / t_mix if t_mix > 0 else PEAK_FP32_VALU_TF
     avg_launch_ms = roll_ms / roll_n if roll_n else 0.0
     hbm_gbs = traffic / (avg_launch_ms * 1e-3) / 1e9 if traffic and avg_launch_ms > 0 else None
-    nn_tf = sw["bf_keys"] * FLOP_KEY / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
+    # walk search: the FLOP of the work it does (exact keys, tile / super-tile bounds, prefiltered records) over
+    # its own launches' time, against the FP32 VALU peak; the brute-force keys it avoids are a separate ratio
+    walk_flop = (FLOP_KEY * sw["exact_keys"] + FLOP_TILE_BOUND * (sw["super_bounds"] + 32 * sw["super_visits"])
+                 + FLOP_PREFILTER * 32 * sw["tiles"])
+    walk_tf = walk_flop / (walk_ms * 1e-3) / 1e12 if walk_ms > 0 else 0.0
+    done_keys = sw["exact_keys"] + 32 * sw["tiles"]
     value = tot_nodes / elapsed
     line = {
         "metric": "nodes expanded/sec (200-obstacle scene)",
@@ -540,19 +550,27 @@ def main():
         },
         "roofline_nn": {
             "bound": "valu",
-            "kernel": "nearest-node search (walk index build + k_walk_search + appended-node merge)",
-            "achieved": nn_tf,
+            "kernel": "k_walk_search (the walk searches: sample order, main grid, overflow split + merge)",
+            "achieved": walk_tf,
             "peak": PEAK_FP32_VALU_TF,
             "unit": "TFLOP/s",
-            "frac": nn_tf / PEAK_FP32_VALU_TF,
-            "work_basis": "brute-force-equivalent Dubins keys (samples x tree nodes, SURVEY §8(d): 40 FP32 FLOP "
-                          "per key) over the search kernels' HIP-event time",
+            "frac": walk_tf / PEAK_FP32_VALU_TF,
+            "work_basis": f"work the walk does: {FLOP_KEY} FLOP per exact Dubins key, {FLOP_TILE_BOUND} per tile or "
+                          f"super-tile bound, {FLOP_PREFILTER} per record of a visited tile (prefilter), over the "
+                          "walk launches' HIP-event time",
+            "walk_ms": walk_ms,
+            "walk_launches": walk_n,
+            "walk_flop": walk_flop,
+            "work_avoided": sw["bf_keys"] / done_keys if done_keys else None,
+            "work_avoided_note": "brute-force-equivalent keys (samples x tree nodes) per key-or-record the walk "
+                                 "touched (exact keys + records of visited tiles)",
+            "super_bounds_per_sample": sw["super_bounds"] / sw["samples"] if sw["samples"] else 0.0,
             "bf_keys": sw["bf_keys"],
             "samples": sw["samples"],
             "tiles_per_sample": sw["tiles"] / sw["samples"] if sw["samples"] else 0.0,
             "exact_keys_per_sample": sw["exact_keys"] / sw["samples"] if sw["samples"] else 0.0,
-            "launches": nn_n,
-            "kernel_ms": nn_ms,
+            "nn_launches": nn_n,
+            "nn_kernel_ms": nn_ms,
         },
         "kernel_ms": {"rollout": roll_ms, "nn": nn_ms, "select_commit": other_ms,
                       "launches": {"rollout": roll_n, "nn": nn_n, "other": other_n}},

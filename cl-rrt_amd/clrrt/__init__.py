@@ -78,6 +78,7 @@ _SIGS = {
     "clrrt_enable_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_search_work_ex": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_obstacle_distance": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32, P(C.c_double)]),
     "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
@@ -449,6 +450,14 @@ class Planner:
         out = (C.c_int64 * 4)()
         self._chk(self.L.clrrt_search_work(self.h, out), "search_work")
         return {"bf_keys": out[0], "samples": out[1], "tiles": out[2], "exact_keys": out[3]}
+
+    def search_work_ex(self):
+        """search_work + the walk's bound work: phase-1 super-tile bounds, super-tile visits (32 tile bounds
+        each), records past the prefilter."""
+        out = (C.c_int64 * 8)()
+        self._chk(self.L.clrrt_search_work_ex(self.h, out), "search_work_ex")
+        return {"bf_keys": out[0], "samples": out[1], "tiles": out[2], "exact_keys": out[3],
+                "super_bounds": out[4], "super_visits": out[5], "queued": out[6]}
 
     def reset_counters(self):
         self._chk(self.L.clrrt_reset_counters(self.h), "reset_counters")

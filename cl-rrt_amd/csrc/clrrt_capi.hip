@@ -113,6 +113,7 @@ struct clrrt_ctx {
   // round, 8192 -> 45.6 vs 58-59 ms; 8 M: 3072 stays best, 25.8 vs 29.9 ms at 8192, profiles/r04as)
   bool nnw_bud_tiles_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
+  int nnw_index = 0;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind)
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
   // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
@@ -281,10 +282,13 @@ struct clrrt_ctx {
   // counters
   clrrt_counters counters{};
   int64_t nn_bf_keys = 0, nn_samples = 0;  // search work: brute-force-equivalent keys, samples searched
+  int64_t nn_super_bounds = 0;             // walk searches' phase-1 super-tile bounds (samples x super-tiles)
   // timing
   bool timing = false;
-  double kt_ms[3] = {0, 0, 0};
-  int64_t kt_n[3] = {0, 0, 0};
+  // per class: 0 nearest-node search (index builds, walks, merges), 1 rollouts, 2 select / commit,
+  // 3 the walk searches alone (launch_nn_walk_search: sample order, k_walk_search, split + merge; within class 0)
+  double kt_ms[4] = {0, 0, 0, 0};
+  int64_t kt_n[4] = {0, 0, 0, 0};
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
 };
@@ -1202,7 +1206,7 @@ int clrrt_get_counters(clrrt_ctx* c, clrrt_counters* out) {
 int clrrt_reset_counters(clrrt_ctx* c) {
   if (!c) return CLRRT_EINVAL;
   memset(&c->counters, 0, sizeof(c->counters));
-  c->nn_bf_keys = c->nn_samples = 0;
+  c->nn_bf_keys = c->nn_samples = c->nn_super_bounds = 0;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipMemsetAsync(c->work_ctr, 0, 64 * sizeof(unsigned long long), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
@@ -1243,6 +1247,21 @@ int clrrt_search_work(clrrt_ctx* c, int64_t out[4]) {
   return CLRRT_OK;
 }
 
+int clrrt_search_work_ex(clrrt_ctx* c, int64_t out[8]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  int64_t w[4];
+  const int rc = clrrt_search_work(c, w);
+  if (rc != CLRRT_OK) return rc;
+  unsigned long long h[19];
+  HIPC(c, hipMemcpy(h, c->work_ctr + 8, sizeof(h), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 4; i++) out[i] = w[i];
+  out[4] = c->nn_super_bounds;
+  out[5] = (int64_t)h[10];  // super-tile visits (32 tile bounds each)
+  out[6] = (int64_t)h[12];  // records past the prefilter (queued for stage 1 / 2)
+  out[7] = 0;
+  return CLRRT_OK;
+}
+
 int clrrt_nn_stats(clrrt_ctx* c, int64_t out[19]) {
   if (!c || !out) return CLRRT_EINVAL;
   HIPC(c, hipSetDevice(c->device));
@@ -1266,6 +1285,11 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
+  else if (k == "nn_walk_index" && value >= 0 && value <= 2) {
+    c->nnw_index = (int)value;
+    c->nnw_built.n = -1;  // the kept index and sort results have the old order
+    c->nnw.sorted_n = c->nnw_alt.sorted_n = c->nnw3.sorted_n = -1;
+  }
   else if (k == "nn_walk_lds_floor" && value >= 0 && value <= 65536) c->nnw_lds_floor = (int)value;
   else if (k == "nn_walk_waves" && value >= -1 && value <= 1 << 20) c->nnw_waves = (int)value;
   else if (k == "nn_walk_chunks" && value >= 1 && value <= kWalkMaxChunks) c->nnw_chunks = (int)value;
@@ -1343,12 +1367,12 @@ int clrrt_enable_timing(clrrt_ctx* c, int32_t on) {
   if (!c) return CLRRT_EINVAL;
   drain_timers(c);
   c->timing = on != 0;
-  for (int i = 0; i < 3; i++) { c->kt_ms[i] = 0; c->kt_n[i] = 0; }
+  for (int i = 0; i < 4; i++) { c->kt_ms[i] = 0; c->kt_n[i] = 0; }
   return CLRRT_OK;
 }
 
 int clrrt_kernel_time(clrrt_ctx* c, int32_t which, double* ms, int64_t* launches) {
-  if (!c || which < 0 || which > 2) return CLRRT_EINVAL;
+  if (!c || which < 0 || which > 3) return CLRRT_EINVAL;
   drain_timers(c);
   if (ms) *ms = c->kt_ms[which];
   if (launches) *launches = c->kt_n[which];
@@ -1432,6 +1456,7 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.max_over = c->nnw_max_over_set || c->n_nodes < (6 << 20) ? c->nnw_max_over : kWalkMaxOver;
   w.nch = c->nnw_chunks;
   w.half_max = c->nnw_half_max;
+  w.index_kind = c->nnw_index;
   w.lds_floor = c->nnw_lds_floor;
   w.waves = c->nnw_waves < 0 ? 10 * c->n_cu : c->nnw_waves;
   // the default grid serves batches of >= 4x its waves (cfg2's 4096-sample rounds run 4% faster with one
@@ -1527,8 +1552,9 @@ static int launch_side_walk(clrrt_ctx* c, int n2, const NnSetup& su) {
   c->nn_samples += n2;
   HIPC(c, hipStreamWaitEvent(c->side, c->ev_tree, 0));
   HIPC(c, hipMemcpyAsync(c->d_samples2, c->h_samples2, sizeof(clrrt_sample) * n2, hipMemcpyHostToDevice, c->side));
+  c->nn_super_bounds += (int64_t)n2 * walk_super_count(c->n_nodes);
   {
-    KTimer kt(c, 0, c->side);
+    KTimer kt(c, 0, c->side), kt3(c, 3, c->side);
     HIPC(c, launch_nn_walk_search(c->side, c->d_samples2, n2, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0,
                                   su.x1, su.y1, c->nnw, c->cand2, c->ckey2, c->ncand2, c->ctie2, c->work_ctr + 18,
                                   c->nnw_stateless));
@@ -2410,8 +2436,9 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     c->nn_samples += n;
     HIPC(c, hipStreamWaitEvent(s, c->ev_tree, 0));
     HIPC(c, hipMemcpyAsync(sl.d, sl.h, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, s));
+    c->nn_super_bounds += (int64_t)n * walk_super_count(c->n_nodes);
     {
-      KTimer kt(c, 0, s);
+      KTimer kt(c, 0, s), kt3(c, 3, s);
       HIPC(c, launch_nn_walk_search(s, sl.d, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1, su.y1,
                                     *W[k], sl.cand, sl.ckey, sl.ncand, sl.ctie, c->work_ctr + 18, c->nnw_stateless));
     }
@@ -2485,7 +2512,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         if ((rc = build(wk, su)) != CLRRT_OK) break;
         c->nn_bf_keys += (int64_t)nb * c->n_nodes;
         c->nn_samples += nb;
-        KTimer kt(c, 0);
+        c->nn_super_bounds += (int64_t)nb * walk_super_count(c->n_nodes);
+        KTimer kt(c, 0), kt3(c, 3);
         HIPC(c, launch_nn_walk_search(c->stream, c->d_samples, nb, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0,
                                       su.x1, su.y1, *W[wk], c->cand, c->ckey, c->ncand, c->ctie, c->work_ctr + 18,
                                       c->nnw_stateless));

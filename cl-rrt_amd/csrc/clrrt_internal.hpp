@@ -195,6 +195,11 @@ struct WalkBufs {
   int lds_floor = 0;    // bytes of LDS each walk wave reserves at least (caps the walk's waves per CU)
   int waves = 0;        // > 0: a persistent walk grid of this many waves (samples from per-XCD counters)
   int waves_min_batch = 0;  // ... used for batches of at least this many samples
+  // place order of the index (option "nn_walk_index"): 0 = ang_par sector, then the 2D Morton code of the
+  // position; 1 = 3D Morton code of (x, y, rho * heading) in one metric scale (the Dubins key is bounded below by
+  // max(|q|, rho * beta), so tiles compact in that space prune by heading as well as by distance); 2 = the same
+  // with rho * ang_par
+  int index_kind = 0;
   int* wctr = nullptr;  // [8] the per-XCD sample counters
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
@@ -206,6 +211,7 @@ struct WalkBufs {
   int* sids;
   int64_t sorted_n;
   double sorted_x0, sorted_y0, sorted_scale;
+  int sorted_kind;
   int64_t cap_nodes;  // the buffers hold an index of up to this many nodes (checked at every launch)
   int cap_batch;      // and searches of up to this many samples
 };

@@ -84,17 +84,44 @@ __device__ __forceinline__ uint32_t w_spread(uint32_t v) {
   return v;
 }
 
-// Sort key of each node: ang_par sector (3 bits), Morton code of its position in the frame box
-// (non-finite positions last within the sector), then the costE bits (top 29), so records with equal
-// key inputs (e.g. the root's zero-length children of one sector) end up next to each other.
+__device__ __forceinline__ uint64_t w_spread3(uint32_t v) {  // 16 bits -> every third bit of 48
+  uint64_t x = v & 0xffff;
+  x = (x | (x << 16)) & 0x0000ff0000ffull;
+  x = (x | (x << 8)) & 0x00f00f00f00full;
+  x = (x | (x << 4)) & 0x0c30c30c30c3ull;
+  x = (x | (x << 2)) & 0x249249249249ull;
+  return x;
+}
+
+// Sort key of each node (the index's place order; any order gives valid bounds, the order sets how tight they are).
+// kind 0: ang_par sector (3 bits), Morton code of its position in the frame box (non-finite positions last
+// within the sector), then the costE bits (top 29).  kind 1 / 2: 3D Morton code (16 bits per axis) of (x, y,
+// rho * angle) in one metric scale -- angle = the node's heading (kind 1, from the Dubins rotation (c, s) = (cos,
+// sin)(-heading)) or ang_par (kind 2), wrapped to [-pi, pi) -- then the top 16 costE bits.  Records with equal key
+// inputs (e.g. the root's zero-length children) end up next to each other in every kind.
 __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
-                            uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0) {
+                            uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0, int kind = 0) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (k0 >= N - first) return;
   const int i = first + k0;
   keys += -first;  // entries are written at [k0] (keys[i] below)
   vals += -first;
   const double x = nodes[i].x, y = nodes[i].y;
+  if (kind != 0) {
+    const float ang = kind == 1 ? atan2f(-nodes[i].s, nodes[i].c) : (float)nodes[i].ang_par;
+    const double a = isfinite(ang) ? (double)ang - 6.283185307179586 * floor(((double)ang + M_PI) / 6.283185307179586)
+                                   : 0.0;  // [-pi, pi)
+    uint64_t m = 0xffffffffffffull;
+    if (isfinite(x) && isfinite(y)) {
+      const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
+      const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
+      const double fz = fmin(fmax((a + M_PI) * 4.77 * scale, 0.0), 65535.0);
+      m = w_spread3((uint32_t)fx) | (w_spread3((uint32_t)fy) << 1) | (w_spread3((uint32_t)fz) << 2);
+    }
+    keys[i] = (m << 16) | (__float_as_uint(nodes[i].costE) >> 16);
+    vals[i] = i;
+    return;
+  }
   uint32_t k = 0xffffffffu;
   if (isfinite(x) && isfinite(y)) {
     const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
@@ -1263,16 +1290,19 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   if (N > w.cap_nodes) return hipErrorInvalidValue;  // the buffers' shapes (alloc_walk)
   const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
-  const double span = fmax(x1 - x0, y1 - y0);
+  const int kind = w.index_kind;
+  // 3D keys: one metric scale for x, y and rho * angle (2 pi rho = 30 m of the third axis)
+  const double span = kind ? fmax(fmax(x1 - x0, y1 - y0), 2.0 * M_PI * 4.77) : fmax(x1 - x0, y1 - y0);
   const double scale = span > 0 ? 65535.0 / span : 1.0;
   hipError_t e;
   const bool incremental = prev && prev != &w && prev->sorted_n > 0 && prev->sorted_n <= N &&
-                           prev->sorted_x0 == x0 && prev->sorted_y0 == y0 && prev->sorted_scale == scale;
+                           prev->sorted_x0 == x0 && prev->sorted_y0 == y0 && prev->sorted_scale == scale &&
+                           prev->sorted_kind == kind;
   if (incremental) {
     const int n0 = (int)prev->sorted_n, nn = N - n0;
     if (nn > 0) {
       hipLaunchKernelGGL(k_walk_keys, dim3((nn + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
-                         (uint64_t*)w.keys, w.vals, n0);
+                         (uint64_t*)w.keys, w.vals, n0, kind);
       LAUNCH_CHECK3();
       size_t bytes = w.tmp_bytes;
       e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, (uint64_t*)w.keys2, w.vals,
@@ -1291,7 +1321,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
     }
   } else {
     hipLaunchKernelGGL(k_walk_keys, dim3((N + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
-                       (uint64_t*)w.keys, w.vals, 0);
+                       (uint64_t*)w.keys, w.vals, 0, kind);
     LAUNCH_CHECK3();
     size_t bytes = w.tmp_bytes;
     e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, w.skeys, w.vals, w.sids, N, 0, 64,
@@ -1302,6 +1332,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   w.sorted_x0 = x0;
   w.sorted_y0 = y0;
   w.sorted_scale = scale;
+  w.sorted_kind = kind;
   // one-wave blocks (see launch_nn_delta)
   hipLaunchKernelGGL(k_walk_gather, dim3((Npad + 63) / 64), dim3(64), 0, st, nodes, N, Npad, w.sids, fr.ox, fr.oy,
                      w.P, w.Q, w.CE, w.ID, w.vals);

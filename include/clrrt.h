@@ -420,8 +420,9 @@ int clrrt_reset_counters(clrrt_ctx* ctx);
 int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 
 /* Launch-time profile of the last clrrt_expand / round call: device milliseconds per kernel
- * family measured with HIP events on the context stream.  which: 0 = nn, 1 = rollout,
- * 2 = commit; returns the summed ms and the launch count. */
+ * family measured with HIP events on the stream each launch runs on.  which: 0 = nn (index builds,
+ * walk searches, merges), 1 = rollout, 2 = commit, 3 = the walk searches alone (part of 0); returns the
+ * summed ms and the launch count. */
 int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
 int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
 
@@ -444,6 +445,10 @@ int clrrt_nn_stats(clrrt_ctx* ctx, int64_t out[19]);
  * (samples x tree nodes of every search, plus the appended nodes merged into prefetched lists),
  * out[1] = samples searched, out[2] = walk-search tiles visited, out[3] = exact keys evaluated. */
 int clrrt_search_work(clrrt_ctx* ctx, int64_t out[4]);
+/* The same plus the walk's bound work (the hardware roofline basis of the walk search): out[0..3] as
+ * clrrt_search_work, out[4] = phase-1 super-tile bounds (samples x super-tiles of each walk search), out[5] =
+ * super-tile visits (each evaluates its 32 tile bounds), out[6] = records past the prefilter, out[7] = 0. */
+int clrrt_search_work_ex(clrrt_ctx* ctx, int64_t out[8]);
 /* Diagnostics: the context's 64 raw work counters (0..2 rollout work, 8..39 search statistics,
  * 40..63 rollout profile counters of a -DCLRRT_ROLL_PROFILE build: 40..47 per-phase clocks, 48..51 wave
  * lifetimes (sum, max), busiest lane's steps, waves, 52..55 queue-drain times and tail steps). */
