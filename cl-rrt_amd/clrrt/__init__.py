@@ -79,6 +79,9 @@ _SIGS = {
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work_ex": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_tree_truncate": (C.c_int, [C.c_void_p, C.c_int64]),
+    "clrrt_iteration_log": (C.c_int, [C.c_void_p, C.c_int32]),
+    "clrrt_iteration_records": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(abi.Iteration), P(C.c_int64)]),
     "clrrt_obstacle_distance": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32, P(C.c_double)]),
     "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
@@ -450,6 +453,22 @@ class Planner:
         out = (C.c_int64 * 4)()
         self._chk(self.L.clrrt_search_work(self.h, out), "search_work")
         return {"bf_keys": out[0], "samples": out[1], "tiles": out[2], "exact_keys": out[3]}
+
+    def tree_truncate(self, n):
+        """Drop the nodes appended after the first n (clrrt_tree_truncate)."""
+        self._chk(self.L.clrrt_tree_truncate(self.h, int(n)), "tree_truncate")
+
+    def iteration_log(self, on=True):
+        self._chk(self.L.clrrt_iteration_log(self.h, 1 if on else 0), "iteration_log")
+
+    def iterations(self):
+        """The logged per-iteration records (clrrt_iteration_records) as a dict of numpy arrays."""
+        n = C.c_int64()
+        self._chk(self.L.clrrt_iteration_records(self.h, 0, 0, None, C.byref(n)), "iteration_records")
+        arr = (abi.Iteration * max(1, n.value))()
+        self._chk(self.L.clrrt_iteration_records(self.h, 0, n.value, arr, C.byref(n)), "iteration_records")
+        return {f: np.array([getattr(arr[i], f) for i in range(n.value)], dtype=np.int64)
+                for f, _ in abi.Iteration._fields_}
 
     def search_work_ex(self):
         """search_work + the walk's bound work: phase-1 super-tile bounds, super-tile visits (32 tile bounds

@@ -5,7 +5,7 @@ header documents so a drift between the two fails at import time.
 """
 import ctypes as C
 
-CLRRT_ABI_VERSION = 9  # include/clrrt.h
+CLRRT_ABI_VERSION = 10  # include/clrrt.h
 UNIT_OBB, UNIT_ODE, UNIT_LATERAL, UNIT_PROFILE, UNIT_ANGLE = 0, 1, 2, 3, 4  # CLRRT_UNIT_*
 UNIT_DUBINS, UNIT_FEASIBLE, UNIT_GOALBIAS, UNIT_GOALREF, UNIT_CTRL = 5, 6, 7, 8, 9
 UNIT_PROFILE_NMAX = 1024
@@ -71,6 +71,11 @@ class Stats(C.Structure):
     _fields_ = [("iterations", C.c_int64), ("nodes_added", C.c_int64), ("goal_nodes_added", C.c_int64),
                 ("rounds", C.c_int64), ("speculated", C.c_int64), ("elapsed_ms", C.c_double),
                 ("capacity_stop", C.c_int64), ("deferred", C.c_int64)]
+
+
+class Iteration(C.Structure):  # clrrt_iteration
+    _fields_ = [("nodes", C.c_int32), ("sim_count", C.c_int32), ("fail_collision", C.c_int32),
+                ("fail_acclimit", C.c_int32), ("fail_iterlimit", C.c_int32), ("rollouts", C.c_int32)]
 
 
 class Capacity(C.Structure):

@@ -272,6 +272,10 @@ struct clrrt_ctx {
   // write, polled while waiting for the launch
   bool debug_sync = false;
   unsigned long long* dbg_host = nullptr;
+  // clrrt_iteration_log: one record per committed iteration (EXACT / non-deferred BATCH rounds)
+  bool iter_log = false;
+  std::vector<clrrt_iteration> iters;
+  std::vector<SampleOut> iter_tmp;
   // host staging (pinned)
   clrrt_sample* h_samples = nullptr;
   int64_t* h_totals = nullptr;
@@ -916,6 +920,36 @@ int clrrt_tree_load(clrrt_ctx* c, const clrrt_node* nodes, int64_t n) {
   return CLRRT_OK;
 }
 
+int clrrt_tree_truncate(clrrt_ctx* c, int64_t n) {
+  if (!c || n < 1 || n > c->n_nodes) return CLRRT_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  int rc = flush_replays(c);  // pending rows of committed nodes land first (the arena stays consistent)
+  if (rc != CLRRT_OK) return rc;
+  pf_reset(c);  // prefetched lists and kept walk sort results describe the longer tree
+  if (n == c->n_nodes) return CLRRT_OK;
+  clrrt_node h;
+  HIPC(c, hipMemcpyAsync(&h, c->tree + n, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  c->n_nodes = n;
+  if (h.row_offset >= 0 && h.row_offset <= c->n_rows) c->n_rows = h.row_offset;  // rows are appended in node order
+  return CLRRT_OK;  // (the tree's box stays a superset: a valid search frame)
+}
+
+int clrrt_iteration_log(clrrt_ctx* c, int32_t on) {
+  if (!c) return CLRRT_EINVAL;
+  c->iter_log = on != 0;
+  c->iters.clear();
+  return CLRRT_OK;
+}
+
+int clrrt_iteration_records(clrrt_ctx* c, int64_t first, int64_t count, clrrt_iteration* out, int64_t* n_total) {
+  if (!c || first < 0 || count < 0 || first + count > (int64_t)c->iters.size() || (count > 0 && !out))
+    return CLRRT_EINVAL;
+  if (n_total) *n_total = (int64_t)c->iters.size();
+  for (int64_t i = 0; i < count; i++) out[i] = c->iters[first + i];
+  return CLRRT_OK;
+}
+
 int clrrt_tree_size(clrrt_ctx* c, int64_t* n_nodes, int64_t* n_rows) {
   if (!c) return CLRRT_EINVAL;
   if (n_nodes) *n_nodes = c->n_nodes;
@@ -1511,6 +1545,7 @@ static void pf_reset(clrrt_ctx* c) {
   c->nnw_built.n = -1;
   c->nnw.sorted_n = -1;  // the kept sort results describe the old tree
   c->nnw_alt.sorted_n = -1;
+  c->nnw3.sorted_n = -1;
 }
 
 // Launches the walk search of samples h2[0..n2) (host, pinned) over the current tree on the side
@@ -1826,6 +1861,18 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   {
     const int rw = watchdog_check(c);
     if (rw != CLRRT_OK) return rw;
+  }
+  if (c->iter_log && !defer && L > 0) {  // the committed iterations' records, in sample order
+    c->iter_tmp.resize(L);
+    HIPC(c, hipMemcpy(c->iter_tmp.data(), c->so, sizeof(SampleOut) * L, hipMemcpyDeviceToHost));
+    for (int j = 0; j < L; j++) {
+      const SampleOut& o = c->iter_tmp[j];
+      clrrt_iteration r;
+      r.nodes = (o.k >= 0) + (o.k >= 0 && o.gb_ok);
+      r.sim_count = o.steps; r.fail_collision = o.f_col; r.fail_acclimit = o.f_acc; r.fail_iterlimit = o.f_it;
+      r.rollouts = o.rollouts;
+      c->iters.push_back(r);
+    }
   }
   if (merge_bbox) bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
   if (defer) {

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 9
+#define CLRRT_ABI_VERSION 10
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -226,6 +226,22 @@ int clrrt_tree_load(clrrt_ctx* ctx, const clrrt_node* nodes, int64_t n);
 int clrrt_tree_size(clrrt_ctx* ctx, int64_t* n_nodes, int64_t* n_rows);
 int clrrt_tree_download(clrrt_ctx* ctx, int64_t first, int64_t count, clrrt_node* out);
 int clrrt_tree_rows(clrrt_ctx* ctx, int64_t row_offset, int64_t nrows, double* out);
+/* Engine extension (no reference counterpart): drop the nodes [n, size) appended last (and their rows), e.g. the
+ * iterations a caller speculated but did not take (clrrt_adapter's dropin::expandTree cache). 1 <= n <= size. */
+int clrrt_tree_truncate(clrrt_ctx* ctx, int64_t n);
+
+/* Per-iteration record of the expandTree iterations an expansion commits, in iteration order (clrrt_iteration_log
+ * on; EXACT rounds and BATCH rounds without deferred samples): the nodes the iteration appended (0, 1 regular, 2
+ * regular + goal-biased, rrtplanner.cpp:150-173) and its share of the reference's counters (rrt_node.cpp:21-24:
+ * sim_count, fail_collision, fail_acclimit, fail_iterlimit) and rollouts. */
+typedef struct clrrt_iteration {
+  int32_t nodes;
+  int32_t sim_count, fail_collision, fail_acclimit, fail_iterlimit, rollouts;
+} clrrt_iteration;
+/* on != 0: start (or restart) logging, clearing the records; 0: stop and clear. */
+int clrrt_iteration_log(clrrt_ctx* ctx, int32_t on);
+/* Records logged so far (*n_total), and records [first, first + count) into out. */
+int clrrt_iteration_records(clrrt_ctx* ctx, int64_t first, int64_t count, clrrt_iteration* out, int64_t* n_total);
 
 /* extractBestPath (rrtplanner.cpp:318-368; declared rrtplanner.h:92): among the nodes with
  * goalReached set, in tree order, the front after the reference's std::sort by costS (ascending,

@@ -151,6 +151,7 @@ class Engine {
   clrrt_ctx* ctx() { return ctx_; }
   const clrrt_params& params() const { return p_; }
   void set_params(const clrrt_params& p) {
+    drop_cache();
     check(ctx_, clrrt_set_params(ctx_, &p), "clrrt_set_params");
     p_ = p;
   }
@@ -166,6 +167,7 @@ class Engine {
 
   template <class ObsVec>
   void set_obstacles(const ObsVec& det) {
+    drop_cache();
     std::vector<clrrt_obstacle> o;
     o.reserve(det.size());
     for (const auto& d : det) o.push_back(obstacle_to_c(d));
@@ -177,6 +179,7 @@ class Engine {
   /* The device tree := RRT.tree (e.g. after MyRRT::addInitialNode or initializeTree). */
   template <class RRTT>
   void load_tree(const RRTT& rrt) {
+    spec_ = Spec{};
     std::vector<clrrt_node> h;
     h.reserve(rrt.tree.size());
     for (const auto& n : rrt.tree) h.push_back(node_to_c(n));
@@ -187,7 +190,10 @@ class Engine {
   }
   /* Forget the synced tree: the next expansion reloads RRT.tree (call after replacing RRT.tree by other
    * means than expansion; a changed root or last synced node is also detected by itself). */
-  void invalidate() { synced_ = -1; }
+  void invalidate() {
+    drop_cache();
+    synced_ = -1;
+  }
 
   /* The rand() stream (srand(seed) semantics) the expansion draws from; rng() for the explicit form. */
   void srand(uint32_t seed) { clrrt_rng_seed(&rng_, seed); }
@@ -209,13 +215,22 @@ class Engine {
 
   /* expandTree (rrtplanner.h:87): one iteration (exactly three rand() draws of the engine's stream and of
    * the process's), appending 0-2 nodes to RRT.tree, bumping the counters; the detections `det` are
-   * (re)loaded when they differ from the last ones loaded. */
+   * (re)loaded when they differ from the last ones loaded.
+   *
+   * Served from a speculation cache (set_speculation; on by default): the reference's Timer loop
+   * (motionplanner.cpp:39-43) calls expandTree once per iteration, and one GPU round per call would run at
+   * the round's latency.  The first call of a query expands the next `width` iterations at once in EXACT mode
+   * (the reference's sequential tree, bit for bit) on the device with the per-iteration log on, and each call
+   * appends one iteration's nodes (0-2) from the cache and its share of the counters; the cache is re-made,
+   * twice as wide up to the cap, when it runs out, and dropped (the device tree truncated back) when anything it
+   * was made for changes: RRT.tree (a new query, an edited tree), the stream state, the obstacles, the
+   * parameters.  Iterations speculated but never served are discarded. */
   template <class VehicleT, class RRTT, class PubT, class ObsVec>
   void expandTree(VehicleT&, RRTT& RRT, PubT* /*ptrPub (unused)*/, const ObsVec& det,
                   const std::vector<double>& /*Cxy (unused)*/) {
     sync_obstacles(det);
     int64_t c[4] = {0, 0, 0, 0};
-    run(RRT, rng_, 1, 0.0, CLRRT_MODE_EXACT, 16, c);
+    one_iteration(RRT, rng_, c);
     for (int i = 0; i < 3; i++) (void)rand();
     for (int i = 0; i < 4; i++) {
       counters_[i] += c[i];
@@ -227,9 +242,19 @@ class Engine {
   void expandTree(VehicleT&, RRTT& rrt, void* /*ros::Publisher* (unused)*/, const ObsVec& det,
                   const std::vector<double>& /*Cxy (unused)*/, clrrt_rng& rng, int64_t counters[4]) {
     sync_obstacles(det);
-    run(rrt, rng, 1, 0.0, CLRRT_MODE_EXACT, 16, counters);
+    one_iteration(rrt, rng, counters);
     for (int i = 0; i < 3; i++) (void)rand();
   }
+  /* The speculation of expandTree: the first cache of a query holds `width0` iterations, each next one twice as
+   * many up to `width_max`; width0 = 0: no cache (one device round per call). */
+  void set_speculation(int64_t width0, int64_t width_max) {
+    drop_cache();
+    spec_w0_ = std::max<int64_t>(0, width0);
+    spec_wmax_ = std::max(spec_w0_, width_max);
+  }
+  /* Iterations served from caches, and speculated in all (statistics). */
+  int64_t served_iterations() const { return spec_served_; }
+  int64_t speculated_iterations() const { return spec_made_; }
 
   /* The planMotion Timer loop (motionplanner.cpp:39-43) as one call: EXACT reproduces the reference's
    * tree for the same rand() stream, BATCH is the throughput mode.  Returns the iterations consumed. */
@@ -277,9 +302,124 @@ class Engine {
     if (!same) set_obstacles(det);
   }
 
+  /* The speculation cache: headers and rows of `count` iterations' nodes expanded past RRT.tree's first
+   * tree_size nodes from stream state `rng0`; `next` of them served. */
+  struct Spec {
+    bool valid = false;
+    clrrt_rng next_rng{};         // the stream state before iteration `next`
+    int64_t next = 0, count = 0;
+    int64_t tree_size = 0;        // RRT.tree.size() expected before serving iteration `next`
+    clrrt_node last{};            // and RRT.tree.back()
+    int64_t dev_base = 0;         // device tree size before the cache's nodes
+    std::vector<clrrt_iteration> its;
+    std::vector<int64_t> off;     // first cached node of each iteration
+    std::vector<clrrt_node> hdr;
+    std::vector<std::vector<double>> rows;
+    int64_t width = 0;            // iterations of the next cache
+  };
+  /* The device tree back to RRT.tree (the served prefix) and no cache. */
+  void drop_cache() {
+    if (spec_.valid) {
+      const int64_t keep = spec_.dev_base + (spec_.next < (int64_t)spec_.off.size() ? spec_.off[spec_.next]
+                                                                                     : (int64_t)spec_.hdr.size());
+      if (keep >= 1 && clrrt_tree_truncate(ctx_, keep) == CLRRT_OK) {
+        synced_ = keep;
+        last_ = spec_.last;  // RRT.tree.back() when the last iteration was served = device node keep - 1
+      } else {
+        synced_ = -1;
+      }
+    }
+    spec_ = Spec{};
+  }
+  static bool same_rng(const clrrt_rng& a, const clrrt_rng& b) {
+    for (int i = 0; i < 34; i++)
+      if (a.r[i] != b.r[i]) return false;
+    return a.pos == b.pos;
+  }
+  template <class RRTT>
+  bool cache_serves(const RRTT& rrt, const clrrt_rng& rng) const {
+    return spec_.valid && spec_.next < spec_.count && (int64_t)rrt.tree.size() == spec_.tree_size &&
+           !rrt.tree.empty() && same_node(node_to_c(rrt.tree.back()), spec_.last) && same_rng(rng, spec_.next_rng);
+  }
+  template <class RRTT>
+  void one_iteration(RRTT& rrt, clrrt_rng& rng, int64_t counters[4]) {
+    if (spec_w0_ <= 0 || full_ref_) {  // one device round per call
+      run(rrt, rng, 1, 0.0, CLRRT_MODE_EXACT, 16, counters);
+      return;
+    }
+    if (!cache_serves(rrt, rng)) speculate(rrt, rng);
+    const int64_t i = spec_.next;
+    const clrrt_iteration& it = spec_.its[(size_t)i];
+    using NodeT = typename std::decay<decltype(rrt.tree[0])>::type;
+    for (int64_t k = spec_.off[(size_t)i]; k < spec_.off[(size_t)i] + it.nodes; k++)
+      rrt.tree.push_back(node_from_c<NodeT>(spec_.hdr[(size_t)k], spec_.rows[(size_t)k].data()));
+    if (counters) {
+      counters[0] += it.sim_count;
+      counters[1] += it.fail_collision;
+      counters[2] += it.fail_acclimit;
+      counters[3] += it.fail_iterlimit;
+    }
+    for (int q = 0; q < 3; q++) clrrt_rng_next(&rng);
+    spec_.next_rng = rng;
+    spec_.next++;
+    spec_.tree_size = (int64_t)rrt.tree.size();
+    spec_.last = node_to_c(rrt.tree.back());
+    spec_served_++;
+  }
+  /* A new cache for the iterations that follow RRT.tree and the stream state rng. */
+  template <class RRTT>
+  void speculate(RRTT& rrt, const clrrt_rng& rng) {
+    // the device tree: RRT.tree is the served prefix of the old cache's (truncate), or reload it
+    const bool prefix = spec_.valid && (int64_t)rrt.tree.size() == spec_.tree_size && !rrt.tree.empty() &&
+                        same_node(node_to_c(rrt.tree.back()), spec_.last);
+    const int64_t width = prefix && spec_.width > 0 ? spec_.width : spec_w0_;
+    drop_cache();
+    if (!prefix || synced_ != (int64_t)rrt.tree.size()) load_tree(rrt);
+    Spec s;
+    s.dev_base = (int64_t)rrt.tree.size();
+    clrrt_rng work = rng;
+    check(ctx_, clrrt_iteration_log(ctx_, 1), "clrrt_iteration_log");
+    clrrt_stats st;
+    const int rc = clrrt_expand(ctx_, &work, width, 0.0, CLRRT_MODE_EXACT, 256, &st);
+    if (rc != CLRRT_OK) clrrt_iteration_log(ctx_, 0);
+    check(ctx_, rc, "clrrt_expand");
+    s.its.resize((size_t)st.iterations);
+    int64_t total = 0;
+    if (st.iterations > 0)
+      check(ctx_, clrrt_iteration_records(ctx_, 0, st.iterations, s.its.data(), &total), "clrrt_iteration_records");
+    check(ctx_, clrrt_iteration_log(ctx_, 0), "clrrt_iteration_log");
+    int64_t n = 0, nr = 0;
+    check(ctx_, clrrt_tree_size(ctx_, &n, &nr), "clrrt_tree_size");
+    s.hdr.resize((size_t)(n - s.dev_base));
+    if (n > s.dev_base) check(ctx_, clrrt_tree_download(ctx_, s.dev_base, n - s.dev_base, s.hdr.data()), "clrrt_tree_download");
+    s.rows.resize(s.hdr.size());
+    for (size_t k = 0; k < s.hdr.size(); k++) {
+      s.rows[k].resize(10 * (size_t)s.hdr[k].nrows);
+      check(ctx_, clrrt_tree_rows(ctx_, s.hdr[k].row_offset, s.hdr[k].nrows, s.rows[k].data()), "clrrt_tree_rows");
+    }
+    s.off.resize(s.its.size());
+    int64_t o = 0;
+    for (size_t i = 0; i < s.its.size(); i++) {
+      s.off[i] = o;
+      o += s.its[i].nodes;
+    }
+    if (o != (int64_t)s.hdr.size()) throw Error("expandTree cache: the iteration log does not match the nodes appended");
+    s.valid = st.iterations > 0;
+    s.next_rng = rng;
+    s.count = st.iterations;
+    s.tree_size = (int64_t)rrt.tree.size();
+    s.last = node_to_c(rrt.tree.back());
+    s.width = std::min(spec_wmax_, 2 * width);
+    spec_ = std::move(s);
+    spec_made_ += st.iterations;
+    synced_ = -1;  // the device holds the cache's nodes beyond RRT.tree (drop_cache truncates them)
+    if (!spec_.valid) throw Error("expandTree cache: the expansion consumed no iteration");
+  }
+
   template <class RRTT>
   int64_t run(RRTT& rrt, clrrt_rng& rng, int64_t n_iters, double budget_ms, int32_t mode, int32_t batch,
               int64_t counters[4]) {
+    drop_cache();
     if (!tree_synced(rrt)) load_tree(rrt);
     const clrrt_rng rng0 = rng;
     clrrt_counters c0, c1;
@@ -388,6 +528,9 @@ class Engine {
   int* gc_[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<clrrt_obstacle> det_;
   bool det_set_ = false;
+  Spec spec_;
+  int64_t spec_w0_ = 32, spec_wmax_ = 512;
+  int64_t spec_served_ = 0, spec_made_ = 0;
 };
 
 /* The step h of a reference coordinate built by LinearSpacedVector (functions.h:11-21: val += h from v[0]):

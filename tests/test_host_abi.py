@@ -17,7 +17,7 @@ def _header_functions():
 
 def test_library_loads_and_exports_every_header_symbol():
     L = clrrt.lib()
-    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 9
+    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 10
     declared = _header_functions()
     assert len(declared) >= 25
     out = subprocess.run(["nm", "-D", "--defined-only", clrrt.LIB_PATH], capture_output=True, text=True).stdout

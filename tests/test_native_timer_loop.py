@@ -1,0 +1,80 @@
+"""The reference's unchanged Timer(200) loop (motionplanner.cpp:39-43, Timer rrtplanner.h:11-25) through the drop-in
+expandTree (clrrt_adapter::dropin, its speculation cache) in a native program linked against libclrrt
+(tests/native/timer_loop.cpp): the tree it grows in one 200 ms (CPU time) query equals the oracle's sequential
+expandTree (rrtplanner.cpp:123-174) after the same number of iterations, node for node and bit for bit (state,
+float costs, parents, goal flags, trajectory row hashes) with the reference's failure counters, and it grows at
+GPU speed (>= 1000 nodes per wall-clock second; one device round per call ran at ~200)."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from clrrt import abi, scenes
+from oracle_binding import Oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "timer_loop")
+
+
+def fnv1a(b):
+    h = 0xcbf29ce484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_timer_loop_program_compiles_against_the_header():
+    """CPU: the program and the adapter compile (host C++ only)."""
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "timer_loop.cpp")], check=True)
+
+
+def _read(path):
+    b = open(path, "rb").read()
+    it, n = struct.unpack_from("<ii", b, 0)
+    cnt = struct.unpack_from("<4i", b, 8)
+    off, rec = 24, 12 + 80 + 8 + 8
+    nodes = []
+    for _ in range(n):
+        parent, goal, nrows = struct.unpack_from("<3i", b, off)
+        state = np.frombuffer(b, dtype="<f8", count=10, offset=off + 12).copy()
+        ce, cs = struct.unpack_from("<II", b, off + 92)
+        h, = struct.unpack_from("<Q", b, off + 100)
+        nodes.append((parent, goal, nrows, state, ce, cs, h))
+        off += rec
+    return it, cnt, nodes
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", [3, 5])
+def test_timer_loop_dropin_matches_oracle(tmp_path, seed):
+    assert os.path.exists(EXE), "tests/native/timer_loop not built (make -C cl-rrt_amd/csrc)"
+    obs = scenes.urban_scene(200)
+    obs_path = tmp_path / "obs.bin"
+    obs_path.write_bytes(np.ascontiguousarray(obs, dtype="<f8").tobytes())
+    out_path = tmp_path / "tree.bin"
+    r = subprocess.run([EXE, str(obs_path), str(seed), "200", str(out_path)], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    iters, cnt, nodes = _read(out_path)
+    o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+    Oracle.srand(seed)
+    o.init_tree()
+    o.expand(iters)
+    on = o.nodes()
+    assert len(nodes) == len(on["parent"]) > 50
+    for i, (parent, goal, nrows, state, ce, cs, h) in enumerate(nodes):
+        same = (parent == on["parent"][i] and goal == on["goal"][i] and nrows == on["nrows"][i]
+                and np.array_equal(state.view(np.uint64), on["state"][i].view(np.uint64))
+                and ce == int(on["costE"][i:i + 1].view(np.uint32)[0]) and cs == int(on["costS"][i:i + 1].view(np.uint32)[0]))
+        if i > 0:
+            same = same and h == fnv1a(np.ascontiguousarray(o.rows(i)).tobytes())
+        assert same, f"node {i} differs"
+    oc = o.counters()
+    assert list(cnt) == [oc["sim_count"], oc["fail_collision"], oc["fail_acclimit"], oc["fail_iterlimit"]]
+    rate = float(r.stdout.split(" nodes/s")[0].split(": ")[-1])
+    assert rate >= 1000.0, r.stdout
