@@ -233,7 +233,7 @@ struct clrrt_ctx {
     uint8_t* pend = nullptr;      // [vcap]
     void* sel_tmp = nullptr;
     size_t sel_bytes = 0;
-    int* d_cnt = nullptr;         // [2] selected views, suspended chains (device)
+    int* d_cnt = nullptr;         // [3] selected views, suspended chains, this round's samples left pending (device)
     void* carry[2] = {nullptr, nullptr};
     int cur_c = 0, ncarry = 0, carry_cap = 0;
     int64_t round = 0;            // rounds of the current expansion
@@ -1810,7 +1810,9 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     s.sbase = d.slot * (int)c->cap.max_batch;
     s.gv = d.gv;
     s.pend = d.pend;
+    s.new_pend = d.d_cnt + 2;
     s.B = d.nd + n;
+    HIPC(c, hipMemsetAsync(d.d_cnt + 2, 0, sizeof(int), st));
   }
   c->def.nd_eval = defer ? c->def.nd : -1;
   {
@@ -1855,6 +1857,7 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   if (merge_bbox) HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
   if (defer) {
     HIPC(c, hipMemcpyAsync(c->h_int, d.d_cnt, sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+    HIPC(c, hipMemcpyAsync(c->h_int + 3, d.d_cnt + 2, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPC(c, hipMemcpyAsync(c->h_int + 2, (const char*)(c->work_ctr + 62), sizeof(int), hipMemcpyDeviceToHost, st));
   }
   HIPC(c, hipStreamSynchronize(st));
@@ -1878,7 +1881,7 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
   if (defer) {
     if (c->h_int[2] != 0 || c->h_int[1] > d.carry_cap)
       return fail(c, CLRRT_ECAPACITY, "suspended rollouts exceed the carry buffer (raise defer_steps)");
-    d.deferred_total += std::max(0, c->h_int[0] - d.nd_eval);  // this round's samples that stay pending
+    if (L > 0) d.deferred_total += c->h_int[3];  // this round's samples left pending (k_select)
     d.cur_dl ^= 1;
     d.nd = c->h_int[0];
     d.cur_c ^= 1;
@@ -1976,7 +1979,7 @@ static int ensure_defer(clrrt_ctx* c) {
     HIPC(c, dalloc(&d.pend, V));
     d.sel_bytes = defer_select_bytes((int)V);
     HIPC(c, hipMalloc(&d.sel_tmp, std::max<size_t>(d.sel_bytes, 256)));
-    HIPC(c, dalloc(&d.d_cnt, 2));
+    HIPC(c, dalloc(&d.d_cnt, 3));
     // suspended chains: at most every job of the rounds in flight (a launch's chains all come from them)
     d.carry_cap = (int)std::min<int64_t>(V * CAND_K, 1 << 21);
     HIPC(c, hipMalloc(&d.carry[0], carry_bytes() * (size_t)d.carry_cap));

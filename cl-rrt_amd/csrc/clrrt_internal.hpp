@@ -153,6 +153,7 @@ struct SelArgs {
   int nd, sbase;
   int* gv;                           // [B] ring index of view v (null: not needed)
   uint8_t* pend;                     // [B] 1 = view v is not resolved yet (null: every sample resolves)
+  int* new_pend;                     // counts this round's samples (views >= nd) left pending (null: no count)
 };
 
 // Frame of the brute-force search's float prune: positions relative to (ox, oy) in float are within

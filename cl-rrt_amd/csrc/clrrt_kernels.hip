@@ -1831,6 +1831,7 @@ __global__ void k_select(SelArgs a) {
     a.so[v] = z;
     if (a.gv) a.gv[v] = g;
     if (a.pend) a.pend[v] = 1;
+    if (a.new_pend && v >= a.nd) atomicAdd(a.new_pend, 1);  // a sample of this round deferred (statistics)
     return;
   }
   if (a.gv) a.gv[v] = g;
