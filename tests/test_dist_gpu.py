@@ -37,8 +37,10 @@ def _free_port():
 def _planner(world=WORLD):
     import clrrt
     from clrrt import abi, scenes
+    # (the single-process reference runs world x B samples per round: its conservative arena check wants room for
+    # 2 full-horizon rows per sample of a round + its deferred samples)
     pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), device=0, max_nodes=1 << 18,
-                       max_rows=1 << 25, max_batch=world * B)
+                       max_rows=(1 << 25) * max(1, world // 2), max_batch=world * B)
     pl.set_obstacles(scenes.urban_scene(200))
     pl.tree_init()
     return pl
