@@ -1319,7 +1319,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
-  else if (k == "nn_walk_index" && value >= 0 && value <= 2) {
+  else if (k == "nn_walk_index" && value >= 0 && value <= 4) {
     c->nnw_index = (int)value;
     c->nnw_built.n = -1;  // the kept index and sort results have the old order
     c->nnw.sorted_n = c->nnw_alt.sorted_n = c->nnw3.sorted_n = -1;

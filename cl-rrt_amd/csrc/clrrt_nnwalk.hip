@@ -97,7 +97,8 @@ __device__ __forceinline__ uint64_t w_spread3(uint32_t v) {  // 16 bits -> every
 // kind 0: ang_par sector (3 bits), Morton code of its position in the frame box (non-finite positions last
 // within the sector), then the costE bits (top 29).  kind 1 / 2: 3D Morton code (16 bits per axis) of (x, y,
 // rho * angle) in one metric scale -- angle = the node's heading (kind 1, from the Dubins rotation (c, s) = (cos,
-// sin)(-heading)) or ang_par (kind 2), wrapped to [-pi, pi) -- then the top 16 costE bits.  Records with equal key
+// sin)(-heading)) or ang_par (kind 2), wrapped to [-pi, pi) -- then the top 16 costE bits.  kind 3 / 4: the
+// ang_par sector, then kind 1's / kind 2's 3D code, then the top 13 costE bits.  Records with equal key
 // inputs (e.g. the root's zero-length children) end up next to each other in every kind.
 __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
                             uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0, int kind = 0) {
@@ -107,8 +108,28 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   keys += -first;  // entries are written at [k0] (keys[i] below)
   vals += -first;
   const double x = nodes[i].x, y = nodes[i].y;
+  // ang_par octant (kinds 0, 3, 4)
+  const float apf = (float)nodes[i].ang_par;
+  int bin = (int)floorf((apf + 3.14159265f) * (WALK_APBINS / 6.2831853f));
+  bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
+  if (kind >= 3) {  // octant, then the 3D Morton code of (x, y, rho * heading | ang_par) inside it
+    const float ang = kind == 3 ? atan2f(-nodes[i].s, nodes[i].c) : apf;
+    const double a = isfinite(ang) ? (double)ang - 6.283185307179586 * floor(((double)ang + M_PI) / 6.283185307179586)
+                                   : 0.0;  // [-pi, pi)
+    uint64_t m = 0xffffffffffffull;
+    if (isfinite(x) && isfinite(y)) {
+      const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
+      const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
+      const double fz = fmin(fmax((a + M_PI) * 4.77 * scale, 0.0), 65535.0);
+      m = w_spread3((uint32_t)fx) | (w_spread3((uint32_t)fy) << 1) | (w_spread3((uint32_t)fz) << 2);
+    }
+    keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | (m << (16 - WALK_SECTOR_BITS)) |
+              (__float_as_uint(nodes[i].costE) >> (16 + WALK_SECTOR_BITS));
+    vals[i] = i;
+    return;
+  }
   if (kind != 0) {
-    const float ang = kind == 1 ? atan2f(-nodes[i].s, nodes[i].c) : (float)nodes[i].ang_par;
+    const float ang = kind == 1 ? atan2f(-nodes[i].s, nodes[i].c) : apf;
     const double a = isfinite(ang) ? (double)ang - 6.283185307179586 * floor(((double)ang + M_PI) / 6.283185307179586)
                                    : 0.0;  // [-pi, pi)
     uint64_t m = 0xffffffffffffull;
@@ -130,9 +151,6 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   }
   // ang_par octant first: tiles then hold similar reference directions, which sharpens the tiles'
   // feasibleNode bound (measured: 555 -> 332 tiles per explore sample, same work for optimize)
-  const float a = (float)nodes[i].ang_par;
-  int bin = (int)floorf((a + 3.14159265f) * (WALK_APBINS / 6.2831853f));
-  bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
   keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | ((uint64_t)k << (32 - WALK_SECTOR_BITS)) |
             (__float_as_uint(nodes[i].costE) >> WALK_SECTOR_BITS);
   vals[i] = i;
@@ -1293,6 +1311,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   const int kind = w.index_kind;
   // 3D keys: one metric scale for x, y and rho * angle (2 pi rho = 30 m of the third axis)
   const double span = kind ? fmax(fmax(x1 - x0, y1 - y0), 2.0 * M_PI * 4.77) : fmax(x1 - x0, y1 - y0);
+  // (kinds 3 / 4 keep the sector on top: the same scale)
   const double scale = span > 0 ? 65535.0 / span : 1.0;
   hipError_t e;
   const bool incremental = prev && prev != &w && prev->sorted_n > 0 && prev->sorted_n <= N &&

@@ -246,7 +246,9 @@ class Engine {
     for (int i = 0; i < 3; i++) (void)rand();
   }
   /* The speculation of expandTree: the first cache of a query holds `width0` iterations, each next one twice as
-   * many up to `width_max`; width0 = 0: no cache (one device round per call). */
+   * many up to `width_max` (default 32 / 64: the loop's Timer stops while a cache is partly served, and what is
+   * left of it was computed for nothing -- a 256-iteration cache wasted ~60% of a 200 ms query); width0 = 0: no
+   * cache (one device round per call). */
   void set_speculation(int64_t width0, int64_t width_max) {
     drop_cache();
     spec_w0_ = std::max<int64_t>(0, width0);
@@ -393,9 +395,18 @@ class Engine {
     s.hdr.resize((size_t)(n - s.dev_base));
     if (n > s.dev_base) check(ctx_, clrrt_tree_download(ctx_, s.dev_base, n - s.dev_base, s.hdr.data()), "clrrt_tree_download");
     s.rows.resize(s.hdr.size());
-    for (size_t k = 0; k < s.hdr.size(); k++) {
-      s.rows[k].resize(10 * (size_t)s.hdr[k].nrows);
-      check(ctx_, clrrt_tree_rows(ctx_, s.hdr[k].row_offset, s.hdr[k].nrows, s.rows[k].data()), "clrrt_tree_rows");
+    if (!s.hdr.empty()) {  // the expansion's rows are one contiguous range of the arena: one download
+      int64_t r0 = INT64_MAX, r1 = 0;
+      for (const auto& h : s.hdr) {
+        r0 = std::min<int64_t>(r0, h.row_offset);
+        r1 = std::max<int64_t>(r1, h.row_offset + h.nrows);
+      }
+      std::vector<double> all(10 * (size_t)(r1 - r0));
+      check(ctx_, clrrt_tree_rows(ctx_, r0, r1 - r0, all.data()), "clrrt_tree_rows");
+      for (size_t k = 0; k < s.hdr.size(); k++) {
+        const double* src = all.data() + 10 * (size_t)(s.hdr[k].row_offset - r0);
+        s.rows[k].assign(src, src + 10 * (size_t)s.hdr[k].nrows);
+      }
     }
     s.off.resize(s.its.size());
     int64_t o = 0;
@@ -529,7 +540,7 @@ class Engine {
   std::vector<clrrt_obstacle> det_;
   bool det_set_ = false;
   Spec spec_;
-  int64_t spec_w0_ = 32, spec_wmax_ = 512;
+  int64_t spec_w0_ = 32, spec_wmax_ = 64;
   int64_t spec_served_ = 0, spec_made_ = 0;
 };
 
