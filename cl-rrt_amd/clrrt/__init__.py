@@ -81,6 +81,7 @@ _SIGS = {
     "clrrt_search_work_ex": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_tree_truncate": (C.c_int, [C.c_void_p, C.c_int64]),
     "clrrt_iteration_log": (C.c_int, [C.c_void_p, C.c_int32]),
+    "clrrt_exact_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_iteration_records": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, P(abi.Iteration), P(C.c_int64)]),
     "clrrt_obstacle_distance": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32, P(C.c_double)]),
     "clrrt_debug_counters": (C.c_int, [C.c_void_p, P(C.c_int64)]),
@@ -457,6 +458,11 @@ class Planner:
     def tree_truncate(self, n):
         """Drop the nodes appended after the first n (clrrt_tree_truncate)."""
         self._chk(self.L.clrrt_tree_truncate(self.h, int(n)), "tree_truncate")
+
+    def exact_stats(self):
+        out = (C.c_int64 * 4)()
+        self._chk(self.L.clrrt_exact_stats(self.h, out), "exact_stats")
+        return {"rounds": out[0], "resolved": out[1], "fixup_rollouts": out[2], "conflict_rounds": out[3]}
 
     def iteration_log(self, on=True):
         self._chk(self.L.clrrt_iteration_log(self.h, 1 if on else 0), "iteration_log")

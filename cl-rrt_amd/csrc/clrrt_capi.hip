@@ -113,7 +113,7 @@ struct clrrt_ctx {
   // round, 8192 -> 45.6 vs 58-59 ms; 8 M: 3072 stays best, 25.8 vs 29.9 ms at 8192, profiles/r04as)
   bool nnw_bud_tiles_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
-  int nnw_index = 0;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind)
+  int nnw_index = 3;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind); 3 since round 5
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
   // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
@@ -143,6 +143,20 @@ struct clrrt_ctx {
   int roll_lanes = 0;         // option "roll_lanes": lanes per wave that take jobs (0: 64, or fewer by roll_spread)
   int nn_exact_fused = 1;     // option "nn_exact_fused": EXACT lists of small trees by k_nn_exact_fused
   int exact_min_width = 8;    // option "exact_min_width": EXACT rounds speculate at least this many samples
+  // option "exact_fixup" (default 1): EXACT rounds resolve a conflict by rolling out the conflicting new nodes for
+  // the sample (k_conflict_fix) instead of ending the committed prefix there, when that decides it
+  int exact_fixup = 1;
+  int* fix_n = nullptr;        // [max_batch]
+  int* fix_ids = nullptr;      // [max_batch * FIX_MAX]
+  Job* fix_jobs = nullptr;     // [max_batch * FIX_MAX]
+  RollRes* fix_res = nullptr;  // [max_batch * FIX_MAX]
+  std::vector<int> h_fix;      // fix_n then fix_ids
+  std::vector<clrrt_sample> h_fix_smp;
+  std::vector<Job> h_fix_jobs;
+  std::vector<int> h_fix_owner;
+  std::vector<RollRes> h_fix_res;
+  std::vector<SampleOut> h_fix_so;
+  int64_t ex_stats[4] = {0, 0, 0, 0};  // EXACT: rounds, conflicts resolved, fix-up rollouts, conflicts left
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
@@ -538,7 +552,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun, c->nnw.wctr, c->nnw_alt.wctr, c->nnw3.wctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
-  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal};
+  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal, c->fix_n, c->fix_ids, c->fix_jobs, c->fix_res};
   for (void* p : sptrs)
     if (p) hipFree(p);
   void* dptrs[] = {c->def.res, c->def.res_gb, c->def.cand, c->def.ncand, c->def.samp, c->def.best, c->def.dlist[0],
@@ -933,6 +947,12 @@ int clrrt_tree_truncate(clrrt_ctx* c, int64_t n) {
   c->n_nodes = n;
   if (h.row_offset >= 0 && h.row_offset <= c->n_rows) c->n_rows = h.row_offset;  // rows are appended in node order
   return CLRRT_OK;  // (the tree's box stays a superset: a valid search frame)
+}
+
+int clrrt_exact_stats(clrrt_ctx* c, int64_t out[4]) {
+  if (!c || !out) return CLRRT_EINVAL;
+  for (int i = 0; i < 4; i++) out[i] = c->ex_stats[i];
+  return CLRRT_OK;
 }
 
 int clrrt_iteration_log(clrrt_ctx* c, int32_t on) {
@@ -1348,6 +1368,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     c->rows_deferred = value != 0;
   }
   else if (k == "exact_min_width" && value >= 1 && value <= 1 << 20) c->exact_min_width = (int)value;
+  else if (k == "exact_fixup") c->exact_fixup = value != 0;
   else if (k == "defer_steps" && value >= 0 && value <= 1 << 20) {
     // BATCH rounds with deferred samples (changes the BATCH tree: samples whose rollouts run past T steps
     // per launch commit in a later round, by a deterministic rule the oracle restates); 0 = off
@@ -1662,6 +1683,102 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
   return CLRRT_OK;
 }
 
+// EXACT mode, stage 5 with fix-ups (k_conflict_fix): the committed prefix of the round's n samples runs up to the
+// first sample whose conflict is not resolvable or whose fix-up rollouts (the conflicting new nodes rolled out
+// for it, one job per wave) are not all failures; the resolved samples' counters take the fix-ups.  *L: the prefix.
+static int exact_fixups(clrrt_ctx* c, int n, int* L) {
+  hipStream_t st = c->stream;
+  const int64_t B = c->cap.max_batch;
+  if (!c->fix_n) {
+    HIPC(c, dalloc(&c->fix_n, B));
+    HIPC(c, dalloc(&c->fix_ids, B * FIX_MAX));
+    HIPC(c, dalloc(&c->fix_jobs, B * FIX_MAX));
+    HIPC(c, dalloc(&c->fix_res, B * FIX_MAX));
+  }
+  HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->fix_n,
+                              c->fix_ids));
+  c->h_fix.resize((size_t)n * (1 + FIX_MAX));
+  c->h_fix_smp.resize(n);
+  c->h_fix_so.resize(n);
+  HIPC(c, hipMemcpyAsync(c->h_fix.data(), c->fix_n, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix.data() + n, c->fix_ids, sizeof(int) * n * FIX_MAX, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix_smp.data(), c->d_samples, sizeof(clrrt_sample) * n, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix_so.data(), c->so, sizeof(SampleOut) * n, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  const int* fn = c->h_fix.data();
+  const int* fid = c->h_fix.data() + n;
+  int stop = n;
+  c->h_fix_jobs.clear();
+  c->h_fix_owner.clear();
+  for (int j = 0; j < n; j++) {
+    if (fn[j] < 0) { stop = j; break; }
+    for (int i = 0; i < fn[j]; i++) {
+      Job jb;
+      const int id = fid[j * FIX_MAX + i];
+      jb.parent = id >> 1;
+      jb.from_reg = 1 + (id & 1);
+      jb.gb = 0;
+      jb.pad = 0;
+      jb.sx = c->h_fix_smp[j].x;
+      jb.sy = c->h_fix_smp[j].y;
+      jb.row_off = -1;
+      c->h_fix_jobs.push_back(jb);
+      c->h_fix_owner.push_back(j);
+    }
+  }
+  const int nj = (int)c->h_fix_jobs.size();
+  c->h_fix_res.resize(nj);
+  if (nj > 0) {
+    HIPC(c, hipMemcpyAsync(c->fix_jobs, c->h_fix_jobs.data(), sizeof(Job) * nj, hipMemcpyHostToDevice, st));
+    RollArgs a = roll_args(c, nj);
+    a.jobs = c->fix_jobs;
+    a.res = c->fix_res;
+    a.res_gb = c->fix_res;  // (SRC_LIST runs no goal-biased pass)
+    a.xreg = c->regnodes;
+    a.xgb = c->gbnodes;
+    a.job_stride = 64;  // one job per wave: the fix-ups run at the lone lane's step latency
+    {
+      KTimer kt(c, 1);
+      HIPC(c, launch_rollout(st, SRC_LIST, a));
+    }
+    HIPC(c, hipMemcpyAsync(c->h_fix_res.data(), c->fix_res, sizeof(RollRes) * nj, hipMemcpyDeviceToHost, st));
+    HIPC(c, hipStreamSynchronize(st));
+  }
+  // in sample order: a fix-up that succeeds changes the sample's result (it ends the prefix); all failed: the
+  // sample stands, with the reference's counters for the extra rollouts
+  int Lr = stop, resolved = 0;
+  bool patched = false;
+  for (int q = 0; q < nj;) {
+    const int j = c->h_fix_owner[q];
+    if (j >= Lr) break;
+    int e = q;
+    bool ok = true;
+    SampleOut add = {};
+    for (; e < nj && c->h_fix_owner[e] == j; e++) {
+      const RollRes& r = c->h_fix_res[e];
+      if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL || r.outcome < 0) ok = false;
+      add.rollouts++;
+      add.steps += r.nrows - 1;
+      add.f_col += r.outcome == CLRRT_ROLL_COLLISION;
+      add.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
+      add.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
+    }
+    if (!ok) { Lr = j; break; }
+    SampleOut& o = c->h_fix_so[j];
+    o.rollouts += add.rollouts; o.steps += add.steps; o.f_col += add.f_col; o.f_acc += add.f_acc; o.f_it += add.f_it;
+    patched = true;
+    resolved++;
+    q = e;
+  }
+  if (patched) HIPC(c, hipMemcpyAsync(c->so, c->h_fix_so.data(), sizeof(SampleOut) * Lr, hipMemcpyHostToDevice, st));
+  c->ex_stats[0]++;
+  c->ex_stats[1] += resolved;
+  c->ex_stats[2] += nj;
+  c->ex_stats[3] += Lr < n;
+  *L = std::max(1, Lr);
+  return CLRRT_OK;
+}
+
 // Stages 1-4 (+5 in EXACT mode) for n samples already in c->d_samples.  Returns the number of
 // samples to commit (n in BATCH mode).  have_lists: the candidate lists are already in c->cand
 // (pipelined rounds); during_roll runs right after the rollout kernel's launch.
@@ -1820,7 +1937,10 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     HIPC(c, launch_select(st, s));
   }
   int L = n;
-  if (exact && n > 1) {
+  if (exact && n > 1 && c->exact_fixup) {
+    int rc = exact_fixups(c, n, &L);
+    if (rc != CLRRT_OK) return rc;
+  } else if (exact && n > 1) {
     c->h_int[0] = n;
     HIPC(c, hipMemcpyAsync(c->first_conflict, c->h_int, sizeof(int), hipMemcpyHostToDevice, st));
     {

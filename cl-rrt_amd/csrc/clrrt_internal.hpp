@@ -132,6 +132,12 @@ struct RollArgs {
   int carry_cap;
   int jbase, sbase;
   unsigned long long* dbg;  // diagnostics (CLRRT_DEBUG_SYNC): per-wave heartbeat in host-mapped memory, or null
+  // SRC_LIST jobs whose parent is a node of the round being committed (Job::from_reg 1: xreg[parent], 2:
+  // xgb[parent]; EXACT fix-up rollouts), and the lanes that take jobs (job_stride 64: one job per wave, each at
+  // the lone lane's step latency; 0 or 1: every lane)
+  const clrrt_node* __restrict__ xreg;
+  const clrrt_node* __restrict__ xgb;
+  int job_stride;
 };
 
 // k_select over B "views": view v < nd is the still unresolved sample view[v] of an earlier round (deferred
@@ -267,6 +273,13 @@ hipError_t launch_replay_gather(hipStream_t st, const Job* jobs, const clrrt_nod
 hipError_t launch_select(hipStream_t st, const SelArgs& a);
 hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* recs, int n, const double* slots,
                             int slot_rows, int slot_jobs, double* arena);
+// EXACT fix-ups (k_conflict_fix): per sample j of the round, the nodes appended earlier in the round that enter
+// its candidate list before its result (fix_n[j] = their count m, fix_ids[j * FIX_MAX + i] = 2 k + (0 regular, 1
+// goal-biased) of sample k), or -1 when the conflict cannot be resolved by rolling them out (see the kernel)
+#define FIX_MAX 4
+hipError_t launch_conflict_fix(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
+                               const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
+                               const int* ncand, int* fix_n, int* fix_ids);
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                            const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
                            int* first);

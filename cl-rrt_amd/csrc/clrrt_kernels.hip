@@ -1178,9 +1178,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   extern __shared__ float4 lds[];
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int js = a.job_stride > 1 ? a.job_stride : 1;
+  const int j = gt / js;
   WorkCtr w{0, 0, 0};
-  bool act = j < a.njobs;
+  bool act = j < a.njobs && gt % js == 0;
   St10 ps;
   double pbx = 0, pby = 0, pvb = 0, sx = 0, sy = 0;
   int gb = 0;
@@ -1233,7 +1235,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       }
     } else {
       const Job& jb = a.jobs[j];
-      n = &a.tree[jb.parent];
+      n = jb.from_reg == 1 ? &a.xreg[jb.parent] : jb.from_reg == 2 ? &a.xgb[jb.parent] : &a.tree[jb.parent];
       gb = jb.gb; sx = jb.sx; sy = jb.sy;
       if (jb.row_off >= 0) rows = a.arena + (size_t)jb.row_off * 10;
     }
@@ -1287,7 +1289,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     if (threadIdx.x < 3 && s_ctr[threadIdx.x]) atomicAdd(&a.ctr[threadIdx.x], s_ctr[threadIdx.x]);
   }
 #ifdef CLRRT_ROLL_PROFILE
-  if (a.ctr && j < a.njobs)
+  if (a.ctr && j < a.njobs && gt % js == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.t[q]);
 #endif
 }
@@ -1898,6 +1900,52 @@ __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ 
     }
   }
   if (conflict) atomicMin(first_conflict, j);
+}
+
+// EXACT mode, fix-ups: a conflict of sample j with nodes appended earlier in the round does not always change
+// j's result.  The reference tries j's candidates in key order until the first success (rrtplanner.cpp:150-160):
+// a new node n that sorts before j's accepted candidate k is tried before it, and if n's rollout fails the result
+// is still k's (k stays inside the sortLimit window as long as k + m <= sortLimit - 1 for the m such nodes) with
+// n's rollout added to j's counters.  So the conflicting nodes are rolled out for j (the fix-up launch) and j
+// stands when all of them fail.  Not resolvable this way (fix_n = -1, j conflicts as before): a tie among j's
+// keys (std::sort's order of equal keys depends on the whole array), a new node whose key equals j's threshold
+// (its order against k is the sort's), more than FIX_MAX new nodes, k pushed out of the window, and samples
+// without a result whose full window (sortLimit candidates, all failed) would lose candidates the reference
+// then never simulates.
+__global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restrict__ S,
+                               const clrrt_node* __restrict__ regnodes, const clrrt_node* __restrict__ gbnodes,
+                               const SampleOut* __restrict__ so, const int* __restrict__ ctie,
+                               const int* __restrict__ ncand, int* __restrict__ fix_n, int* __restrict__ fix_ids) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  const double sx = S[j].x, sy = S[j].y;
+  const int ex = S[j].explore;
+  const float thr = so[j].thr;
+  const bool tie = ctie[j] != 0;
+  int m = 0;
+  bool bad = false;
+  for (int k = 0; k < j && !bad; k++) {
+    if (so[k].k < 0) continue;
+    if (tie) { bad = true; break; }
+    for (int w = 0; w < 2; w++) {
+      if (w == 1 && !so[k].gb_ok) break;
+      const clrrt_node& n = w == 0 ? regnodes[k] : gbnodes[k];
+      float c, s;
+      glibc::sincosf((float)(-n.state[2] - 0.0), s, c);  // dubinsDistance: cos/sin of one float -> sincosf
+      float key = dubins_key(sx, sy, n.state[0], n.state[1], c, s);
+      if (!ex) key = n.costE + key;
+      if (!(key > thr) && feasible_node(n.ref_back[0], n.ref_back[1], n.ang_par, sx, sy, p.feas_len)) {
+        if (key == thr || m == FIX_MAX) { bad = true; break; }
+        fix_ids[j * FIX_MAX + m] = 2 * k + w;
+        m++;
+      }
+    }
+  }
+  if (!bad && m > 0) {
+    const int kk = so[j].k, nc = ncand[j];
+    bad = kk >= 0 ? kk + m > p.sort_limit - 1 : nc + m > p.sort_limit;
+  }
+  fix_n[j] = bad ? -1 : m;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -2666,7 +2714,8 @@ template <int SRC>
 static hipError_t launch_roll_t(hipStream_t st, const RollArgs& a) {
   if (a.njobs <= 0) return hipSuccess;
   const size_t lds = roll_lds_bytes(a);
-  dim3 grid((a.njobs + 255) / 256), block(256);
+  const int64_t threads = (int64_t)a.njobs * (a.job_stride > 1 ? a.job_stride : 1);
+  dim3 grid((unsigned)((threads + 255) / 256)), block(256);
   if (a.p.need_gap)
     hipLaunchKernelGGL((k_rollout<SRC, true>), grid, block, 0, st, a);
   else
@@ -2774,6 +2823,16 @@ hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* r
                             int slot_rows, int slot_jobs, double* arena) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_copy_rows, dim3(n), dim3(256), 0, st, jobs, recs, slots, slot_rows, slot_jobs, arena);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_conflict_fix(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
+                               const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
+                               const int* ncand, int* fix_n, int* fix_ids) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_conflict_fix, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, ctie, ncand, fix_n,
+                     fix_ids);
   LAUNCH_CHECK();
   return hipSuccess;
 }

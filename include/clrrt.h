@@ -238,6 +238,10 @@ typedef struct clrrt_iteration {
   int32_t nodes;
   int32_t sim_count, fail_collision, fail_acclimit, fail_iterlimit, rollouts;
 } clrrt_iteration;
+/* EXACT rounds since the context was made: out[0] rounds with a conflict check, out[1] conflicts resolved by
+ * fix-up rollouts (option "exact_fixup"), out[2] fix-up rollouts run, out[3] rounds whose prefix ended at a
+ * conflict. */
+int clrrt_exact_stats(clrrt_ctx* ctx, int64_t out[4]);
 /* on != 0: start (or restart) logging, clearing the records; 0: stop and clear. */
 int clrrt_iteration_log(clrrt_ctx* ctx, int32_t on);
 /* Records logged so far (*n_total), and records [first, first + count) into out. */

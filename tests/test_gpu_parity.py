@@ -442,6 +442,42 @@ def test_exact_min_width_identical():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,seed,iters", [("obb200", 3, 400), ("moving", 4, 300), ("empty", 2, 300)])
+def test_exact_fixups_identical(kind, seed, iters):
+    """EXACT rounds with fix-ups (option exact_fixup, the default: a conflicting sample stands when the new nodes
+    that enter its list before its result all fail their rollouts for it) grow the tree of rounds without them
+    and of the oracle's sequential expandTree, node for node, rows and counters too -- and they resolve conflicts."""
+    mode, obs = _scene(kind)
+    o = Oracle(abi.default_params(collision_mode=mode), obs)
+    Oracle.srand(seed)
+    o.init_tree()
+    o.expand(iters)
+    trees = []
+    for fix in (1, 0):
+        pl = clrrt.Planner(clrrt.default_params(collision_mode=mode), max_nodes=1 << 16, max_rows=1 << 22,
+                           max_batch=256)
+        pl.set_option("exact_fixup", fix)
+        if obs is not None:
+            pl.set_obstacles(obs)
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(seed), n_iters=iters, mode=clrrt.CLRRT_MODE_EXACT, batch=256)
+        assert st["iterations"] == iters
+        n, nr = pl.size()
+        trees.append((bytes(pl.nodes_raw()), pl.rows(0, nr).tobytes(), pl.counters(), st["rounds"], pl.exact_stats()))
+        if fix:
+            on, gn, bad = _compare_trees(o, pl, f"exact fix-ups {kind} seed {seed}")
+            assert bad is None and len(on["parent"]) == len(gn["parent"])
+            oc = o.counters()
+            for k in ("sim_count", "fail_collision", "fail_acclimit", "fail_iterlimit", "rollouts"):
+                assert oc[k] == trees[-1][2][k], (k, oc[k], trees[-1][2][k])
+        pl.close()
+    print(f"{kind}: rounds with fix-ups {trees[0][3]} vs {trees[1][3]} without; stats {trees[0][4]}")
+    assert trees[0][0] == trees[1][0] and trees[0][1] == trees[1][1] and trees[0][2] == trees[1][2]
+    if kind != "empty":
+        assert trees[0][4]["resolved"] > 0 and trees[0][3] < trees[1][3]
+
+
+@pytest.mark.gpu
 def test_deferred_batch_rounds_identical():
     """Full-size property of the deferred-sample rounds (defer_steps 128, as bench.py runs cfg3): the pipelines (none, lag 1, lag 2) and
     the scheduling options (grid width, queue order, per-lane collision checks) grow exactly the same tree --
