@@ -460,9 +460,10 @@ class Planner:
         self._chk(self.L.clrrt_tree_truncate(self.h, int(n)), "tree_truncate")
 
     def exact_stats(self):
-        out = (C.c_int64 * 4)()
+        out = (C.c_int64 * 10)()
         self._chk(self.L.clrrt_exact_stats(self.h, out), "exact_stats")
-        return {"rounds": out[0], "resolved": out[1], "fixup_rollouts": out[2], "conflict_rounds": out[3]}
+        return dict(zip(("rounds", "resolved", "fixup_rollouts", "conflict_rounds", "end_fixup_succeeded", "end_tie",
+                         "end_key_eq_thr", "end_over_slots", "end_pushed_out", "end_full_window"), list(out)))
 
     def iteration_log(self, on=True):
         self._chk(self.L.clrrt_iteration_log(self.h, 1 if on else 0), "iteration_log")

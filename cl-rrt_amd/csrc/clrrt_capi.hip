@@ -156,7 +156,10 @@ struct clrrt_ctx {
   std::vector<int> h_fix_owner;
   std::vector<RollRes> h_fix_res;
   std::vector<SampleOut> h_fix_so;
-  int64_t ex_stats[4] = {0, 0, 0, 0};  // EXACT: rounds, conflicts resolved, fix-up rollouts, conflicts left
+  // EXACT: rounds, conflicts resolved, fix-up rollouts, rounds ended by a conflict; then why the ending conflicts
+  // were not resolved: a fix-up succeeded, tie, key equal to the threshold, > FIX_MAX nodes, k pushed out, full
+  // window without a result
+  int64_t ex_stats[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int* roll_perm = nullptr;   // [max_batch * CAND_K] queue order
   int* roll_pflag = nullptr;  // [2 max_batch * CAND_K + scratch] flags, scan positions, scan scratch
   // extractBestPath scratch (allocated on first use, max_nodes entries each)
@@ -949,9 +952,9 @@ int clrrt_tree_truncate(clrrt_ctx* c, int64_t n) {
   return CLRRT_OK;  // (the tree's box stays a superset: a valid search frame)
 }
 
-int clrrt_exact_stats(clrrt_ctx* c, int64_t out[4]) {
+int clrrt_exact_stats(clrrt_ctx* c, int64_t out[10]) {
   if (!c || !out) return CLRRT_EINVAL;
-  for (int i = 0; i < 4; i++) out[i] = c->ex_stats[i];
+  for (int i = 0; i < 10; i++) out[i] = c->ex_stats[i];
   return CLRRT_OK;
 }
 
@@ -1711,7 +1714,11 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
   c->h_fix_jobs.clear();
   c->h_fix_owner.clear();
   for (int j = 0; j < n; j++) {
-    if (fn[j] < 0) { stop = j; break; }
+    if (fn[j] < 0) {
+      stop = j;
+      if (-fn[j] >= 1 && -fn[j] <= 5) c->ex_stats[4 + -fn[j]]++;
+      break;
+    }
     for (int i = 0; i < fn[j]; i++) {
       Job jb;
       const int id = fid[j * FIX_MAX + i];
@@ -1763,7 +1770,11 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
       add.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
       add.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
     }
-    if (!ok) { Lr = j; break; }
+    if (!ok) {
+      Lr = j;
+      c->ex_stats[4]++;
+      break;
+    }
     SampleOut& o = c->h_fix_so[j];
     o.rollouts += add.rollouts; o.steps += add.steps; o.f_col += add.f_col; o.f_acc += add.f_acc; o.f_it += add.f_it;
     patched = true;

@@ -1923,10 +1923,10 @@ __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restric
   const float thr = so[j].thr;
   const bool tie = ctie[j] != 0;
   int m = 0;
-  bool bad = false;
+  int bad = 0;  // why not resolvable: 1 tie, 2 a key equal to the threshold, 3 > FIX_MAX, 4 k pushed out, 5 full window
   for (int k = 0; k < j && !bad; k++) {
     if (so[k].k < 0) continue;
-    if (tie) { bad = true; break; }
+    if (tie) { bad = 1; break; }
     for (int w = 0; w < 2; w++) {
       if (w == 1 && !so[k].gb_ok) break;
       const clrrt_node& n = w == 0 ? regnodes[k] : gbnodes[k];
@@ -1935,7 +1935,7 @@ __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restric
       float key = dubins_key(sx, sy, n.state[0], n.state[1], c, s);
       if (!ex) key = n.costE + key;
       if (!(key > thr) && feasible_node(n.ref_back[0], n.ref_back[1], n.ang_par, sx, sy, p.feas_len)) {
-        if (key == thr || m == FIX_MAX) { bad = true; break; }
+        if (key == thr || m == FIX_MAX) { bad = key == thr ? 2 : 3; break; }
         fix_ids[j * FIX_MAX + m] = 2 * k + w;
         m++;
       }
@@ -1943,9 +1943,9 @@ __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restric
   }
   if (!bad && m > 0) {
     const int kk = so[j].k, nc = ncand[j];
-    bad = kk >= 0 ? kk + m > p.sort_limit - 1 : nc + m > p.sort_limit;
+    if (kk >= 0 ? kk + m > p.sort_limit - 1 : nc + m > p.sort_limit) bad = kk >= 0 ? 4 : 5;
   }
-  fix_n[j] = bad ? -1 : m;
+  fix_n[j] = bad ? -bad : m;
 }
 
 // --------------------------------------------------------------------------------------------

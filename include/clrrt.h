@@ -240,8 +240,10 @@ typedef struct clrrt_iteration {
 } clrrt_iteration;
 /* EXACT rounds since the context was made: out[0] rounds with a conflict check, out[1] conflicts resolved by
  * fix-up rollouts (option "exact_fixup"), out[2] fix-up rollouts run, out[3] rounds whose prefix ended at a
- * conflict. */
-int clrrt_exact_stats(clrrt_ctx* ctx, int64_t out[4]);
+ * conflict; why those conflicts were not resolved: out[4] a fix-up rollout succeeded, out[5] a key tie in the
+ * sample's list, out[6] a new key equal to the sample's threshold, out[7] more new nodes than fix-up slots,
+ * out[8] the accepted candidate pushed out of the sortLimit window, out[9] a full window without a result. */
+int clrrt_exact_stats(clrrt_ctx* ctx, int64_t out[10]);
 /* on != 0: start (or restart) logging, clearing the records; 0: stop and clear. */
 int clrrt_iteration_log(clrrt_ctx* ctx, int32_t on);
 /* Records logged so far (*n_total), and records [first, first + count) into out. */
