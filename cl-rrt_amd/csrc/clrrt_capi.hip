@@ -148,6 +148,7 @@ struct clrrt_ctx {
   int exact_fixup = 1;
   int* fix_n = nullptr;        // [max_batch]
   int* fix_ids = nullptr;      // [max_batch * FIX_MAX]
+  int* fix_adj = nullptr;      // [max_batch * 5]
   Job* fix_jobs = nullptr;     // [max_batch * FIX_MAX]
   RollRes* fix_res = nullptr;  // [max_batch * FIX_MAX]
   std::vector<int> h_fix;      // fix_n then fix_ids
@@ -555,7 +556,7 @@ static void free_all(clrrt_ctx* c) {
                   c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun, c->nnw.wctr, c->nnw_alt.wctr, c->nnw3.wctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
-  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal, c->fix_n, c->fix_ids, c->fix_jobs, c->fix_res};
+  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal, c->fix_n, c->fix_ids, c->fix_jobs, c->fix_res, c->fix_adj};
   for (void* p : sptrs)
     if (p) hipFree(p);
   void* dptrs[] = {c->def.res, c->def.res_gb, c->def.cand, c->def.ncand, c->def.samp, c->def.best, c->def.dlist[0],
@@ -1697,19 +1698,23 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     HIPC(c, dalloc(&c->fix_ids, B * FIX_MAX));
     HIPC(c, dalloc(&c->fix_jobs, B * FIX_MAX));
     HIPC(c, dalloc(&c->fix_res, B * FIX_MAX));
+    HIPC(c, dalloc(&c->fix_adj, B * 5));
   }
-  HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->fix_n,
-                              c->fix_ids));
-  c->h_fix.resize((size_t)n * (1 + FIX_MAX));
+  HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->ckey,
+                              c->res_spec, c->fix_n, c->fix_ids, c->fix_adj));
+  c->h_fix.resize((size_t)n * (1 + FIX_MAX + 5));
   c->h_fix_smp.resize(n);
   c->h_fix_so.resize(n);
   HIPC(c, hipMemcpyAsync(c->h_fix.data(), c->fix_n, sizeof(int) * n, hipMemcpyDeviceToHost, st));
   HIPC(c, hipMemcpyAsync(c->h_fix.data() + n, c->fix_ids, sizeof(int) * n * FIX_MAX, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix.data() + n * (1 + FIX_MAX), c->fix_adj, sizeof(int) * n * 5, hipMemcpyDeviceToHost,
+                         st));
   HIPC(c, hipMemcpyAsync(c->h_fix_smp.data(), c->d_samples, sizeof(clrrt_sample) * n, hipMemcpyDeviceToHost, st));
   HIPC(c, hipMemcpyAsync(c->h_fix_so.data(), c->so, sizeof(SampleOut) * n, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
   const int* fn = c->h_fix.data();
   const int* fid = c->h_fix.data() + n;
+  const int* fadj = c->h_fix.data() + n * (1 + FIX_MAX);
   int stop = n;
   c->h_fix_jobs.clear();
   c->h_fix_owner.clear();
@@ -1777,6 +1782,8 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     }
     SampleOut& o = c->h_fix_so[j];
     o.rollouts += add.rollouts; o.steps += add.steps; o.f_col += add.f_col; o.f_acc += add.f_acc; o.f_it += add.f_it;
+    const int* ad = fadj + 5 * j;  // old candidates pushed out of the window (samples without a result)
+    o.rollouts += ad[0]; o.steps += ad[1]; o.f_col += ad[2]; o.f_acc += ad[3]; o.f_it += ad[4];
     patched = true;
     resolved++;
     q = e;

@@ -277,9 +277,12 @@ hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* r
 // its candidate list before its result (fix_n[j] = their count m, fix_ids[j * FIX_MAX + i] = 2 k + (0 regular, 1
 // goal-biased) of sample k), or -1 when the conflict cannot be resolved by rolling them out (see the kernel)
 #define FIX_MAX 4
+// fix_adj[j * 5 ..]: counters (rollouts, steps, collisions, acceleration limits, iteration limits) to add for old
+// candidates of a sample without a result that the grown window pushes out (<= 0)
 hipError_t launch_conflict_fix(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                                const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
-                               const int* ncand, int* fix_n, int* fix_ids);
+                               const int* ncand, const float* ckey, const RollRes* res, int* fix_n, int* fix_ids,
+                               int* fix_adj);
 hipError_t launch_conflict(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                            const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
                            int* first);

@@ -1915,14 +1915,26 @@ __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ 
 __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restrict__ S,
                                const clrrt_node* __restrict__ regnodes, const clrrt_node* __restrict__ gbnodes,
                                const SampleOut* __restrict__ so, const int* __restrict__ ctie,
-                               const int* __restrict__ ncand, int* __restrict__ fix_n, int* __restrict__ fix_ids) {
+                               const int* __restrict__ ncand, const float* __restrict__ ckey,
+                               const RollRes* __restrict__ res, int* __restrict__ fix_n, int* __restrict__ fix_ids,
+                               int* __restrict__ fix_adj) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B) return;
   const double sx = S[j].x, sy = S[j].y;
   const int ex = S[j].explore;
   const float thr = so[j].thr;
-  const bool tie = ctie[j] != 0;
+  const int kk = so[j].k, nc = ncand[j], lim = p.sort_limit;
+  const int g0 = so[j].g * CAND_K;
+  // Equal keys in j's list leave their order to std::sort, which the new nodes can change.  With a result k whose
+  // key is unique in the list (and k not the window's last entry, whose successor is not kept), every
+  // reordering keeps the set of candidates tried before k (all keys below k's: all failed) and k itself, so the
+  // result stands; otherwise a tie ends the prefix at any appended node, as before.
+  const bool tie = ctie[j] != 0 &&
+                   !(kk >= 0 && kk < lim - 1 && (kk == 0 || ckey[g0 + kk - 1] != ckey[g0 + kk]) &&
+                     (kk + 1 >= nc || ckey[g0 + kk + 1] != ckey[g0 + kk]));
   int m = 0;
+  int ids[FIX_MAX];
+  float nk[FIX_MAX];
   int bad = 0;  // why not resolvable: 1 tie, 2 a key equal to the threshold, 3 > FIX_MAX, 4 k pushed out, 5 full window
   for (int k = 0; k < j && !bad; k++) {
     if (so[k].k < 0) continue;
@@ -1936,16 +1948,55 @@ __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restric
       if (!ex) key = n.costE + key;
       if (!(key > thr) && feasible_node(n.ref_back[0], n.ref_back[1], n.ang_par, sx, sy, p.feas_len)) {
         if (key == thr || m == FIX_MAX) { bad = key == thr ? 2 : 3; break; }
-        fix_ids[j * FIX_MAX + m] = 2 * k + w;
+        ids[m] = 2 * k + w;
+        nk[m] = key;
         m++;
       }
     }
   }
+  int adj[5] = {0, 0, 0, 0, 0};  // counters of old candidates the grown window no longer reaches (subtracted)
+  int mw = m;                     // new nodes inside the window
   if (!bad && m > 0) {
-    const int kk = so[j].k, nc = ncand[j];
-    if (kk >= 0 ? kk + m > p.sort_limit - 1 : nc + m > p.sort_limit) bad = kk >= 0 ? 4 : 5;
+    if (kk >= 0) {
+      // every new node precedes the accepted candidate (key < thr): all are tried, k moves to k + m
+      if (kk + m > lim - 1) bad = 4;
+    } else {
+      // no result: the reference tries the first sortLimit of (old candidates + new nodes) by key.  Equal keys
+      // would leave that order to std::sort: not resolvable.
+      for (int a = 0; a < m && !bad; a++) {
+        for (int b = a + 1; b < m; b++)
+          if (nk[a] == nk[b]) bad = 1;
+        for (int o = 0; o < nc; o++)
+          if (nk[a] == ckey[g0 + o]) bad = 1;
+      }
+      if (!bad) {
+        mw = 0;
+        for (int a = 0; a < m; a++) {  // rank among old and new
+          int r = 0;
+          for (int o = 0; o < nc; o++) r += ckey[g0 + o] < nk[a];
+          for (int b = 0; b < m; b++) r += nk[b] < nk[a];
+          if (r < lim) ids[mw++] = ids[a];
+        }
+        for (int o = 0; o < nc; o++) {
+          int r = o;
+          for (int b = 0; b < m; b++) r += nk[b] < ckey[g0 + o];
+          if (r >= lim) {  // pushed out: its rollout (a failure, run speculatively) is not the reference's
+            const RollRes& q = res[g0 + o];
+            if (q.outcome < 0) continue;
+            adj[0] -= 1;
+            adj[1] -= q.nrows - 1;
+            adj[2] -= q.outcome == CLRRT_ROLL_COLLISION;
+            adj[3] -= q.outcome == CLRRT_ROLL_ACCLIMIT;
+            adj[4] -= q.outcome == CLRRT_ROLL_ITERLIMIT;
+          }
+        }
+      }
+    }
   }
-  fix_n[j] = bad ? -bad : m;
+  for (int a = 0; a < (bad ? 0 : mw); a++) fix_ids[j * FIX_MAX + a] = ids[a];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fix_adj[j * 5 + q] = adj[q];
+  fix_n[j] = bad ? -bad : mw;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -2829,10 +2880,11 @@ hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* r
 
 hipError_t launch_conflict_fix(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,
                                const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, const int* ctie,
-                               const int* ncand, int* fix_n, int* fix_ids) {
+                               const int* ncand, const float* ckey, const RollRes* res, int* fix_n, int* fix_ids,
+                               int* fix_adj) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_conflict_fix, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, ctie, ncand, fix_n,
-                     fix_ids);
+  hipLaunchKernelGGL(k_conflict_fix, dim3((B + 63) / 64), dim3(64), 0, st, p, B, S, reg, gbn, so, ctie, ncand, ckey,
+                     res, fix_n, fix_ids, fix_adj);
   LAUNCH_CHECK();
   return hipSuccess;
 }
