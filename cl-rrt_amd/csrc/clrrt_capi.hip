@@ -149,8 +149,15 @@ struct clrrt_ctx {
   int* fix_n = nullptr;        // [max_batch]
   int* fix_ids = nullptr;      // [max_batch * FIX_MAX]
   int* fix_adj = nullptr;      // [max_batch * 5]
-  Job* fix_jobs = nullptr;     // [max_batch * FIX_MAX]
-  RollRes* fix_res = nullptr;  // [max_batch * FIX_MAX]
+  NnRec* fix_xrec = nullptr;   // [2 max_batch] the round's new nodes as nearest-node records
+  int* fix_xi = nullptr;       // [2 max_batch] samples whose list is recomputed, their new-node counts
+  int* fix_xcand = nullptr;    // [max_batch * K] recomputed lists
+  float* fix_xkey = nullptr;   // [max_batch * K]
+  int* fix_xn = nullptr;       // [2 max_batch] list lengths, tie flags
+  std::vector<int> h_fix_cand;
+  std::vector<RollRes> h_fix_spec;
+  Job* fix_jobs = nullptr;     // [max_batch * CAND_K]
+  RollRes* fix_res = nullptr;  // [max_batch * CAND_K]
   std::vector<int> h_fix;      // fix_n then fix_ids
   std::vector<clrrt_sample> h_fix_smp;
   std::vector<Job> h_fix_jobs;
@@ -556,7 +563,8 @@ static void free_all(clrrt_ctx* c) {
                   c->nnw.trun, c->nnw_alt.trun, c->nnw3.trun, c->nnw.wctr, c->nnw_alt.wctr, c->nnw3.wctr};
   for (void* p : ptrs)
     if (p) hipFree(p);
-  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal, c->fix_n, c->fix_ids, c->fix_jobs, c->fix_res, c->fix_adj};
+  void* sptrs[] = {c->sh.xbuf, c->sh.xkey, c->sh.xtmp, c->sh.d_goal, c->fix_n, c->fix_ids, c->fix_jobs, c->fix_res, c->fix_adj,
+                   c->fix_xrec, c->fix_xi, c->fix_xcand, c->fix_xkey, c->fix_xn};
   for (void* p : sptrs)
     if (p) hipFree(p);
   void* dptrs[] = {c->def.res, c->def.res_gb, c->def.cand, c->def.ncand, c->def.samp, c->def.best, c->def.dlist[0],
@@ -1688,54 +1696,161 @@ static int run_nn(clrrt_ctx* c, int n, KeyId* scratch) {
 }
 
 // EXACT mode, stage 5 with fix-ups (k_conflict_fix): the committed prefix of the round's n samples runs up to the
-// first sample whose conflict is not resolvable or whose fix-up rollouts (the conflicting new nodes rolled out
-// for it, one job per wave) are not all failures; the resolved samples' counters take the fix-ups.  *L: the prefix.
+// first sample whose result the reference would not reproduce.  A sample k_conflict_fix resolves takes the fix-up
+// rollouts of the new nodes that enter its list before its result; a sample it cannot resolve (ties, thresholds,
+// window changes) gets its list recomputed over the tree the reference's sort sees for it -- the N tree nodes and
+// the round's new nodes before it, std::sort's tie order included (launch_nn_exact_x) -- and the candidates that
+// list tries before its result which the speculative evaluation did not try (new nodes, or old ones it ordered
+// after its result) become fix-ups too.  The fix-ups run in one launch (one job per wave); a sample stands when all
+// of its fix-ups fail and its result is still the first success of its list; its counters become those of the
+// list's tried candidates.  *L: the prefix.
 static int exact_fixups(clrrt_ctx* c, int n, int* L) {
   hipStream_t st = c->stream;
   const int64_t B = c->cap.max_batch;
+  const int K = CAND_K;
   if (!c->fix_n) {
     HIPC(c, dalloc(&c->fix_n, B));
     HIPC(c, dalloc(&c->fix_ids, B * FIX_MAX));
-    HIPC(c, dalloc(&c->fix_jobs, B * FIX_MAX));
-    HIPC(c, dalloc(&c->fix_res, B * FIX_MAX));
     HIPC(c, dalloc(&c->fix_adj, B * 5));
+    HIPC(c, dalloc(&c->fix_jobs, B * K));
+    HIPC(c, dalloc(&c->fix_res, B * K));
+    HIPC(c, dalloc(&c->fix_xrec, 2 * B));
+    HIPC(c, dalloc(&c->fix_xi, 2 * B));
+    HIPC(c, dalloc(&c->fix_xcand, B * K));
+    HIPC(c, dalloc(&c->fix_xkey, B * K));
+    HIPC(c, dalloc(&c->fix_xn, 2 * B));
   }
   HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->ckey,
                               c->res_spec, c->fix_n, c->fix_ids, c->fix_adj));
   c->h_fix.resize((size_t)n * (1 + FIX_MAX + 5));
   c->h_fix_smp.resize(n);
   c->h_fix_so.resize(n);
+  c->h_fix_cand.resize((size_t)n * K);
+  c->h_fix_spec.resize((size_t)n * K);
   HIPC(c, hipMemcpyAsync(c->h_fix.data(), c->fix_n, sizeof(int) * n, hipMemcpyDeviceToHost, st));
   HIPC(c, hipMemcpyAsync(c->h_fix.data() + n, c->fix_ids, sizeof(int) * n * FIX_MAX, hipMemcpyDeviceToHost, st));
   HIPC(c, hipMemcpyAsync(c->h_fix.data() + n * (1 + FIX_MAX), c->fix_adj, sizeof(int) * n * 5, hipMemcpyDeviceToHost,
                          st));
   HIPC(c, hipMemcpyAsync(c->h_fix_smp.data(), c->d_samples, sizeof(clrrt_sample) * n, hipMemcpyDeviceToHost, st));
   HIPC(c, hipMemcpyAsync(c->h_fix_so.data(), c->so, sizeof(SampleOut) * n, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix_cand.data(), c->cand, sizeof(int) * n * K, hipMemcpyDeviceToHost, st));
+  HIPC(c, hipMemcpyAsync(c->h_fix_spec.data(), c->res_spec, sizeof(RollRes) * n * K, hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
   const int* fn = c->h_fix.data();
   const int* fid = c->h_fix.data() + n;
   const int* fadj = c->h_fix.data() + n * (1 + FIX_MAX);
+  const int64_t N = c->n_nodes;
+  // the round's new nodes in commit order: count before each sample, and (sample, 0 regular | 1 goal-biased) by position
+  std::vector<int> xpre(n + 1, 0);
+  std::vector<int> xpos;
+  for (int k = 0; k < n; k++) {
+    const SampleOut& o = c->h_fix_so[k];
+    xpre[k + 1] = xpre[k];
+    if (o.k >= 0) {
+      xpos.push_back(2 * k);
+      xpre[k + 1]++;
+      if (o.gb_ok) { xpos.push_back(2 * k + 1); xpre[k + 1]++; }
+    }
+  }
+  // the samples that need their list recomputed (and whether that fits the LDS kernel)
+  const bool x_fits = N + xpre[n] <= nn_exact_small_max() && c->dp.sort_limit <= K;
   int stop = n;
+  std::vector<int> xl;
+  for (int j = 0; j < n; j++) {
+    if (fn[j] >= 0) continue;
+    if (!x_fits) { stop = j; if (-fn[j] >= 1 && -fn[j] <= 5) c->ex_stats[4 + -fn[j]]++; break; }
+    xl.push_back(j);
+  }
+  const int nl = (int)xl.size();
+  std::vector<int> xc, xn;
+  if (nl > 0) {
+    std::vector<int> xs(2 * nl);
+    for (int i = 0; i < nl; i++) { xs[i] = xl[i]; xs[nl + i] = xpre[xl[i]]; }
+    HIPC(c, hipMemcpyAsync(c->fix_xi, xs.data(), sizeof(int) * 2 * nl, hipMemcpyHostToDevice, st));
+    HIPC(c, launch_nn_exact_x(st, c->d_samples, c->nn, (int)N, c->dp, c->regnodes, c->gbnodes, c->so, n, c->fix_xrec,
+                              c->fix_xi, c->fix_xi + nl, nl, xpre[n], c->fix_xcand, c->fix_xkey, c->fix_xn,
+                              c->fix_xn + nl));
+    xc.resize((size_t)nl * K);
+    xn.resize(nl);
+    HIPC(c, hipMemcpyAsync(xc.data(), c->fix_xcand, sizeof(int) * nl * K, hipMemcpyDeviceToHost, st));
+    HIPC(c, hipMemcpyAsync(xn.data(), c->fix_xn, sizeof(int) * nl, hipMemcpyDeviceToHost, st));
+    HIPC(c, hipStreamSynchronize(st));
+  }
+  auto is_fail = [](int oc) { return oc >= 0 && oc != CLRRT_ROLL_END && oc != CLRRT_ROLL_GOAL; };
+  auto add_res = [](SampleOut& d, const RollRes& r, int sign) {
+    d.rollouts += sign;
+    d.steps += sign * (r.nrows - 1);
+    d.f_col += sign * (r.outcome == CLRRT_ROLL_COLLISION);
+    d.f_acc += sign * (r.outcome == CLRRT_ROLL_ACCLIMIT);
+    d.f_it += sign * (r.outcome == CLRRT_ROLL_ITERLIMIT);
+  };
+  // per sample: the fix-up jobs and the counters' change apart from them
   c->h_fix_jobs.clear();
   c->h_fix_owner.clear();
-  for (int j = 0; j < n; j++) {
-    if (fn[j] < 0) {
-      stop = j;
-      if (-fn[j] >= 1 && -fn[j] <= 5) c->ex_stats[4 + -fn[j]]++;
-      break;
+  std::vector<SampleOut> delta(n);
+  auto job = [&](int j, int from, int parent) {
+    Job jb;
+    jb.parent = parent;
+    jb.from_reg = from;
+    jb.gb = 0;
+    jb.pad = 0;
+    jb.sx = c->h_fix_smp[j].x;
+    jb.sy = c->h_fix_smp[j].y;
+    jb.row_off = -1;
+    c->h_fix_jobs.push_back(jb);
+    c->h_fix_owner.push_back(j);
+  };
+  for (int j = 0, xi = 0; j < stop; j++) {
+    SampleOut& d = delta[j];
+    d = SampleOut{};
+    if (fn[j] >= 0) {
+      for (int i = 0; i < fn[j]; i++) {
+        const int id = fid[j * FIX_MAX + i];
+        job(j, 1 + (id & 1), id >> 1);
+      }
+      const int* ad = fadj + 5 * j;  // old candidates pushed out of the window (samples without a result)
+      d.rollouts += ad[0]; d.steps += ad[1]; d.f_col += ad[2]; d.f_acc += ad[3]; d.f_it += ad[4];
+      continue;
     }
-    for (int i = 0; i < fn[j]; i++) {
-      Job jb;
-      const int id = fid[j * FIX_MAX + i];
-      jb.parent = id >> 1;
-      jb.from_reg = 1 + (id & 1);
-      jb.gb = 0;
-      jb.pad = 0;
-      jb.sx = c->h_fix_smp[j].x;
-      jb.sy = c->h_fix_smp[j].y;
-      jb.row_off = -1;
-      c->h_fix_jobs.push_back(jb);
-      c->h_fix_owner.push_back(j);
+    // the recomputed list
+    const SampleOut& o = c->h_fix_so[j];
+    const int* lst = xc.data() + (size_t)xi * K;
+    const int ln = xn[xi];
+    xi++;
+    const int* spec = c->h_fix_cand.data() + (size_t)j * K;
+    const RollRes* sres = c->h_fix_spec.data() + (size_t)j * K;
+    const int acc = o.k >= 0 ? spec[o.k] : -1;
+    // the speculative counters of the candidates tried before the result (all of them without one) come out ...
+    for (int q = 0; q < K; q++) {
+      if (spec[q] < 0 || (o.k >= 0 && q >= o.k)) break;
+      add_res(d, sres[q], -1);
+    }
+    // ... and those of the recomputed list's candidates before the result go in (known failures, or fix-ups)
+    bool found = false;
+    for (int t = 0; t < ln; t++) {
+      const int e = lst[t];
+      if (e == acc) { found = true; break; }
+      int q = -1;
+      if (e < N)
+        for (int r = 0; r < K && spec[r] >= 0; r++)
+          if (spec[r] == e) { q = r; break; }
+      if (q >= 0 && (o.k < 0 || q < o.k) && is_fail(sres[q].outcome)) {
+        add_res(d, sres[q], +1);
+      } else if (e < N) {
+        job(j, 0, e);
+      } else {
+        const int pw = xpos[e - N];
+        job(j, 1 + (pw & 1), pw >> 1);
+      }
+    }
+    if (o.k >= 0 && !found) {  // the result is not its list's first success any more
+      stop = j;
+      c->ex_stats[8]++;
+      while (!c->h_fix_owner.empty() && c->h_fix_owner.back() == j) {
+        c->h_fix_owner.pop_back();
+        c->h_fix_jobs.pop_back();
+      }
+      break;
     }
   }
   const int nj = (int)c->h_fix_jobs.size();
@@ -1756,37 +1871,27 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     HIPC(c, hipMemcpyAsync(c->h_fix_res.data(), c->fix_res, sizeof(RollRes) * nj, hipMemcpyDeviceToHost, st));
     HIPC(c, hipStreamSynchronize(st));
   }
-  // in sample order: a fix-up that succeeds changes the sample's result (it ends the prefix); all failed: the
-  // sample stands, with the reference's counters for the extra rollouts
+  // in sample order: a fix-up that succeeds changes the sample's result (it ends the prefix)
   int Lr = stop, resolved = 0;
   bool patched = false;
-  for (int q = 0; q < nj;) {
-    const int j = c->h_fix_owner[q];
-    if (j >= Lr) break;
-    int e = q;
-    bool ok = true;
-    SampleOut add = {};
-    for (; e < nj && c->h_fix_owner[e] == j; e++) {
-      const RollRes& r = c->h_fix_res[e];
-      if (r.outcome == CLRRT_ROLL_END || r.outcome == CLRRT_ROLL_GOAL || r.outcome < 0) ok = false;
-      add.rollouts++;
-      add.steps += r.nrows - 1;
-      add.f_col += r.outcome == CLRRT_ROLL_COLLISION;
-      add.f_acc += r.outcome == CLRRT_ROLL_ACCLIMIT;
-      add.f_it += r.outcome == CLRRT_ROLL_ITERLIMIT;
+  for (int j = 0, q = 0; j < stop; j++) {
+    SampleOut add = delta[j];
+    bool ok = true, any = fn[j] != 0;
+    for (; q < nj && c->h_fix_owner[q] == j; q++) {
+      const RollRes& r = c->h_fix_res[q];
+      if (!is_fail(r.outcome)) ok = false;
+      add_res(add, r, +1);
     }
     if (!ok) {
       Lr = j;
       c->ex_stats[4]++;
       break;
     }
+    if (!any) continue;
     SampleOut& o = c->h_fix_so[j];
     o.rollouts += add.rollouts; o.steps += add.steps; o.f_col += add.f_col; o.f_acc += add.f_acc; o.f_it += add.f_it;
-    const int* ad = fadj + 5 * j;  // old candidates pushed out of the window (samples without a result)
-    o.rollouts += ad[0]; o.steps += ad[1]; o.f_col += ad[2]; o.f_acc += ad[3]; o.f_it += ad[4];
     patched = true;
     resolved++;
-    q = e;
   }
   if (patched) HIPC(c, hipMemcpyAsync(c->so, c->h_fix_so.data(), sizeof(SampleOut) * Lr, hipMemcpyHostToDevice, st));
   c->ex_stats[0]++;

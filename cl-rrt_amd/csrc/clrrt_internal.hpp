@@ -277,6 +277,13 @@ hipError_t launch_copy_rows(hipStream_t st, const Job* jobs, const clrrt_node* r
 // its candidate list before its result (fix_n[j] = their count m, fix_ids[j * FIX_MAX + i] = 2 k + (0 regular, 1
 // goal-biased) of sample k), or -1 when the conflict cannot be resolved by rolling them out (see the kernel)
 #define FIX_MAX 4
+// EXACT fix-ups of the samples k_conflict_fix could not resolve: their lists over the tree they will see (the N
+// tree nodes + the round's new nodes before them, xcnt[i] for sample slist[i]), one wave each (k_nn_exact_fused
+// with std::sort's tie order), into rows 0 .. nlist of cand / ckey / ncand / ctie; xrec: [2 n] scratch
+hipError_t launch_nn_exact_x(hipStream_t st, const clrrt_sample* S, const NnRec* nodes, int N, const DevParams& p,
+                             const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, int n, NnRec* xrec,
+                             const int* slist, const int* xcnt, int nlist, int xmax, int* cand, float* ckey,
+                             int* ncand, int* ctie);
 // fix_adj[j * 5 ..]: counters (rollouts, steps, collisions, acceleration limits, iteration limits) to add for old
 // candidates of a sample without a result that the grown window pushes out (<= 0)
 hipError_t launch_conflict_fix(hipStream_t st, const DevParams& p, int B, const clrrt_sample* S,

@@ -559,14 +559,27 @@ __global__ void __launch_bounds__(64) k_nn_exact_lds(const clrrt_sample* __restr
 // flag; a tied sample replays std::sort on the LDS array (only the positions up to the last key <= the
 // list's `sort_limit`-th key are needed) and walks the sorted order for the first `sort_limit` feasible
 // entries (rrtplanner.cpp:227-268), exactly as k_nn_exact_lds does after the brute force.
+// xrec / xcnt / slist (EXACT fix-ups, k_conflict_fix): block b searches sample slist[b] over the tree's N nodes
+// followed by the first xcnt[b] records of xrec (the nodes the round appends before that sample, as they will
+// stand in the tree: ids N, N + 1, ...) and writes its list at row b; Nlds = the LDS entries allotted per block.
 __global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __restrict__ S, int B,
-                                                       const NnRec* __restrict__ nodes, int N, DevParams p,
+                                                       const NnRec* __restrict__ nodes, int N0, DevParams p,
                                                        int* __restrict__ cand, float* __restrict__ ckey,
-                                                       int* __restrict__ ncand, int* __restrict__ ctie) {
+                                                       int* __restrict__ ncand, int* __restrict__ ctie,
+                                                       const NnRec* __restrict__ xrec = nullptr,
+                                                       const int* __restrict__ xcnt = nullptr,
+                                                       const int* __restrict__ slist = nullptr, int Nlds = 0) {
   extern __shared__ KeyId s_kv[];
-  int2* s_pairs = (int2*)(s_kv + N);  // [N / 2 + 64]
-  const int s = blockIdx.x;
-  if (s >= B) return;
+  int2* s_pairs = (int2*)(s_kv + (slist ? Nlds : N0));  // [N / 2 + 64]
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int s = slist ? slist[b] : b;  // the sample
+  const int ob = slist ? b : s;        // its output row
+  const int N = N0 + (xcnt ? xcnt[b] : 0);
+  cand += (ob - s) * CAND_K;
+  ckey += (ob - s) * CAND_K;
+  ncand += ob - s;
+  ctie += ob - s;
   const int lane = threadIdx.x;
   const double sx = S[s].x, sy = S[s].y;
   const int ex = S[s].explore;
@@ -575,7 +588,7 @@ __global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __res
 #pragma unroll
   for (int j = 0; j < NN_K; j++) { tk[j] = __builtin_inff(); ti[j] = 0x7fffffff; }
   for (int n = lane; n < N; n += 64) {
-    const NnRec& rec = nodes[n];
+    const NnRec& rec = n < N0 ? nodes[n] : xrec[n - N0];
     float k = dubins_key(sx, sy, rec.x, rec.y, rec.c, rec.s);
     if (!ex) k = rec.costE + k;
     const bool f = feasible_search(sx, sy, rec.bx, rec.by, rec.ca, rec.sa, rec.ang_par, p.feas_len);
@@ -2697,6 +2710,43 @@ hipError_t launch_nn_exact_small(hipStream_t st, const clrrt_sample* S, int B, c
 }
 
 int nn_exact_small_max() { return NN_EXACT_LDS_MAX; }
+
+// The round's new nodes in commit order (sample k's regular node, then its goal-biased one) as the tree's
+// nearest-node records will hold them (ids base, base + 1, ...).  One lane: a round has a few dozen samples.
+__global__ void k_build_xrec(const clrrt_node* __restrict__ reg, const clrrt_node* __restrict__ gbn,
+                             const SampleOut* __restrict__ so, int n, int64_t base, NnRec* __restrict__ xrec) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int64_t pos = 0;
+  for (int k = 0; k < n; k++) {
+    if (so[k].k < 0) continue;
+    xrec[pos] = nn_record(reg[k], base + pos);
+    pos++;
+    if (so[k].gb_ok) {
+      xrec[pos] = nn_record(gbn[k], base + pos);
+      pos++;
+    }
+  }
+}
+
+hipError_t launch_nn_exact_x(hipStream_t st, const clrrt_sample* S, const NnRec* nodes, int N, const DevParams& p,
+                             const clrrt_node* reg, const clrrt_node* gbn, const SampleOut* so, int n, NnRec* xrec,
+                             const int* slist, const int* xcnt, int nlist, int xmax, int* cand, float* ckey,
+                             int* ncand, int* ctie) {
+  if (nlist <= 0) return hipSuccess;
+  const int Nl = N + xmax;
+  if (Nl > NN_EXACT_LDS_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_build_xrec, dim3(1), dim3(64), 0, st, reg, gbn, so, n, (int64_t)N, xrec);
+  LAUNCH_CHECK();
+  const size_t lds = sizeof(KeyId) * (size_t)Nl + sizeof(int2) * (size_t)(Nl / 2 + 64);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)&k_nn_exact_fused, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_nn_exact_fused, dim3(nlist), dim3(64), lds, st, S, nlist, nodes, N, p, cand, ckey, ncand, ctie,
+                     (const NnRec*)xrec, xcnt, slist, Nl);
+  return hipGetLastError();
+}
 
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
