@@ -146,6 +146,9 @@ struct clrrt_ctx {
   // option "exact_fixup" (default 1): EXACT rounds resolve a conflict by rolling out the conflicting new nodes for
   // the sample (k_conflict_fix) instead of ending the committed prefix there, when that decides it
   int exact_fixup = 1;
+  // option "exact_fixup_cap": fix-up rollouts run at most this many steps (0: to their end); one that reaches it is
+  // undecided and ends the prefix at its sample (re-evaluated next round), so a round never waits for a long one
+  int exact_fix_cap = 0;
   int* fix_n = nullptr;        // [max_batch]
   int* fix_ids = nullptr;      // [max_batch * FIX_MAX]
   int* fix_adj = nullptr;      // [max_batch * 5]
@@ -1381,6 +1384,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "exact_min_width" && value >= 1 && value <= 1 << 20) c->exact_min_width = (int)value;
   else if (k == "exact_fixup") c->exact_fixup = value != 0;
+  else if (k == "exact_fixup_cap" && value >= 0 && value < INT_MAX) c->exact_fix_cap = (int)value;
   else if (k == "defer_steps" && value >= 0 && value <= 1 << 20) {
     // BATCH rounds with deferred samples (changes the BATCH tree: samples whose rollouts run past T steps
     // per launch commit in a later round, by a deterministic rule the oracle restates); 0 = off
@@ -1864,6 +1868,7 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     a.xreg = c->regnodes;
     a.xgb = c->gbnodes;
     a.job_stride = 64;  // one job per wave: the fix-ups run at the lone lane's step latency
+    if (c->exact_fix_cap > 0 && c->exact_fix_cap < a.p.n_steps_max) a.p.n_steps_max = c->exact_fix_cap;
     {
       KTimer kt(c, 1);
       HIPC(c, launch_rollout(st, SRC_LIST, a));
@@ -1874,12 +1879,14 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
   // in sample order: a fix-up that succeeds changes the sample's result (it ends the prefix)
   int Lr = stop, resolved = 0;
   bool patched = false;
+  const int cap = c->exact_fix_cap > 0 && c->exact_fix_cap < c->dp.n_steps_max ? c->exact_fix_cap : 0;
   for (int j = 0, q = 0; j < stop; j++) {
     SampleOut add = delta[j];
     bool ok = true, any = fn[j] != 0;
     for (; q < nj && c->h_fix_owner[q] == j; q++) {
       const RollRes& r = c->h_fix_res[q];
-      if (!is_fail(r.outcome)) ok = false;
+      // (a capped rollout stopped at the cap: undecided -- the true iteration limit lies beyond it)
+      if (!is_fail(r.outcome) || (cap && r.outcome == CLRRT_ROLL_ITERLIMIT)) ok = false;
       add_res(add, r, +1);
     }
     if (!ok) {
