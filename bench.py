@@ -465,8 +465,15 @@ def main():
         # secondary figure: EXACT mode (the reference's sequential expandTree tree, bit for bit) on the
         # same scene and horizon, one query from a fresh tree
         pl.tree_init()
+        x0 = pl.exact_stats()
+        pl.enable_timing(True)
         st = pl.expand(clrrt.Rng(args.seed), n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_EXACT, batch=B)
+        x1 = pl.exact_stats()
+        ex_ms = {name: pl.kernel_time(w)[0] / max(1, st["rounds"]) for name, w in (("nn", 0), ("rollout", 1), ("commit", 2))}
         exact_line = {"value": st["nodes_added"] / (st["elapsed_ms"] * 1e-3), "unit": "nodes/s",
+                      "ms_per_round": st["elapsed_ms"] / max(1, st["rounds"]),
+                      "device_ms_per_round": ex_ms,
+                      "fixups": {k: x1[k] - x0[k] for k in x1},
                       "feasible_paths_per_s": st["goal_nodes_added"] / (st["elapsed_ms"] * 1e-3),
                       "iterations": st["iterations"], "rounds": st["rounds"], "speculated": st["speculated"],
                       "horizon_ms": horizon,

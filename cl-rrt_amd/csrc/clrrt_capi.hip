@@ -1724,8 +1724,11 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     HIPC(c, dalloc(&c->fix_xkey, B * K));
     HIPC(c, dalloc(&c->fix_xn, 2 * B));
   }
-  HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->ckey,
-                              c->res_spec, c->fix_n, c->fix_ids, c->fix_adj));
+  {
+    KTimer kt(c, 2);
+    HIPC(c, launch_conflict_fix(st, c->dp, n, c->d_samples, c->regnodes, c->gbnodes, c->so, c->ctie, c->ncand, c->ckey,
+                                c->res_spec, c->fix_n, c->fix_ids, c->fix_adj));
+  }
   c->h_fix.resize((size_t)n * (1 + FIX_MAX + 5));
   c->h_fix_smp.resize(n);
   c->h_fix_so.resize(n);
@@ -1771,9 +1774,12 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
     std::vector<int> xs(2 * nl);
     for (int i = 0; i < nl; i++) { xs[i] = xl[i]; xs[nl + i] = xpre[xl[i]]; }
     HIPC(c, hipMemcpyAsync(c->fix_xi, xs.data(), sizeof(int) * 2 * nl, hipMemcpyHostToDevice, st));
-    HIPC(c, launch_nn_exact_x(st, c->d_samples, c->nn, (int)N, c->dp, c->regnodes, c->gbnodes, c->so, n, c->fix_xrec,
-                              c->fix_xi, c->fix_xi + nl, nl, xpre[n], c->fix_xcand, c->fix_xkey, c->fix_xn,
-                              c->fix_xn + nl));
+    {
+      KTimer kt(c, 0);
+      HIPC(c, launch_nn_exact_x(st, c->d_samples, c->nn, (int)N, c->dp, c->regnodes, c->gbnodes, c->so, n, c->fix_xrec,
+                                c->fix_xi, c->fix_xi + nl, nl, xpre[n], c->fix_xcand, c->fix_xkey, c->fix_xn,
+                                c->fix_xn + nl));
+    }
     xc.resize((size_t)nl * K);
     xn.resize(nl);
     HIPC(c, hipMemcpyAsync(xc.data(), c->fix_xcand, sizeof(int) * nl * K, hipMemcpyDeviceToHost, st));
