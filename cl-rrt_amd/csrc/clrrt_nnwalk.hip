@@ -62,6 +62,9 @@ namespace clrrt {
 #define WALK_HALF_SUPER 1  // HALF format: keep each super-tile's phase-1 bound in LDS (2 more bytes per super-tile)
 #endif
 #define WALK_TQ 68      // tile stack entries (a super-tile pair adds <= 64 to <= 3 pending)
+#ifndef WALK_SPLIT_SHARE
+#define WALK_SPLIT_SHARE 1  // the overflow split waves of one record share their bounds (round 5)
+#endif
 #ifndef WALK_APBINS
 #define WALK_APBINS 8  // ang_par sectors (top key bits)
 #endif
@@ -622,6 +625,17 @@ __device__ __forceinline__ void walk_one(const clrrt_sample* __restrict__ S, int
     if (SPLIT && w_less(kb, ib, kth, idk)) { kth = kb; idk = ib; }
     const float u10 = uni(__shfl(uk, NN_K - 1, 64));
     if (u10 < kth) { kth = u10; idk = 0x7fffffff; }
+#if WALK_SPLIT_SHARE
+    if constexpr (SPLIT) {
+      // the record's nch waves share their bounds: each one's 11th entry (or u10, or the handed-over entry) bounds
+      // the sample's true 11th key, so a pair above the smallest of them enters no list (a key-only bound, ties
+      // kept); published with an ordered-int atomicMin (keys are >= 0) in the record's spare word
+      int* sh = &ovf[o_sp].w;
+      if (lane == 0 && kth < __builtin_inff() && !(kth < 0.f)) atomicMin(sh, kth > 0.f ? __float_as_int(kth) : 0);
+      const float shv = __int_as_float(uni(__atomic_load_n(sh, __ATOMIC_RELAXED)));
+      if (shv < kth) { kth = shv; idk = 0x7fffffff; }
+    }
+#endif
     if constexpr (CODED) kth_c = uni(lc_le(kth - base));
     if (kth < __builtin_inff()) {
       const float R = (kth + 2e-4f) * (1.0f / 0.9999f);
@@ -912,6 +926,9 @@ __device__ __forceinline__ void walk_one(const clrrt_sample* __restrict__ S, int
   // those of their tiles beyond T
   auto visit_supers = [&](int la, int lb2, float Tp, float T, bool first) {
     const uint64_t c0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+#if WALK_SPLIT_SHARE
+    if constexpr (SPLIT) refresh();  // the other waves' bounds
+#endif
     n_sup += 1 + (lb2 >= 0);
     const int sa = gst(la), sb = lb2 >= 0 ? gst(lb2) : -1;
     const int lo = lane < 32 ? la : lb2;  // local index (LDS)
@@ -1079,7 +1096,9 @@ __device__ __forceinline__ void walk_one(const clrrt_sample* __restrict__ S, int
           if (lane == 0) slot = atomicAdd(ovf_n, 1);
           slot = uni(__shfl(slot, 0, 64));
           if (slot < max_over) {  // hand over: the split waves and the merge write this sample's list
-            if (lane == 0) ovf[slot] = make_int4(s, __float_as_int(kth), idk == 0x7fffffff ? idk : idk + 1, 0);
+            if (lane == 0)
+              ovf[slot] = make_int4(s, __float_as_int(kth), idk == 0x7fffffff ? idk : idk + 1,
+                                    kth > 0.f ? __float_as_int(kth) : kth == 0.f ? 0 : 0x7f800000);  // .w: shared bound
             if (stats && lane == 0) atomicAdd(&stats[14], 1ull);  // overflow records (work_ctr[32])
             flush_stats();
             return;

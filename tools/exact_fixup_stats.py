@@ -11,9 +11,12 @@ import clrrt  # noqa: E402
 from clrrt import abi, scenes  # noqa: E402
 
 ms = float(sys.argv[1]) if len(sys.argv) > 1 else 2000.0
-for opts in ({"exact_fixup": 0}, {"exact_fixup": 1}, {"exact_fixup": 1, "exact_fixup_cap": 48},
-             {"exact_fixup": 1, "exact_fixup_cap": 96}, {"exact_fixup": 1, "exact_fixup_cap": 160},
-             {"exact_fixup": 1, "exact_fixup_cap": 96, "exact_min_width": 16}):
+sets = ({"exact_fixup": 0}, {"exact_fixup": 1}, {"exact_fixup": 1, "exact_fixup_cap": 48},
+        {"exact_fixup": 1, "exact_fixup_cap": 96}, {"exact_fixup": 1, "exact_fixup_cap": 160},
+        {"exact_fixup": 1, "exact_fixup_cap": 96, "exact_min_width": 16})
+if len(sys.argv) > 2 and sys.argv[2] == "default":  # (kernel traces: the default settings only)
+    sets = ({"exact_fixup": 1},)
+for opts in sets:
     pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 20,
                        max_rows=1 << 26, max_batch=16384)
     pl.set_obstacles(scenes.urban_scene(200))
