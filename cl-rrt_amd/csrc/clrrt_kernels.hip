@@ -639,14 +639,22 @@ __global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __res
     if (lane == 0) { ncand[s] = sel; ctie[s] = 0; }
     return;
   }
-  // positions needed: every entry with key <= the sort_limit-th feasible key (all when fewer are feasible)
-  int need = N;
-  if (sel == p.sort_limit) {
-    const float K = keys[sel - 1];
-    int c = 0, nan = 0;
+  // Only the order of equal keys is std::sort's: KT = the largest key of a tie in the list (list entry j and the
+  // next feasible entry equal).  Every feasible entry with key <= KT takes its place from the replay, which
+  // needs positions [0, need), need = the entries with key <= KT; the list's entries above KT have keys no other
+  // feasible entry shares (a neighbour with an equal key would make theirs a tie <= KT), so they follow in key
+  // order.  (Round 4 replayed up to the sort_limit-th key, and the whole array when fewer entries were feasible:
+  // hundreds of microseconds per tied sample on one lane's final insertion sort.)
+  float KT = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < CAND_K; j++)
+    if (j < sel && j + 1 < valid && keys[j] == keys[j + 1]) KT = keys[j];  // (ascending: the last is the largest)
+  int need, nan = 0;
+  {
+    int c = 0;
     for (int n = lane; n < N; n += 64) {
       const float k = s_kv[n].key;
-      c += !(K < k);
+      c += !(KT < k);
       nan |= k != k;
     }
 #pragma unroll
@@ -654,16 +662,16 @@ __global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __res
       c += __shfl_xor(c, o, 64);
       nan |= __shfl_xor(nan, o, 64);
     }
-    need = nan ? N : c;  // (a NaN key has no place in the order: the whole replay)
+    need = nan ? N : c;  // (a NaN key has no place in the order: the whole replay, and the walk below covers all)
   }
   __syncthreads();
   wave_std_sort(s_kv, N, s_pairs, need);
   int cnt = 0;
-  for (int i0 = 0; i0 < N && cnt < p.sort_limit; i0 += 64) {
+  for (int i0 = 0; i0 < need && cnt < p.sort_limit; i0 += 64) {
     const int i = i0 + lane;
     bool f = false;
     KeyId e{0, 0.f};
-    if (i < N) {
+    if (i < need) {
       e = s_kv[i];
       f = e.id >= 0;
     }
@@ -674,6 +682,18 @@ __global__ void __launch_bounds__(64) k_nn_exact_fused(const clrrt_sample* __res
       ckey[s * CAND_K + rank] = e.key;
     }
     cnt = min(p.sort_limit, cnt + __popcll(m));
+  }
+  if (!nan) {  // the list's entries above KT, in key order
+#pragma unroll
+    for (int j = 0; j < CAND_K; j++) {
+      if (j < sel && KT < keys[j] && cnt < p.sort_limit) {
+        if (lane == 0) {
+          cand[s * CAND_K + cnt] = ids[j];
+          ckey[s * CAND_K + cnt] = keys[j];
+        }
+        cnt++;
+      }
+    }
   }
   for (int j = cnt + lane; j < CAND_K; j += 64) cand[s * CAND_K + j] = -1;
   if (lane == 0) { ncand[s] = cnt; ctie[s] = 1; }
@@ -883,6 +903,8 @@ __device__ __forceinline__ double roll_step_pre(Roll& r, const DevParams& p, dou
   // VehicleODE + IntegrateEuler (simulation.cpp:11-34)
   const double d2 = ode_euler(r, p, dc, ac);
   if (pc) pc->mark(2);
+  // (round 5: the branched functions for waves with at most 2 lanes in flight measured 5% slower per lone step
+  // than this block, whose independent chains interleave -- profiles/r05l_sparse_trig_tie_replay_ab.txt)
   if (!glibc::step_trig(r.x2, r.x3, r.s2, r.c2, r.swp, r.cwp, r.t3)) {  // one branch-free block (in domain)
     glibc::sincos_sel(r.x2, r.s2, r.c2);
     r.t3 = glibc::tan(r.x3);
