@@ -14,8 +14,8 @@ ms = float(sys.argv[1]) if len(sys.argv) > 1 else 2000.0
 sets = ({"exact_fixup": 0}, {"exact_fixup": 1}, {"exact_fixup": 1, "exact_fixup_cap": 48},
         {"exact_fixup": 1, "exact_fixup_cap": 96}, {"exact_fixup": 1, "exact_fixup_cap": 160},
         {"exact_fixup": 1, "exact_fixup_cap": 96, "exact_min_width": 16})
-if len(sys.argv) > 2 and sys.argv[2] == "default":  # (kernel traces: the default settings only)
-    sets = ({"exact_fixup": 1},)
+if len(sys.argv) > 2 and sys.argv[2] == "default":  # (kernel traces: the default settings only; k=v options after)
+    sets = ({"exact_fixup": 1, **{kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[3:]}},)
 for opts in sets:
     pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 20,
                        max_rows=1 << 26, max_batch=16384)
