@@ -260,6 +260,53 @@ def _replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
     out.put((nodes, goals, time.perf_counter() - t0))
 
 
+def _gpu_exact_replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
+    """One GPU EXACT-mode planner process (its own HIP context and streams): a warm-up query, then n_queries
+    queries of horizon_ms (fresh tree each, seeds seed, seed + 1, ...) after the common start line."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "cl-rrt_amd"))
+    import clrrt
+    from clrrt import abi, scenes
+    cfg = CONFIGS[cfg_name]
+    obs = scenes.urban_scene(cfg["obstacles"], cfg["moving"])
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 18,
+                       max_rows=1 << 24, max_batch=1024, max_obstacles=max(1, len(obs)))
+    pl.set_obstacles(obs)
+    pl.tree_init()
+    pl.expand(clrrt.Rng(seed + 999), n_iters=0, budget_ms=200.0, mode=clrrt.CLRRT_MODE_EXACT, batch=1024)
+    barrier.wait()
+    t0 = time.perf_counter()
+    nodes = goals = 0
+    for q in range(n_queries):
+        pl.tree_init()
+        st = pl.expand(clrrt.Rng(seed + q), n_iters=0, budget_ms=horizon_ms, mode=clrrt.CLRRT_MODE_EXACT, batch=1024)
+        nodes += st["nodes_added"]
+        goals += st["goal_nodes_added"]
+    out.put((nodes, goals, time.perf_counter() - t0))
+    pl.close()
+
+
+def gpu_exact_replicas(cfg_name, horizon_ms, R, seed, n_queries=2):
+    """EXACT mode as the CPU baseline's replicas run the reference: R independent planner processes sharing the GPU
+    (each query's tree is the reference's sequential one), started together; aggregate nodes/s over the slowest
+    replica's wall time.  Runs before the bench process touches the GPU (the replicas are separate processes)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    barrier, out = ctx.Barrier(R), ctx.Queue()
+    procs = [ctx.Process(target=_gpu_exact_replica, args=(cfg_name, horizon_ms, n_queries, seed + 100 * k, barrier, out))
+             for k in range(R)]
+    for p in procs:
+        p.start()
+    res = [out.get() for _ in range(R)]
+    for p in procs:
+        p.join()
+    wall = max(r[2] for r in res)
+    return {"value": sum(r[0] for r in res) / wall, "unit": "nodes/s", "replicas": R,
+            "feasible_paths_per_s": sum(r[1] for r in res) / wall,
+            "sample": f"{R} independent EXACT-mode planner processes on the one GPU x {n_queries} queries x "
+                      f"{horizon_ms:.0f} ms, seeds {seed}+100k, started together, aggregate nodes over the slowest "
+                      f"replica's {wall:.2f} s (each tree the reference's sequential one for its seed)"}
+
+
 def cpu_share():
     """Host cores this job may use: the affinity set, capped by OMP_NUM_THREADS where the GPU box sets
     the job's CPU share (16 per GPU) — os.cpu_count() there is the whole machine's."""
@@ -317,6 +364,11 @@ def main():
     cpu_line = None
     if world == 1 and not args.no_cpu:
         cpu_line = cpu_baseline(args.config, horizon, args.cpu_queries, args.seed)
+    # EXACT mode the way the CPU baseline's replicas run the reference: as many independent planner processes as
+    # the CPU replicas (at most 16 share the GPU), also before this process touches the GPU
+    exact_rep = None
+    if world == 1 and not args.no_exact and not cfg.get("replan"):
+        exact_rep = gpu_exact_replicas(args.config, horizon, min(16, cpu_share()), args.seed)
 
     import torch
     import torch.distributed as dist
@@ -479,6 +531,8 @@ def main():
                       "horizon_ms": horizon,
                       "note": "EXACT mode: trees identical to the reference's sequential expandTree (same seed); "
                               "1 query, wall clock"}
+        if exact_rep is not None:
+            exact_line["replicas"] = exact_rep
 
     if rank != 0:
         if world > 1:

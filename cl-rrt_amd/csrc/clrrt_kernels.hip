@@ -974,7 +974,7 @@ struct CoopLds {
 constexpr size_t kCoopLdsPerWave = 64 * sizeof(Box4) + 64 * sizeof(double) + 64 * sizeof(int) + COOP_QCAP * sizeof(uint32_t);
 
 __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p, const ObsView& ov, uint32_t& tests,
-                                    const CoopLds& cl) {
+                                    const CoopLds& cl, unsigned long long* cs = nullptr) {
   const int lane = threadIdx.x & 63;
   // owner records in the scratch: (fvx, fvy, ft, first item) | pair-range start | static count | window
   // start owners | survivor flags
@@ -1021,6 +1021,10 @@ __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p,
   s_need[lane] = 0;
   __builtin_amdgcn_wave_barrier();
   int carry = -1;  // owner of the window's first pair when its range began in an earlier window
+#ifdef CLRRT_COLL_STATS
+  // diagnostics: wave-steps, lanes checked, pairs, windows, windows with a survivor, survivors, vehicle boxes built
+  unsigned long long st_w = 0, st_s = 0, st_v = 0;
+#endif
   for (int t0 = 0; t0 < total; t0 += 64) {
     // the owners whose range starts inside this window, at their first position
     const bool starts = len > 0 && pre >= t0 && pre < t0 + 64;
@@ -1046,7 +1050,14 @@ __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p,
     }
     // the window's last pair's owner continues into the next window
     carry = __shfl(owner, 63, 64);
+#ifdef CLRRT_COLL_STATS
+    st_w++;
+    st_s += __popcll(__ballot(surv));
+#endif
     if (__ballot(surv)) {
+#ifdef CLRRT_COLL_STATS
+      st_v++;
+#endif
       if (surv && s_need[owner] != 2) s_need[owner] = 1;
       __builtin_amdgcn_wave_barrier();
       if (s_need[lane] == 1) {  // setVertices of the lanes with a survivor (once per step)
@@ -1064,6 +1075,17 @@ __device__ double obs_distance_coop(bool act, const Roll& r, const DevParams& p,
     }
     __builtin_amdgcn_wave_barrier();
   }
+#ifdef CLRRT_COLL_STATS
+  const unsigned long long st_u = __popcll(__ballot(use));
+  if (cs && lane == 0) {
+    atomicAdd(&cs[0], 1ull);
+    atomicAdd(&cs[1], st_u);
+    atomicAdd(&cs[2], (unsigned long long)total);
+    atomicAdd(&cs[3], st_w);
+    atomicAdd(&cs[4], st_v);
+    atomicAdd(&cs[5], st_s);
+  }
+#endif
   double D = 10000;
   if (use) {
     const int h = cl.hit[lane];
@@ -1730,7 +1752,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     }
     double Dobs;
     if constexpr (COOP) {
-      Dobs = obs_distance_coop(act, r, a.p, ov, w.box, cl);
+      Dobs = obs_distance_coop(act, r, a.p, ov, w.box, cl, a.ctr ? a.ctr + 33 : nullptr);
       if (!act) continue;
     } else {
       Dobs = obs_distance<NEED_GAP>(r, a.p, ov, w.box);
