@@ -1227,6 +1227,22 @@ __device__ __forceinline__ ObsView stage_obstacles(const RollArgs& a, float4* ld
                  a.grid.gw, a.grid.gh, a.grid.nmov, a.grid.x0, a.grid.y0, a.grid.inv};
 }
 
+// The query's parameters in the rollout kernels: in LDS (CLRRT_PARAMS_LDS 1: the step reads each one when it needs it,
+// instead of holding ~100 SGPRs of them all kernel long -- spilled to VGPR lanes and read back lane by lane) or the
+// kernel argument (0).
+#ifndef CLRRT_PARAMS_LDS
+#define CLRRT_PARAMS_LDS 1
+#endif
+#if CLRRT_PARAMS_LDS
+#define CLRRT_PARAMS_DECL(P)                    \
+  __shared__ DevParams s_params_;               \
+  if (threadIdx.x == 0) s_params_ = a.p;        \
+  __syncthreads();                              \
+  const DevParams& P = s_params_
+#else
+#define CLRRT_PARAMS_DECL(P) const DevParams& P = a.p
+#endif
+
 #ifndef CLRRT_ROLLOUT_WAVES
 #define CLRRT_ROLLOUT_WAVES 1
 #endif
@@ -1235,6 +1251,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   extern __shared__ float4 lds[];
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
+  CLRRT_PARAMS_DECL(P);
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int js = a.job_stride > 1 ? a.job_stride : 1;
   const int j = gt / js;
@@ -1253,7 +1270,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       const SimJob& sj = a.sims[j];
       RefD R;
       if (sj.gb) {
-        R = make_goal_ref(sj.ax, sj.ay, a.p);
+        R = make_goal_ref(sj.ax, sj.ay, P);
       } else {
         R.a1x = sj.ax; R.a1y = sj.ay; R.h1x = sj.hx; R.h1y = sj.hy;
         R.a2x = R.a2y = R.h2x = R.h2y = 0.0;
@@ -1264,7 +1281,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       for (int k = 0; k < 10; k++) ps.v[k] = sj.st[k];
       RollRes out;
       Roll ini;
-      run_rollout_ref<NEED_GAP>(ps, R, sj.vstart, sj.gb, a.p, ov, sj.row_off >= 0 ? a.arena + sj.row_off * 10 : nullptr,
+      run_rollout_ref<NEED_GAP>(ps, R, sj.vstart, sj.gb, P, ov, sj.row_off >= 0 ? a.arena + sj.row_off * 10 : nullptr,
                                 1, out, w, &ini);
       a.res[j] = out;
       if (sj.ref_off >= 0) {  // the reference the Simulation used, with the profile it generated
@@ -1312,8 +1329,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   if (act) {
     for (int pass = 0; pass < 2; pass++) {
       RollRes out;
-      const RefD R = gb ? make_goal_ref(pbx, pby, a.p) : make_ref(pbx, pby, sx, sy, a.p);
-      run_rollout_ref<NEED_GAP>(ps, R, pvb, gb, a.p, ov, rows, es, out, w, nullptr, pc);
+      const RefD R = gb ? make_goal_ref(pbx, pby, P) : make_ref(pbx, pby, sx, sy, P);
+      run_rollout_ref<NEED_GAP>(ps, R, pvb, gb, P, ov, rows, es, out, w, nullptr, pc);
       if (pass == 1) {
         a.res_gb[j] = out;
         break;
@@ -1321,7 +1338,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       a.res[j] = out;
       if (SRC != SRC_SPEC) break;
       const bool ok = (out.outcome == CLRRT_ROLL_END || out.outcome == CLRRT_ROLL_GOAL) &&
-                      feasible_goal_bias(a.p, out.st, out.bx, out.by);
+                      feasible_goal_bias(P, out.st, out.bx, out.by);
       if (!ok) {
         a.res_gb[j].outcome = -1;
         break;
@@ -1467,6 +1484,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   extern __shared__ float4 lds[];
   glibc::stage_tables();
   const ObsView ov = stage_obstacles<NEED_GAP>(a, lds);
+  CLRRT_PARAMS_DECL(P);
   const int lane = threadIdx.x & 63;
   CoopLds cl{};
   if constexpr (COOP) {
@@ -1576,7 +1594,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
           a.res[j] = out;
           const bool ok = fin == CLRRT_ROLL_END || fin == CLRRT_ROLL_GOAL;
           if (ok) atomicMin(&best[bs], k);
-          if (ok && feasible_goal_bias(a.p, out.st, out.bx, out.by)) {
+          if (ok && feasible_goal_bias(P, out.st, out.bx, out.by)) {
             // goal-biased rollout from the node this rollout would append (expandTree :163-173)
 #pragma unroll
             for (int q = 0; q < 10; q++) src.st[q] = out.st[q];
@@ -1598,8 +1616,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   // :165-168; simulation.cpp:36-47), and stateArray[0] when the lane writes rows
   auto init_pending = [&]() {
     if (iq) {
-      const RefD R = src.gb ? make_goal_ref(src.bx, src.by, a.p) : make_ref(src.bx, src.by, src.sx, src.sy, a.p);
-      roll_init(r, src.st, R, src.vb, src.gb != 0, a.p);
+      const RefD R = src.gb ? make_goal_ref(src.bx, src.by, P) : make_ref(src.bx, src.by, src.sx, src.sy, P);
+      roll_init(r, src.st, R, src.vb, src.gb != 0, P);
       c7 = (double)r.wp; c8 = src.st[8]; c9 = src.st[9];
       steps = 0;
       if (rows) {
@@ -1748,17 +1766,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       const bool check = !rp && (steps & (CLRRT_ABANDON_EVERY - 1)) == 0;
       best_s = check ? __atomic_load_n(&best[bs], __ATOMIC_RELAXED) : 0x7fffffff;
       if (pc) pc->mark(6);
-      d2 = roll_step_pre(r, a.p, c7, c8, c9, w, pc);
+      d2 = roll_step_pre(r, P, c7, c8, c9, w, pc);
     }
     double Dobs;
     if constexpr (COOP) {
-      Dobs = obs_distance_coop(act, r, a.p, ov, w.box, cl, a.ctr ? a.ctr + 33 : nullptr);
+      Dobs = obs_distance_coop(act, r, P, ov, w.box, cl, a.ctr ? a.ctr + 33 : nullptr);
       if (!act) continue;
     } else {
-      Dobs = obs_distance<NEED_GAP>(r, a.p, ov, w.box);
+      Dobs = obs_distance<NEED_GAP>(r, P, ov, w.box);
     }
     if (pc) pc->mark(4);
-    int o = roll_step_post(r, a.p, Dobs, d2);
+    int o = roll_step_post(r, P, Dobs, d2);
 #ifdef CLRRT_ROLL_PROFILE
     job_steps++;
     chain_steps = max(chain_steps, job_steps);
@@ -1771,7 +1789,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     // a replay writes no row past its committed node's (a longer one is counted in n_rep_bad below)
     if (rows && (!rp || steps < nrows_rp)) store_row(rows + (int64_t)steps * 10, 1, r, c7, c8, c9);
     if (pc) pc->mark(5);
-    if (o < 0 && steps >= a.p.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
+    if (o < 0 && steps >= P.n_steps_max) o = CLRRT_ROLL_ITERLIMIT;
     if (o >= 0) {
       fin = o;
     } else if (best_s < k) {
