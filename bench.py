@@ -260,7 +260,7 @@ def _replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
     out.put((nodes, goals, time.perf_counter() - t0))
 
 
-def _gpu_exact_replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
+def _gpu_exact_replica(cfg_name, horizon_ms, n_queries, seed, barrier, out, opts=None):
     """One GPU EXACT-mode planner process (its own HIP context and streams): a warm-up query, then n_queries
     queries of horizon_ms (fresh tree each, seeds seed, seed + 1, ...) after the common start line."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "cl-rrt_amd"))
@@ -271,6 +271,8 @@ def _gpu_exact_replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
     pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=1 << 18,
                        max_rows=1 << 24, max_batch=1024, max_obstacles=max(1, len(obs)))
     pl.set_obstacles(obs)
+    for k, v in (opts or {}).items():
+        pl.set_option(k, v)
     pl.tree_init()
     pl.expand(clrrt.Rng(seed + 999), n_iters=0, budget_ms=200.0, mode=clrrt.CLRRT_MODE_EXACT, batch=1024)
     barrier.wait()
@@ -285,15 +287,15 @@ def _gpu_exact_replica(cfg_name, horizon_ms, n_queries, seed, barrier, out):
     pl.close()
 
 
-def gpu_exact_replicas(cfg_name, horizon_ms, R, seed, n_queries=2):
+def gpu_exact_replicas(cfg_name, horizon_ms, R, seed, n_queries=2, opts=None):
     """EXACT mode as the CPU baseline's replicas run the reference: R independent planner processes sharing the GPU
     (each query's tree is the reference's sequential one), started together; aggregate nodes/s over the slowest
     replica's wall time.  Runs before the bench process touches the GPU (the replicas are separate processes)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     barrier, out = ctx.Barrier(R), ctx.Queue()
-    procs = [ctx.Process(target=_gpu_exact_replica, args=(cfg_name, horizon_ms, n_queries, seed + 100 * k, barrier, out))
-             for k in range(R)]
+    procs = [ctx.Process(target=_gpu_exact_replica, args=(cfg_name, horizon_ms, n_queries, seed + 100 * k, barrier, out,
+                                                          opts)) for k in range(R)]
     for p in procs:
         p.start()
     res = [out.get() for _ in range(R)]
