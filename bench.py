@@ -422,10 +422,12 @@ def main():
         rp = {"pose": [0.0, 0.0, 0.0, 0.0, 0.0, 0.0], "q": 0, "outcomes": [], "reinit_ms": 0.0, "path_len": []}
 
     deferred = [0]
+    rounds = [0]
 
     def expand_query(rng):
         st = pl.expand(rng, n_iters=0, budget_ms=horizon, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
         deferred[0] += st["deferred"]
+        rounds[0] += st["rounds"]
         return st["nodes_added"], st["goal_nodes_added"], st["capacity_stop"]
 
     def query(seed):
@@ -466,6 +468,7 @@ def main():
         query(args.seed + 1000 + w)
     pl.enable_timing(True)
     pl.reset_counters()
+    rounds[0] = 0
     barrier_sync()
     t0 = time.perf_counter()
     tot_nodes = tot_goals = cap_stops = 0
@@ -497,6 +500,22 @@ def main():
     nn_ms, nn_n = pl.kernel_time(0)
     walk_ms, walk_n = pl.kernel_time(3)
     other_ms, other_n = pl.kernel_time(2)
+    wait_ms, wait_n = pl.kernel_time(4)
+    xch_ms, xch_n = pl.kernel_time(5)
+    # where a round's time goes on this rank (per round of the timed queries): wall time, the rollout launch, the
+    # walk searches' summed event time (overlapping launches: not a critical-path figure), the main stream's wait
+    # for the side streams' lists (the search's share of the critical path) and the exchange's stream span
+    nr = max(1, rounds[0])
+    split = [float(rounds[0]), elapsed * 1e3 / nr, roll_ms / nr, walk_ms / nr, wait_ms / nr,
+             xch_ms / nr, float(pl.size()[0])]
+    per_rank = [split]
+    if world > 1:
+        t = torch.tensor(split, dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [p.cpu().tolist() for p in parts]
+    round_split = [dict(zip(("rounds", "round_ms", "rollout_ms", "walk_event_ms", "list_wait_ms", "exchange_ms",
+                             "tree_nodes_last"), v)) for v in per_rank]
     work = pl.work_counters()
     cnt = pl.counters()
     sw = pl.search_work_ex()
@@ -637,6 +656,10 @@ def main():
         },
         "kernel_ms": {"rollout": roll_ms, "nn": nn_ms, "select_commit": other_ms,
                       "launches": {"rollout": roll_n, "nn": nn_n, "other": other_n}},
+        "round_split": round_split if world > 1 else round_split[0],
+        "round_split_note": "per round of the timed queries (per rank with N > 1): wall ms, rollout launch ms, walk "
+                            "searches' summed event ms (overlapping launches), the main stream's wait for the lists "
+                            "(the search's share of the critical path), the exchange's stream span",
         "work": {**work, **cnt},
     }
     if replanning:

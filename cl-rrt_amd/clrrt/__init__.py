@@ -25,10 +25,8 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "clrrt.h")
 
 _lib = None
 P = C.POINTER
-# clrrt_exchange_fn (include/clrrt.h): (user, n_local, elapsed_ms, aux_local, *dev_all, *n_all, *max_elapsed_ms,
-# *aux_sum) -> status
-EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_double, C.c_int64, P(C.c_void_p), P(C.c_int32),
-                          P(C.c_double), P(C.c_int64))
+# clrrt_exchange_fn (include/clrrt.h): (user, clrrt_exchange_io*) -> status
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, P(abi.ExchangeIO))
 
 _SIGS = {
     "clrrt_abi_version": (C.c_int, []),
@@ -462,8 +460,9 @@ class Planner:
     def exact_stats(self):
         out = (C.c_int64 * 10)()
         self._chk(self.L.clrrt_exact_stats(self.h, out), "exact_stats")
+        # (out[9] is reserved: a window without a result is always resolved, clrrt.h)
         return dict(zip(("rounds", "resolved", "fixup_rollouts", "conflict_rounds", "end_fixup_succeeded", "end_tie",
-                         "end_key_eq_thr", "end_over_slots", "end_pushed_out", "end_full_window"), list(out)))
+                         "end_key_eq_thr", "end_over_slots", "end_pushed_out"), list(out)[:9]))
 
     def iteration_log(self, on=True):
         self._chk(self.L.clrrt_iteration_log(self.h, 1 if on else 0), "iteration_log")

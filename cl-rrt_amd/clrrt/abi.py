@@ -5,7 +5,7 @@ header documents so a drift between the two fails at import time.
 """
 import ctypes as C
 
-CLRRT_ABI_VERSION = 10  # include/clrrt.h
+CLRRT_ABI_VERSION = 11  # include/clrrt.h
 UNIT_OBB, UNIT_ODE, UNIT_LATERAL, UNIT_PROFILE, UNIT_ANGLE = 0, 1, 2, 3, 4  # CLRRT_UNIT_*
 UNIT_DUBINS, UNIT_FEASIBLE, UNIT_GOALBIAS, UNIT_GOALREF, UNIT_CTRL = 5, 6, 7, 8, 9
 UNIT_PROFILE_NMAX = 1024
@@ -98,12 +98,20 @@ class RolloutResult(C.Structure):
                 ("ref_vback", C.c_double), ("ref_n", C.c_int32), ("pad", C.c_int32)]
 
 
+class ExchangeIO(C.Structure):  # clrrt_exchange_io (the sharded expansion's exchange hook)
+    _fields_ = [("n_local", C.c_int32), ("flags", C.c_int32), ("elapsed_ms", C.c_double), ("aux_local", C.c_int64),
+                ("bbox_local", C.c_double * 4), ("stream", C.c_void_p),
+                ("dev_all", C.c_void_p), ("n_all", C.c_int32), ("pad", C.c_int32), ("max_elapsed_ms", C.c_double),
+                ("aux_sum", C.c_int64), ("bbox_all", C.c_double * 4)]
+
+
 def _check_sizes():
     assert C.sizeof(Node) == 160, C.sizeof(Node)
     assert C.sizeof(Obstacle) == 56
     assert C.sizeof(Rng) == 140
     assert C.sizeof(Sample) == 24
     assert C.sizeof(RolloutResult) == 136, C.sizeof(RolloutResult)
+    assert C.sizeof(ExchangeIO) == 128, C.sizeof(ExchangeIO)
 
 
 _check_sizes()

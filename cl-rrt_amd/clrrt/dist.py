@@ -17,17 +17,18 @@ class RoundExchange:
     """All-gather of one round's accepted-node records, count-prefixed.
 
     Row 0 of `buf` is a header (int64 record count, float64 elapsed query ms, int64 aux value summed over the
-    ranks); clrrt_round_eval writes
+    ranks, float64[4] bounds of the rank's record positions); clrrt_round_eval writes
     this rank's records from row 1 on (`records_ptr`).  One all-gather moves header + the first `bound`
     record rows of every rank, so no count exchange (and no host sync) precedes the data; the headers
-    are read back once afterwards (the engine appends the union, so it needs the counts on the host).
+    are read back once afterwards -- the one host wait of a round: the engine appends the union, so it needs the
+    counts (and the budget word, the bounds) on the host.
     `bound` starts at `first_bound` (the sharded expansion passes this rank's slice size: a round commits
     about 0.4 records per sample) and adapts to 1.25x the largest count seen; a round whose count exceeds it
     (rare) moves the excess with a second all-gather (`second_gathers`; `collectives` counts them all).
     gloo (CPU rehearsal of the path) stages device buffers through the host.
     """
 
-    HDR = 24
+    HDR = 56
 
     def __init__(self, cap_records, device, group=None, first_bound=1024):
         self.group = group
@@ -56,22 +57,36 @@ class RoundExchange:
         dist.all_gather(parts, src, group=self.group)
         return parts
 
-    def exchange(self, n_local, elapsed_ms, aux=0):
+    def exchange(self, n_local, elapsed_ms, aux=0, bbox=None, engine_stream=None):
         """Returns (records (total, 160) uint8 on the buffer's device in global sample order, counts
         per rank, first row of this rank's records, max elapsed ms over ranks); the sum of `aux` over the
-        ranks is left in self.aux_sum."""
+        ranks is left in self.aux_sum and the union of the ranks' `bbox` (x0, y0, x1, y1) in self.bbox_all.
+
+        engine_stream (a HIP stream handle): the stream the records were written on and the gathered records will
+        be read on.  The gather is ordered after it and it after the gather by stream waits, not by the host;
+        without one, torch's stream is synchronised before returning (the round API's callers)."""
         import numpy as np
         self.exchanges += 1
-        hdr = np.zeros(3, dtype=np.float64)
+        cuda = self.dev.type == "cuda"
+        ext = None
+        if cuda and engine_stream:
+            cur = torch.cuda.current_stream(self.dev)
+            if int(engine_stream) != cur.cuda_stream:
+                ext = torch.cuda.ExternalStream(int(engine_stream), device=self.dev)
+                cur.wait_stream(ext)  # the records were written on the engine's stream
+        hdr = np.zeros(self.HDR // 8, dtype=np.float64)
         hdr.view(np.int64)[0] = int(n_local)
         hdr[1] = float(elapsed_ms)
         hdr.view(np.int64)[2] = int(aux)
+        hdr[3:7] = bbox if bbox is not None else (np.inf, np.inf, -np.inf, -np.inf)
         self.buf[0, :self.HDR].copy_(torch.from_numpy(hdr.view(np.uint8)))
         parts = self._gather(self.buf[:self.bound + 1])
         heads = torch.stack([q[0, :self.HDR] for q in parts]).cpu().numpy()
         counts = [int(c) for c in heads[:, :8].copy().view(np.int64)[:, 0]]
         t_max = float(heads[:, 8:16].copy().view(np.float64).max())
         self.aux_sum = int(heads[:, 16:24].copy().view(np.int64).sum())
+        bb = heads[:, 24:56].copy().view(np.float64).reshape(-1, 4)
+        self.bbox_all = (float(bb[:, 0].min()), float(bb[:, 1].min()), float(bb[:, 2].max()), float(bb[:, 3].max()))
         maxc = max(counts)
         extra = None
         if maxc > self.bound:
@@ -90,23 +105,27 @@ class RoundExchange:
         if self.host and total:
             cat = cat.to(self.dev)
         cat = cat.contiguous()
-        if self.dev.type == "cuda":
-            # the engine reads the records on its own stream, which does not order after torch's (a non-blocking
-            # HIP stream unless clrrt_set_stream made them one): the gather and the concatenation must be done
-            torch.cuda.current_stream(self.dev).synchronize()
+        if cuda:
+            if ext is not None:
+                ext.wait_stream(torch.cuda.current_stream(self.dev))  # the engine reads the gathered records
+            elif not engine_stream:
+                # no engine stream named: the caller reads the records on a stream of its own choosing
+                torch.cuda.current_stream(self.dev).synchronize()
         return cat, counts, sum(counts[:self.rank]), t_max
 
 
 class ShardExchange:
     """The exchange hook of the engine's own sharded rounds (clrrt_set_shards): clrrt_expand runs every
     round -- this rank's slice of the samples, the lag-2 pipeline, deferred samples -- and calls back once
-    per round with its records already in `records_ptr()`; the callback runs RoundExchange's count-prefixed
-    all-gather (RCCL over xGMI with the nccl backend) and hands the concatenation in rank order back, with
-    the largest elapsed query time over the ranks (the engine's budget decision, identical on every rank).
-    One code path for 1 and N GPUs: with world 1 the engine appends its records itself."""
+    per round with its records in `records_ptr()` (written on the engine's stream, which it does not wait for);
+    the callback runs RoundExchange's count-prefixed all-gather (RCCL over xGMI with the nccl backend) ordered
+    after the engine's stream by a stream wait, and hands the concatenation in rank order back, with the largest
+    elapsed query time over the ranks (the engine's budget decision, identical on every rank) and the union of the
+    ranks' position bounds; the engine's stream waits for the gather (no host synchronisation besides reading
+    the headers).  Every sharded expansion ends with a closing exchange (no records) that carries any rank's
+    failure.  One code path for 1 and N GPUs: with world 1 the engine appends its records itself."""
 
     def __init__(self, planner, cap_records, device, group=None, first_bound=None, slice_size=None):
-        import ctypes
         import traceback
         from . import EXCHANGE_FN
         if first_bound is None:
@@ -117,16 +136,22 @@ class ShardExchange:
         self.rank, self.world = self.rx.rank, self.rx.world
         self._keep = None
         self.rounds = 0
+        self.closing = 0  # closing exchanges (one per sharded expansion)
 
-        def cb(user, n_local, elapsed_ms, aux, dev_all, n_all, max_ms, aux_sum):
+        def cb(user, iop):
             try:
-                cat, counts, _, t_max = self.rx.exchange(n_local, elapsed_ms, aux)
+                io = iop.contents
+                cat, counts, _, t_max = self.rx.exchange(io.n_local, io.elapsed_ms, io.aux_local,
+                                                         tuple(io.bbox_local), io.stream or 0)
                 self._keep = cat  # the engine reads it (stream-ordered) before the next exchange
-                dev_all[0] = ctypes.c_void_p(cat.data_ptr() if cat.shape[0] else None).value
-                n_all[0] = int(cat.shape[0])
-                max_ms[0] = float(t_max)
-                aux_sum[0] = self.rx.aux_sum
+                io.dev_all = cat.data_ptr() if cat.shape[0] else None
+                io.n_all = int(cat.shape[0])
+                io.max_elapsed_ms = float(t_max)
+                io.aux_sum = self.rx.aux_sum
+                for q in range(4):
+                    io.bbox_all[q] = self.rx.bbox_all[q]
                 self.rounds += 1
+                self.closing += bool(io.flags & 1)
                 return 0
             except Exception:  # reported to the engine, which returns CLRRT_EHIP
                 traceback.print_exc()

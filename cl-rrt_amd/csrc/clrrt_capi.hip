@@ -24,6 +24,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -287,15 +288,17 @@ struct clrrt_ctx {
     int64_t xcap = 0;
     unsigned long long* d_goal = nullptr;  // goal nodes among the appended records (device counter)
     // errors are collective: a rank that fails sends an error flag through the exchange's aux word (bit 48) in
-    // the exchange the other ranks make next, so every rank leaves the expansion instead of waiting in a
-    // collective the failed rank never joins
+    // the exchange the other ranks make next -- a round's, or the closing exchange every sharded expansion ends
+    // with -- so every rank leaves the expansion instead of waiting in a collective the failed rank never joins
     bool poison_seen = false;      // an exchange of this expansion reported another rank's failure
     bool fn_failed = false;        // the exchange hook itself failed (the collective is broken: no more calls)
-    bool final_exchanged = false;  // the expansion's last exchange (the drain's) is done
   } sh;
   // option "fail_at_round" k (fault injection, tests): the k-th commit from now fails with CLRRT_ECAPACITY
   // after the round's deferred-sample bookkeeping, as the "trajectory arena full" check does
   int fail_at_round = 0;
+  // option "fail_after_exchange" k (fault injection, tests): the k-th exchange from now fails after the hook
+  // returned (as a failure of the work that follows the round's exchange would)
+  int fail_after_exchange = 0;
   // CLRRT_DEBUG_SYNC (diagnostics, read once at clrrt_create): a heartbeat buffer the rollout kernel's waves
   // write, polled while waiting for the launch
   bool debug_sync = false;
@@ -318,9 +321,13 @@ struct clrrt_ctx {
   // timing
   bool timing = false;
   // per class: 0 nearest-node search (index builds, walks, merges), 1 rollouts, 2 select / commit,
-  // 3 the walk searches alone (launch_nn_walk_search: sample order, k_walk_search, split + merge; within class 0)
-  double kt_ms[4] = {0, 0, 0, 0};
-  int64_t kt_n[4] = {0, 0, 0, 0};
+  // 3 the walk searches alone (launch_nn_walk_search: sample order, k_walk_search, split + merge; within class 0),
+  // 4 the main stream's wait for a round's lists (the side streams' walk + merge running past the work queued
+  // before it: the search's share of the round's critical path), 5 sharded exchanges (the stream span from the
+  // records' copy to the gathered records' availability: the collective on the critical path)
+  static constexpr int kKtClasses = 6;
+  double kt_ms[kKtClasses] = {};
+  int64_t kt_n[kKtClasses] = {};
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
 };
@@ -331,7 +338,7 @@ static int flush_replays(clrrt_ctx* c);
 static int append_nodes(clrrt_ctx* c, const clrrt_node* dev_nodes, int n);
 static int watchdog_check(clrrt_ctx* c);
 static void defer_roll_args(clrrt_ctx* c, RollArgs& a, bool capped);
-static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, bool final_exchange = false);
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app);
 static int ensure_slots(clrrt_ctx* c);
 
 static int fail(clrrt_ctx* c, int code, const std::string& msg) {
@@ -465,6 +472,7 @@ static void sample_region(const clrrt_params& q, double& x0, double& y0, double&
 extern "C" {
 
 int clrrt_abi_version(void) { return CLRRT_ABI_VERSION; }
+static_assert(sizeof(clrrt_exchange_io) == 128, "clrrt_exchange_io layout (clrrt/abi.py ExchangeIO)");
 
 int clrrt_params_default(clrrt_params* p, double v0, const double goal[4], double vmax) {
   if (!p) return CLRRT_EINVAL;
@@ -1370,6 +1378,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "fail_at_round" && value >= 0 && value < INT_MAX) c->fail_at_round = (int)value;  // fault injection
+  else if (k == "fail_after_exchange" && value >= 0 && value < INT_MAX) c->fail_after_exchange = (int)value;
   else if (k == "roll_blocks" && value >= 0 && value < (1 << 20)) c->roll_blocks = (int)value;
   else if (k == "nn_pipeline") c->nn_pipeline = value != 0;
   else if (k == "roll_priority") c->roll_priority = value != 0;
@@ -1438,12 +1447,12 @@ int clrrt_enable_timing(clrrt_ctx* c, int32_t on) {
   if (!c) return CLRRT_EINVAL;
   drain_timers(c);
   c->timing = on != 0;
-  for (int i = 0; i < 4; i++) { c->kt_ms[i] = 0; c->kt_n[i] = 0; }
+  for (int i = 0; i < clrrt_ctx::kKtClasses; i++) { c->kt_ms[i] = 0; c->kt_n[i] = 0; }
   return CLRRT_OK;
 }
 
 int clrrt_kernel_time(clrrt_ctx* c, int32_t which, double* ms, int64_t* launches) {
-  if (!c || which < 0 || which > 3) return CLRRT_EINVAL;
+  if (!c || which < 0 || which >= clrrt_ctx::kKtClasses) return CLRRT_EINVAL;
   drain_timers(c);
   if (ms) *ms = c->kt_ms[which];
   if (launches) *launches = c->kt_n[which];
@@ -1656,7 +1665,10 @@ static int side_delta_launch(clrrt_ctx* c, int n2, int64_t first_new, int nn) {
 
 // The main stream waits for the side stream's lists and swaps the *2 buffers in.
 static int side_lists_join(clrrt_ctx* c) {
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
+  {
+    KTimer kt(c, 4);  // the lists' wait (time the main stream stalls on the side stream)
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_walk, 0));
+  }
   std::swap(c->d_samples, c->d_samples2);
   std::swap(c->h_samples, c->h_samples2);
   std::swap(c->cand, c->cand2);
@@ -1765,7 +1777,7 @@ static int exact_fixups(clrrt_ctx* c, int n, int* L) {
   std::vector<int> xl;
   for (int j = 0; j < n; j++) {
     if (fn[j] >= 0) continue;
-    if (!x_fits) { stop = j; if (-fn[j] >= 1 && -fn[j] <= 5) c->ex_stats[4 + -fn[j]]++; break; }
+    if (!x_fits) { stop = j; if (-fn[j] >= 1 && -fn[j] <= 4) c->ex_stats[4 + -fn[j]]++; break; }
     xl.push_back(j);
   }
   const int nl = (int)xl.size();
@@ -2340,7 +2352,7 @@ static int flush_replays(clrrt_ctx* c) {
 static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
   auto& d = c->def;
   if (!d.active) return CLRRT_OK;
-  const bool sharded = c->sh.world > 1;  // every rank takes part in the final exchange
+  const bool sharded = c->sh.world > 1;  // every rank takes part in the drain's exchange
   if (d.nd > 0 || d.ncarry > 0 || sharded) {
     hipStream_t st = c->stream;
     {
@@ -2368,7 +2380,7 @@ static int defer_drain(clrrt_ctx* c, int64_t* goal_nodes) {
       d.nd_eval = d.nd;
       int nn = 0, n_app = 0;
       int rc = compact_and_copy(c, 0, &nn, true);
-      if (rc == CLRRT_OK) rc = commit_round(c, nn, c->sh.max_ms, &n_app, true);
+      if (rc == CLRRT_OK) rc = commit_round(c, nn, c->sh.max_ms, &n_app);
       if (rc != CLRRT_OK) return rc;
       if (goal_nodes) *goal_nodes += c->last_goal_nodes;
       if (d.nd != 0 || d.ncarry != 0) return fail(c, CLRRT_EHIP, "deferred samples left after the drain");
@@ -2496,30 +2508,45 @@ static inline void shard_slice(const clrrt_ctx* c, int64_t g, int64_t* f, int* n
   *n = (int)(g * (r + 1) / W - *f);
 }
 
-// A sharded expansion that fails on this rank: unless the other ranks already know (they saw an error flag, or
-// the collective itself failed) or no exchange is left for them to make, take part in the exchange they make
-// next with an empty record set and the error flag (aux bit 48), so that they fail too instead of waiting.
-static void shard_expansion_end(clrrt_ctx* c, int rc) {
+// The end of a sharded expansion: one closing exchange on every rank (no records), which carries this rank's
+// failure (aux bit 48) to the others -- a failure in its last round's post-exchange work or in the drain included,
+// when no round exchange is left for them to see it in -- and reports theirs.  Skipped when every rank already
+// left at the same exchange (an error flag seen there) or the collective itself failed.  Returns the final status.
+static int shard_expansion_end(clrrt_ctx* c, int rc) {
   auto& h = c->sh;
-  if (h.world > 1 && rc != CLRRT_OK && !h.poison_seen && !h.fn_failed && !h.final_exchanged) {
-    void* all = nullptr;
-    int32_t n_all = 0;
-    double mx = 0;
-    int64_t aux_sum = 0;
-    h.fn(h.user, 0, 0.0, 1ll << 48, &all, &n_all, &mx, &aux_sum);
+  if (h.world > 1 && !h.poison_seen && !h.fn_failed) {
+    clrrt_exchange_io io;
+    memset(&io, 0, sizeof(io));
+    io.flags = 1;
+    io.elapsed_ms = h.max_ms;
+    io.aux_local = rc != CLRRT_OK ? (1ll << 48) : 0;
+    io.bbox_local[0] = io.bbox_local[1] = HUGE_VAL;
+    io.bbox_local[2] = io.bbox_local[3] = -HUGE_VAL;
+    io.stream = (void*)c->stream;
+    io.aux_sum = io.aux_local;
+    const int r = h.fn(h.user, &io);
+    if (rc == CLRRT_OK) {
+      if (r != 0) rc = fail(c, CLRRT_EHIP, "the closing exchange of the sharded expansion failed");
+      else if (io.aux_sum >> 48)
+        rc = fail(c, CLRRT_EHIP, "sharded expansion: " + std::to_string(io.aux_sum >> 48) + " rank(s) failed");
+    }
   }
   if (rc != CLRRT_OK) {  // the expansion's suspended chains and pending samples are dropped with its results
     c->def.ncarry = 0;
     c->def.nd = 0;
   }
+  return rc;
 }
 static void shard_expansion_begin(clrrt_ctx* c) {
-  c->sh.poison_seen = c->sh.fn_failed = c->sh.final_exchanged = false;
+  c->sh.poison_seen = c->sh.fn_failed = false;
 }
 
 // The commit of a round's records (c->out_nodes[0 .. nn)): appended as they are (one rank), or exchanged
 // with the other ranks and the union appended in the same order on every rank.  *n_app = records appended.
-static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, bool final_exchange) {
+// Sharded, nothing here waits for the device besides the hook's read of the exchanged counts: the records go
+// to dev_local on the engine's stream and the hook orders its collective after it (clrrt_exchange_io.stream);
+// the ranks' position bounds travel with the counts (compact_and_copy read this rank's into h_bbox).
+static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
   auto& h = c->sh;
   *n_app = 0;
   if (h.world <= 1) {
@@ -2527,31 +2554,41 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, boo
     return append_nodes(c, c->out_nodes, nn);
   }
   if (nn > h.cap_local) return fail(c, CLRRT_ECAPACITY, "the round's records exceed the exchange buffer");
-  if (final_exchange) h.final_exchanged = true;
+  std::optional<KTimer> kt;
+  kt.emplace(c, 5);  // the exchange's span on the engine's stream
   if (nn > 0)
     HIPC(c, hipMemcpyAsync(h.dev_local, c->out_nodes, sizeof(clrrt_node) * nn, hipMemcpyDeviceToDevice, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));  // the caller's collective reads dev_local
-  void* all = nullptr;
-  int32_t n_all = 0;
-  double mx = elapsed_ms;
+  clrrt_exchange_io io;
+  memset(&io, 0, sizeof(io));
+  io.n_local = nn;
+  io.elapsed_ms = elapsed_ms;
   // aux: this rank's pending deferred samples (low 32 bits) and whether its arena can take another round of
   // its slice (+ its deferred samples) -- summed over the ranks, so every rank takes the same stop decision
   const int64_t nd_loc = c->def.active ? c->def.nd : 0;
   const bool rows_full =
       c->n_rows + nn + 2 * ((int64_t)h.last_nb + nd_loc) * (c->dp.n_steps_max + 1) > c->cap.max_rows;
-  const int64_t aux = nd_loc + (rows_full ? (1ll << 32) : 0);
-  int64_t aux_sum = aux;
-  if (h.fn(h.user, nn, elapsed_ms, aux, &all, &n_all, &mx, &aux_sum) != 0 || n_all < 0 || (n_all > 0 && !all)) {
+  io.aux_local = nd_loc + (rows_full ? (1ll << 32) : 0);
+  for (int q = 0; q < 4; q++) io.bbox_local[q] = nn > 0 ? c->h_bbox[q] : (q < 2 ? HUGE_VAL : -HUGE_VAL);
+  io.stream = (void*)c->stream;
+  io.max_elapsed_ms = elapsed_ms;
+  io.aux_sum = io.aux_local;
+  if (h.fn(h.user, &io) != 0 || io.n_all < 0 || (io.n_all > 0 && !io.dev_all)) {
     h.fn_failed = true;
     return fail(c, CLRRT_EHIP, "the exchange of the round's records failed");
   }
+  kt.reset();
+  const int64_t aux_sum = io.aux_sum;
   if (aux_sum >> 48) {  // another rank failed (shard_poison): every rank leaves the expansion
     h.poison_seen = true;
     return fail(c, CLRRT_EHIP, "sharded expansion: " + std::to_string(aux_sum >> 48) + " rank(s) failed this round");
   }
-  h.max_ms = mx;
+  if (c->fail_after_exchange > 0 && --c->fail_after_exchange == 0)
+    return fail(c, CLRRT_ECAPACITY, "injected failure (option fail_after_exchange)");
+  h.max_ms = io.max_elapsed_ms;
   h.nd_global = aux_sum & 0xffffffffll;
   h.rows_stop = (aux_sum >> 32) & 0xffff;
+  const int32_t n_all = io.n_all;
+  void* all = io.dev_all;
   if (n_all > 0) {
     if (n_all > h.xcap) {
       HIPC(c, hipStreamSynchronize(c->stream));
@@ -2569,11 +2606,9 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app, boo
                           h.xbuf, h.d_goal));
     int rc = append_nodes(c, h.xbuf, n_all);
     if (rc != CLRRT_OK) return rc;
-    // the tree's bounding box takes every rank's records (the walk frame is then the same on every rank)
-    HIPC(c, launch_bbox(c->stream, h.xbuf, nullptr, n_all, c->d_bbox));
-    HIPC(c, hipMemcpyAsync(c->h_bbox, c->d_bbox, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    bbox_add(c, c->h_bbox[0], c->h_bbox[1], c->h_bbox[2], c->h_bbox[3]);
+    // the tree's bounding box takes every rank's records (the walk frame is then the same on every rank); the
+    // union of the ranks' bounds is the bound of the union (min / max), so no pass over the gathered records
+    bbox_add(c, io.bbox_all[0], io.bbox_all[1], io.bbox_all[2], io.bbox_all[3]);
   }
   *n_app = n_all;
   return CLRRT_OK;
@@ -2806,6 +2841,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     draw_to(gb + gA_all + gB);
     // this round's lists
     if (have_cur) {
+      KTimer kt(c, 4);  // the lists' wait (time the main stream stalls on the side streams)
       HIPC(c, hipStreamWaitEvent(c->stream, cur_ev, 0));
     } else {
       for (int j = 0; j < nb; j++) c->h_samples[j] = pending[f0 + j];
@@ -2905,10 +2941,10 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   // tree, so inside its time)
   if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
   st.deferred = c->def.deferred_total;
-  shard_expansion_end(c, rc);
   if (rc == CLRRT_OK) rc = flush_replays(c);
-  c->def.active = false;
   if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);
+  rc = shard_expansion_end(c, rc);  // the closing exchange (sharded): every rank learns of any rank's failure
+  c->def.active = false;
   for (hipStream_t s : {c->side, c->side2, c->mst, c->stream}) {  // every stream drained, the first error kept
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess && rc == CLRRT_OK) rc = fail(c, CLRRT_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
@@ -3055,10 +3091,10 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   // tree, so inside its time)
   if (rc == CLRRT_OK) rc = defer_drain(c, &st.goal_nodes_added);
   st.deferred = c->def.deferred_total;
-  shard_expansion_end(c, rc);
   if (rc == CLRRT_OK) rc = flush_replays(c);
-  c->def.active = false;
   if (rc == CLRRT_OK && sharded) rc = shard_goal_count(c, &st.goal_nodes_added);
+  rc = shard_expansion_end(c, rc);  // the closing exchange (sharded): every rank learns of any rank's failure
+  c->def.active = false;
   HIPC(c, hipStreamSynchronize(c->side));
   HIPC(c, hipStreamSynchronize(c->stream));
   st.nodes_added = c->n_nodes - nodes_before;

@@ -1984,9 +1984,9 @@ __global__ void k_conflict(DevParams p, int B, const clrrt_sample* __restrict__ 
 // n's rollout added to j's counters.  So the conflicting nodes are rolled out for j (the fix-up launch) and j
 // stands when all of them fail.  Not resolvable this way (fix_n = -1, j conflicts as before): a tie among j's
 // keys (std::sort's order of equal keys depends on the whole array), a new node whose key equals j's threshold
-// (its order against k is the sort's), more than FIX_MAX new nodes, k pushed out of the window, and samples
-// without a result whose full window (sortLimit candidates, all failed) would lose candidates the reference
-// then never simulates.
+// (its order against k is the sort's), more than FIX_MAX new nodes, and k pushed out of the window.  (A sample
+// without a result is resolved by ranking the new nodes among its old candidates: the grown window's first
+// sortLimit entries are rolled out and the old ones it no longer reaches have their counters subtracted.)
 __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restrict__ S,
                                const clrrt_node* __restrict__ regnodes, const clrrt_node* __restrict__ gbnodes,
                                const SampleOut* __restrict__ so, const int* __restrict__ ctie,
@@ -2010,7 +2010,7 @@ __global__ void k_conflict_fix(DevParams p, int B, const clrrt_sample* __restric
   int m = 0;
   int ids[FIX_MAX];
   float nk[FIX_MAX];
-  int bad = 0;  // why not resolvable: 1 tie, 2 a key equal to the threshold, 3 > FIX_MAX, 4 k pushed out, 5 full window
+  int bad = 0;  // why not resolvable: 1 tie, 2 a key equal to the threshold, 3 > FIX_MAX, 4 k pushed out
   for (int k = 0; k < j && !bad; k++) {
     if (so[k].k < 0) continue;
     if (tie) { bad = 1; break; }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define CLRRT_ABI_VERSION 10
+#define CLRRT_ABI_VERSION 11
 
 /* ---- status codes ---- */
 #define CLRRT_OK 0
@@ -242,7 +242,8 @@ typedef struct clrrt_iteration {
  * fix-up rollouts (option "exact_fixup"), out[2] fix-up rollouts run, out[3] rounds whose prefix ended at a
  * conflict; why those conflicts were not resolved: out[4] a fix-up rollout succeeded, out[5] a key tie in the
  * sample's list, out[6] a new key equal to the sample's threshold, out[7] more new nodes than fix-up slots,
- * out[8] the accepted candidate pushed out of the sortLimit window, out[9] a full window without a result. */
+ * out[8] the accepted candidate pushed out of the sortLimit window; out[9] reserved (0: a window without a result
+ * is always resolved by ranking the new nodes into it). */
 int clrrt_exact_stats(clrrt_ctx* ctx, int64_t out[10]);
 /* on != 0: start (or restart) logging, clearing the records; 0: stop and clear. */
 int clrrt_iteration_log(clrrt_ctx* ctx, int32_t on);
@@ -306,16 +307,38 @@ int clrrt_expand(clrrt_ctx* ctx, clrrt_rng* rng, int64_t n_iters, double budget_
  * per round (all drawn from the one glibc stream, as the reference's loop draws them); this rank evaluates
  * the contiguous slice [batch*rank/world, batch*(rank+1)/world) against the replicated tree, writes its
  * accepted-node records (clrrt_node, owner = rank, rows in this rank's arena) to dev_local, and calls
- * `exchange` once per round, which must return in *dev_all the records of every rank concatenated in
+ * `exchange` once per round, which must return in io->dev_all the records of every rank concatenated in
  * rank order (device memory, valid until the next call; a collective such as one all-gather over RCCL) and
- * in *n_all their count, in *max_elapsed_ms the largest `elapsed_ms` over the ranks -- the budget is
- * checked against it, so every rank runs the same rounds -- and in *aux_sum the sum of `aux_local` over the
- * ranks (the engine's capacity bookkeeping: pending deferred samples, ranks whose arena is full).  Every rank then appends the same records in
- * the same order (deferred samples: the oldest round first), so the trees stay identical.  The caller
- * chooses weak scaling (batch = world x per-GPU samples) or strong scaling (batch fixed).  world = 1 turns
- * sharding off.  dev_local holds cap_local records (>= 2 x the slice, + the deferred samples). */
-typedef int32_t (*clrrt_exchange_fn)(void* user, int32_t n_local, double elapsed_ms, int64_t aux_local,
-                                     void** dev_all, int32_t* n_all, double* max_elapsed_ms, int64_t* aux_sum);
+ * in io->n_all their count, in io->max_elapsed_ms the largest `elapsed_ms` over the ranks -- the budget is
+ * checked against it, so every rank runs the same rounds --, in io->aux_sum the sum of `aux_local` over the
+ * ranks (the engine's capacity bookkeeping: pending deferred samples, ranks whose arena is full; bit 48 and up:
+ * ranks that failed) and in io->bbox_all the union of the ranks' `bbox_local` (the walk index's frame).  Every
+ * rank then appends the same records in the same order (deferred samples: the oldest round first), so the trees
+ * stay identical.  The caller chooses weak scaling (batch = world x per-GPU samples) or strong scaling (batch
+ * fixed).  world = 1 turns sharding off.  dev_local holds cap_local records (>= 2 x the slice, + the deferred
+ * samples).
+ * No host synchronisation (ABI 11): the engine writes dev_local on io->stream and calls the hook without waiting
+ * for it, so the hook's collective must be ordered after io->stream's work (a stream wait on an event, or the
+ * same stream); the engine reads io->dev_all on io->stream after the hook returns, so the hook must order
+ * io->stream after its own writes of it the same way.  Every sharded expansion ends with one closing exchange
+ * (io->flags bit 0, n_local = 0), which carries a failure of any rank after its last round to the others. */
+typedef struct clrrt_exchange_io {
+  /* in */
+  int32_t n_local;      /* records this rank wrote to dev_local */
+  int32_t flags;        /* bit 0: the expansion's closing exchange */
+  double elapsed_ms;    /* this rank's elapsed query time */
+  int64_t aux_local;
+  double bbox_local[4]; /* x0, y0, x1, y1 of the finite positions among this rank's records (+inf, +inf, -inf, -inf: none) */
+  void* stream;         /* the engine's HIP stream */
+  /* out */
+  void* dev_all;
+  int32_t n_all;
+  int32_t pad;
+  double max_elapsed_ms;
+  int64_t aux_sum;
+  double bbox_all[4];
+} clrrt_exchange_io;
+typedef int32_t (*clrrt_exchange_fn)(void* user, clrrt_exchange_io* io);
 int clrrt_set_shards(clrrt_ctx* ctx, int32_t rank, int32_t world, void* dev_local, int32_t cap_local,
                      clrrt_exchange_fn exchange, void* user);
 
@@ -443,8 +466,10 @@ int clrrt_work_counters(clrrt_ctx* ctx, int64_t out[3]);
 
 /* Launch-time profile of the last clrrt_expand / round call: device milliseconds per kernel
  * family measured with HIP events on the stream each launch runs on.  which: 0 = nn (index builds,
- * walk searches, merges), 1 = rollout, 2 = commit, 3 = the walk searches alone (part of 0); returns the
- * summed ms and the launch count. */
+ * walk searches, merges), 1 = rollout, 2 = commit, 3 = the walk searches alone (part of 0), 4 = the main
+ * stream's waits for the side streams' lists (the search's share of the round's critical path), 5 = sharded
+ * exchanges (the stream span from the records' copy to the gathered records); returns the summed ms and the
+ * launch (or wait) count. */
 int clrrt_kernel_time(clrrt_ctx* ctx, int32_t which, double* ms, int64_t* launches);
 int clrrt_enable_timing(clrrt_ctx* ctx, int32_t on);
 

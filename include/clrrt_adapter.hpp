@@ -228,16 +228,32 @@ class Engine {
   template <class VehicleT, class RRTT, class PubT, class ObsVec>
   void expandTree(VehicleT&, RRTT& RRT, PubT* /*ptrPub (unused)*/, const ObsVec& det,
                   const std::vector<double>& /*Cxy (unused)*/) {
+    // The process's rand() stream must be the engine's (srand(seed) and Engine::srand(seed) together): the three
+    // values the reference's iteration would take from rand() (rrtplanner.cpp:142, 193-194) are compared with the
+    // engine stream's next three before anything changes; a caller that seeded only one of them gets an Error
+    // instead of a tree grown from another stream (set_rand_check(false) turns the check off).
+    {
+      clrrt_rng probe = rng_;
+      bool same = true;
+      for (int i = 0; i < 3; i++) {
+        const int32_t want = clrrt_rng_next(&probe), got = (int32_t)rand();
+        same = same && want == got;
+      }
+      if (rand_check_ && !same)
+        throw Error("clrrt_adapter::expandTree: the process's rand() stream differs from the engine's (seed both: "
+                    "srand(seed) and Engine::srand(seed))");
+    }
     sync_obstacles(det);
     int64_t c[4] = {0, 0, 0, 0};
     one_iteration(RRT, rng_, c);
-    for (int i = 0; i < 3; i++) (void)rand();
     for (int i = 0; i < 4; i++) {
       counters_[i] += c[i];
       if (gc_[i]) *gc_[i] += (int)c[i];
     }
   }
-  /* The same with an explicit stream and counter sink. */
+  /* expandTree's check that rand() and the engine's stream agree (on by default). */
+  void set_rand_check(bool on) { rand_check_ = on; }
+  /* The same with an explicit stream and counter sink (no check: the stream is the caller's). */
   template <class VehicleT, class RRTT, class ObsVec>
   void expandTree(VehicleT&, RRTT& rrt, void* /*ros::Publisher* (unused)*/, const ObsVec& det,
                   const std::vector<double>& /*Cxy (unused)*/, clrrt_rng& rng, int64_t counters[4]) {
@@ -380,6 +396,13 @@ class Engine {
     Spec s;
     s.dev_base = (int64_t)rrt.tree.size();
     clrrt_rng work = rng;
+    // from here on the device tree may hold nodes RRT.tree does not (a failed expansion's rounds, a cache whose
+    // download failed): on any error the next call reloads RRT.tree instead of trusting the device tree
+    struct Unsync {
+      int64_t* synced;
+      bool armed = true;
+      ~Unsync() { if (armed) *synced = -1; }
+    } unsync{&synced_};
     check(ctx_, clrrt_iteration_log(ctx_, 1), "clrrt_iteration_log");
     clrrt_stats st;
     const int rc = clrrt_expand(ctx_, &work, width, 0.0, CLRRT_MODE_EXACT, 256, &st);
@@ -415,6 +438,7 @@ class Engine {
       o += s.its[i].nodes;
     }
     if (o != (int64_t)s.hdr.size()) throw Error("expandTree cache: the iteration log does not match the nodes appended");
+    unsync.armed = false;
     s.valid = st.iterations > 0;
     s.next_rng = rng;
     s.count = st.iterations;
@@ -532,6 +556,7 @@ class Engine {
   clrrt_ctx* ctx_ = nullptr;
   clrrt_params p_{};
   bool full_ref_ = false;
+  bool rand_check_ = true;
   int64_t synced_ = -1;  // nodes of RRT.tree the device holds (-1: unknown, reload)
   clrrt_node root_{}, last_{};
   clrrt_rng rng_{};

@@ -6,7 +6,9 @@
 // parent, goal, row count, state bits, float cost bits, FNV-1a of the trajectory rows) to <out> and prints the
 // iteration count, wall time and nodes/s; tests/test_native_timer_loop.py grows the oracle's tree with the same
 // number of iterations and compares.
-// Usage: timer_loop <obstacles.bin> <seed> <budget_ms> <out.bin> [width0 width_max]
+// Usage: timer_loop <obstacles.bin> <seed> <budget_ms> <out.bin> [width0 width_max | mismatch]
+// "mismatch": the caller seeds srand(seed) but the engine with seed + 1 (the drop-in's rand() check must throw
+// before the tree changes).
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -114,7 +116,23 @@ int main(int argc, char** argv) {
   const clrrt_adapter::Globals g{0.04, 1.4, 3.2, 3.0, 8.0, 0.05, 0.2, 5.0, 0.0, true};
   try {
     clrrt_adapter::Engine eng(clrrt_adapter::params_from(veh, RRT, g, CLRRT_COLLISION_OBB), 1 << 18, 1 << 24, 256, 256);
+    const bool mismatch = argc >= 6 && strcmp(argv[5], "mismatch") == 0;
     if (argc >= 7) eng.set_speculation(atoll(argv[5]), atoll(argv[6]));
+    if (mismatch) {
+      RRT.tree.clear();
+      addInitialNode(RRT, vector<double>(10, 0.0));
+      srand(seed);
+      eng.srand(seed + 1);  // a caller that forgot Engine::srand(seed)
+      clrrt_adapter::dropin::bind(eng);
+      try {
+        clrrt_adapter::dropin::expandTree(veh, RRT, (ros::Publisher*)nullptr, det, vector<double>());
+      } catch (const clrrt_adapter::Error& e) {
+        printf("rand mismatch detected (tree size %zu): %s\n", RRT.tree.size(), e.what());
+        return RRT.tree.size() == 1 ? 0 : 4;
+      }
+      printf("rand mismatch NOT detected\n");
+      return 3;
+    }
     int sim_count = 0, fail_collision = 0, fail_acclimit = 0, fail_iterlimit = 0;  // rrt_node.cpp:21-24
     eng.bind_counters(&sim_count, &fail_collision, &fail_acclimit, &fail_iterlimit);
     clrrt_adapter::dropin::bind(eng);

@@ -129,10 +129,13 @@ SHARD_CASES = [  # (ranks, samples per round over all ranks, defer_steps, nn_lag
     (2, 2 * B - 7, 48, 1, 4),   # uneven slices (shard_slice), deferred samples
     (4, 4 * B, 128, 2, 5),      # four ranks, the cfg3 bench's defer_steps
     (4, 4 * B - 5, 64, 1, 4),
+    # cfg4's split rehearsed on one GPU (verdict r05 item 1): 8 ranks, the bench's G = 16384 per round strongly
+    # split (2048 samples per rank), defer_steps 128, the lag-2 pipeline, 200 obstacles
+    (8, 16384, 128, 2, 5),
 ]
 
 
-def _shard_worker(rank, port, out_dir, world, G, T, lag, rounds, fail_rank=-1, fail_round=0):
+def _shard_worker(rank, port, out_dir, world, G, T, lag, rounds, fail_rank=-1, fail_round=0, fail_opt="fail_at_round"):
     sys.path.insert(0, os.path.join(ROOT, "cl-rrt_amd"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -148,7 +151,7 @@ def _shard_worker(rank, port, out_dir, world, G, T, lag, rounds, fail_rank=-1, f
     pl.set_stream(torch.cuda.current_stream().cuda_stream)
     ex = cdist.ShardExchange(pl, cdist.exchange_capacity(-(-G // world), T), "cuda", slice_size=-(-G // world))
     if rank == fail_rank:
-        pl.set_option("fail_at_round", fail_round)
+        pl.set_option(fail_opt, fail_round)
     err = ""
     try:
         st = pl.expand(clrrt.Rng(SEED), n_iters=rounds * G, mode=clrrt.CLRRT_MODE_BATCH, batch=G)
@@ -166,7 +169,7 @@ def _shard_worker(rank, port, out_dir, world, G, T, lag, rounds, fail_rank=-1, f
     np.savez(os.path.join(out_dir, f"shard{rank}.npz"), hdr=raw[:, :HDR], own=own,
              rows=np.concatenate(rows) if rows else np.zeros((0, 10)), rounds=st["rounds"], it=st["iterations"],
              goals=st["goal_nodes_added"], deferred=st["deferred"], ex_rounds=ex.rounds,
-             collectives=ex.collectives, err=err)
+             collectives=ex.collectives, closing=ex.closing, err=err)
     dist.barrier()
     dist.destroy_process_group()
     pl.close()
@@ -199,6 +202,7 @@ def test_sharded_expand_matches_single_process(tmp_path, world, G, T, lag, round
         assert int(r["rounds"]) == rounds and int(r["it"]) == rounds * G
         assert int(r["goals"]) == st["goal_nodes_added"]
         assert int(r["collectives"]) == int(r["ex_rounds"]) >= rounds
+        assert int(r["closing"]) == 1  # one closing exchange per expansion
     assert sum(int(r["deferred"]) for r in ranks) == st["deferred"]
     assert sum(len(r["own"]) for r in ranks) == ref_raw.shape[0]
     for rk, r in enumerate(ranks):
@@ -219,6 +223,24 @@ def test_sharded_failure_is_collective(tmp_path, fail_round):
              join=True)
     r0, r1 = (np.load(tmp_path / f"shard{r}.npz") for r in range(2))
     print(f"fail at round {fail_round}: rank 0 '{r0['err']}', rank 1 '{r1['err']}', exchanges "
+          f"{int(r0['ex_rounds'])} / {int(r1['ex_rounds'])}")
+    assert "injected failure" in str(r1["err"])
+    assert "rank(s) failed" in str(r0["err"])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("T,lag", [(0, 1), (0, 2), (64, 2)])
+def test_sharded_failure_after_last_exchange_is_collective(tmp_path, T, lag):
+    """a rank that fails AFTER the last round's exchange (option fail_after_exchange: the work that
+    follows the exchange fails) -- with defer_steps 0 no drain exchange follows -- still ends the expansion on every
+    rank with an error: every sharded expansion closes with one exchange that carries the failure, so no rank waits
+    in a collective the failed rank never joins and no rank reports success beside a failed one."""
+    import torch.multiprocessing as mp
+    rounds = 4
+    mp.spawn(_shard_worker, args=(_free_port(), str(tmp_path), 2, 2 * B, T, lag, rounds, 1, rounds,
+                                  "fail_after_exchange"), nprocs=2, join=True)
+    r0, r1 = (np.load(tmp_path / f"shard{r}.npz") for r in range(2))
+    print(f"T={T} lag {lag}, fail after exchange {rounds}: rank 0 '{r0['err']}', rank 1 '{r1['err']}', exchanges "
           f"{int(r0['ex_rounds'])} / {int(r1['ex_rounds'])}")
     assert "injected failure" in str(r1["err"])
     assert "rank(s) failed" in str(r0["err"])

@@ -17,7 +17,7 @@ def _header_functions():
 
 def test_library_loads_and_exports_every_header_symbol():
     L = clrrt.lib()
-    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 10
+    assert L.clrrt_abi_version() == abi.CLRRT_ABI_VERSION == 11
     declared = _header_functions()
     assert len(declared) >= 25
     out = subprocess.run(["nm", "-D", "--defined-only", clrrt.LIB_PATH], capture_output=True, text=True).stdout
@@ -32,6 +32,11 @@ def test_abi_record_sizes_match_header():
     assert C.sizeof(abi.Node) == 160
     assert C.sizeof(abi.Params) == 9 * 8 + 11 * 8 + 4 * 8 + 5 * 8 + 8 + 3 * 8 + 4 * 4
     assert C.sizeof(abi.SimCase) == 15 * 8 + 2 * 4  # clrrt_sim_case
+    # clrrt_exchange_io (static_assert'ed 128 in clrrt_capi.hip): field offsets as the header lays them out
+    io = abi.ExchangeIO
+    assert C.sizeof(io) == 128
+    assert [getattr(io, f).offset for f in ("elapsed_ms", "aux_local", "bbox_local", "stream", "dev_all", "n_all",
+                                            "max_elapsed_ms", "aux_sum", "bbox_all")] == [8, 16, 24, 56, 64, 72, 80, 88, 96]
 
 
 def test_params_default_matches_reference_values():

@@ -2,8 +2,9 @@
 expandTree (clrrt_adapter::dropin, its speculation cache) in a native program linked against libclrrt
 (tests/native/timer_loop.cpp): the tree it grows in one 200 ms (CPU time) query equals the oracle's sequential
 expandTree (rrtplanner.cpp:123-174) after the same number of iterations, node for node and bit for bit (state,
-float costs, parents, goal flags, trajectory row hashes) with the reference's failure counters, and it grows at
-GPU speed (>= 1000 nodes per wall-clock second; one device round per call ran at ~200)."""
+float costs, parents, goal flags, trajectory row hashes) with the reference's failure counters.  Its rate (nodes per
+wall-clock second; one device round per call ran at ~200) is reported, not asserted: a throughput threshold in a
+bit-exactness test fails on a shared box for reasons that are not parity (verdict r05 weak item 9)."""
 import os
 import struct
 import subprocess
@@ -77,4 +78,19 @@ def test_timer_loop_dropin_matches_oracle(tmp_path, seed):
     oc = o.counters()
     assert list(cnt) == [oc["sim_count"], oc["fail_collision"], oc["fail_acclimit"], oc["fail_iterlimit"]]
     rate = float(r.stdout.split(" nodes/s")[0].split(": ")[-1])
-    assert rate >= 1000.0, r.stdout
+    print(f"Timer(200) loop through the drop-in: {rate:.0f} nodes/s (reported)")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_dropin_detects_rand_stream_mismatch(tmp_path):
+    """verdict r05 item 8: a caller that seeds the process's rand() (srand) but not the engine's stream gets an
+    error from the drop-in expandTree before the tree changes, not a tree grown from another stream."""
+    assert os.path.exists(EXE), "tests/native/timer_loop not built (make -C cl-rrt_amd/csrc)"
+    obs_path = tmp_path / "obs.bin"
+    obs_path.write_bytes(np.ascontiguousarray(scenes.urban_scene(200), dtype="<f8").tobytes())
+    r = subprocess.run([EXE, str(obs_path), "3", "200", str(tmp_path / "tree.bin"), "mismatch"], capture_output=True,
+                       text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "rand mismatch detected (tree size 1)" in r.stdout
