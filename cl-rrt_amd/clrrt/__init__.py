@@ -77,6 +77,8 @@ _SIGS = {
     "clrrt_nn_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work": (C.c_int, [C.c_void_p, P(C.c_int64)]),
     "clrrt_search_work_ex": (C.c_int, [C.c_void_p, P(C.c_int64)]),
+    "clrrt_walk_audit": (C.c_int, [C.c_void_p, P(abi.Sample), C.c_int32, P(C.c_int32)]),
+    "clrrt_round_sizes": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64)]),
     "clrrt_tree_truncate": (C.c_int, [C.c_void_p, C.c_int64]),
     "clrrt_iteration_log": (C.c_int, [C.c_void_p, C.c_int32]),
     "clrrt_exact_stats": (C.c_int, [C.c_void_p, P(C.c_int64)]),
@@ -475,6 +477,25 @@ class Planner:
         self._chk(self.L.clrrt_iteration_records(self.h, 0, n.value, arr, C.byref(n)), "iteration_records")
         return {f: np.array([getattr(arr[i], f) for i in range(n.value)], dtype=np.int64)
                 for f, _ in abi.Iteration._fields_}
+
+    def round_sizes(self):
+        """clrrt_round_sizes: the tree size after each commit of the last expand (rounds, then the drain)."""
+        n = C.c_int64()
+        self._chk(self.L.clrrt_round_sizes(self.h, None, 0, C.byref(n)), "round_sizes")
+        out = np.zeros(max(1, n.value), dtype=np.int64)
+        self._chk(self.L.clrrt_round_sizes(self.h, out.ctypes.data_as(P(C.c_int64)), n.value, C.byref(n)), "round_sizes")
+        return out[:n.value]
+
+    def walk_audit(self, samples):
+        """clrrt_walk_audit (diagnostics): per sample (n, 12) int32 -- tiles with bound <= the true 11th key kth,
+        those holding a list member, feasible records with key <= kth, records past the stage-1 bound at kth,
+        super-tiles with bound <= kth, explore flag, kth bits, records of the admissible tiles, of which
+        infeasible / farther than kth / within kth but key > kth, admissible tiles holding a record with key <= kth."""
+        n = len(samples)
+        arr = (abi.Sample * n)(*samples)
+        out = np.zeros((n, 12), dtype=np.int32)
+        self._chk(self.L.clrrt_walk_audit(self.h, arr, n, out.ctypes.data_as(P(C.c_int32))), "walk_audit")
+        return out
 
     def search_work_ex(self):
         """search_work + the walk's bound work: phase-1 super-tile bounds, super-tile visits (32 tile bounds

@@ -94,6 +94,7 @@ struct clrrt_ctx {
   clrrt_node* out_nodes = nullptr;
   Job* jobs = nullptr;
   int64_t* totals = nullptr;
+  bool totals_zeroed = false;  // the round's prologue fill reset totals (launch_compact skips its own fill)
   unsigned long long* work_ctr = nullptr;  // [3] algorithmic rollout work; [8..15] nn search statistics
   // spatial index of the tree (nearest-node search)
   float* nn_seed = nullptr;  // [max_batch] the brute-force chunks' shared per-sample key caps
@@ -305,6 +306,9 @@ struct clrrt_ctx {
   unsigned long long* dbg_host = nullptr;
   // clrrt_iteration_log: one record per committed iteration (EXACT / non-deferred BATCH rounds)
   bool iter_log = false;
+  // the tree size after each commit of the last clrrt_expand (its rounds, then the drain of deferred samples when it
+  // appended anything): clrrt_round_sizes
+  std::vector<int64_t> round_sizes;
   std::vector<clrrt_iteration> iters;
   std::vector<SampleOut> iter_tmp;
   // host staging (pinned)
@@ -2020,7 +2024,19 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
       HIPC(c, hipStreamSynchronize(rst));
       fprintf(stderr, "[dbg] pre-rollout work done (n %d, nrep %d, ncarry %d)\n", n, a.nrep, a.ncarry);
     }
-    if (persistent)
+    if (persistent && defer) {
+      // the round's resets in one launch: the rollout queue / carry counters and the first-success array, the
+      // count of this round's samples left pending (k_select) and the compaction's totals (launch_compact)
+      FillInts f;
+      f.add(a.ncarry_out, 1, 0);
+      f.add(c->roll_q, 1, 0);
+      f.add(c->def.best + a.sbase, n, 0x7f7f7f7f);
+      f.add(c->def.d_cnt + 2, 1, 0);
+      f.add((int*)c->totals, 16, 0);
+      HIPC(c, launch_fill_ints(rst, f));
+      c->totals_zeroed = true;
+      HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, c->def.best, blocks, true));
+    } else if (persistent)
       HIPC(c, launch_rollout_persistent(rst, a, n, c->roll_q, defer ? c->def.best : c->roll_best, blocks));
     else
       HIPC(c, launch_rollout(rst, SRC_SPEC, a));
@@ -2076,8 +2092,7 @@ static int eval_samples(clrrt_ctx* c, int n, bool exact, int* L_out, bool have_l
     s.gv = d.gv;
     s.pend = d.pend;
     s.new_pend = d.d_cnt + 2;
-    s.B = d.nd + n;
-    HIPC(c, hipMemsetAsync(d.d_cnt + 2, 0, sizeof(int), st));
+    s.B = d.nd + n;  // (d_cnt[2] was reset by the round's prologue fill before the rollouts)
   }
   c->def.nd_eval = defer ? c->def.nd : -1;
   {
@@ -2116,7 +2131,8 @@ static int compact_and_copy(clrrt_ctx* c, int L, int* n_out, bool merge_bbox) {
     const bool tag = defer && c->sh.world > 1;  // the exchange orders deferred samples by age
     HIPC(c, launch_compact(st, V, c->d_samples, c->cand, c->regnodes, c->gbnodes, c->so, c->n_rows, c->rank,
                            c->out_nodes, c->jobs, c->totals, c->cmp, tag ? d.slot : 0, tag ? d.R : 0,
-                           (int)c->cap.max_batch));
+                           (int)c->cap.max_batch, c->totals_zeroed));
+    c->totals_zeroed = false;
     if (merge_bbox) HIPC(c, launch_bbox(st, c->out_nodes, c->totals, 0, c->d_bbox));
     // the views still pending, in view order: the next commit's deferred samples
     if (defer) HIPC(c, launch_defer_select(st, d.gv, d.pend, V, d.dlist[1 - d.cur_dl], d.d_cnt, d.sel_tmp, d.sel_bytes));
@@ -2551,7 +2567,9 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
   *n_app = 0;
   if (h.world <= 1) {
     *n_app = nn;
-    return append_nodes(c, c->out_nodes, nn);
+    const int rc = append_nodes(c, c->out_nodes, nn);
+    if (rc == CLRRT_OK) c->round_sizes.push_back(c->n_nodes);
+    return rc;
   }
   if (nn > h.cap_local) return fail(c, CLRRT_ECAPACITY, "the round's records exceed the exchange buffer");
   std::optional<KTimer> kt;
@@ -2611,6 +2629,7 @@ static int commit_round(clrrt_ctx* c, int nn, double elapsed_ms, int* n_app) {
     bbox_add(c, io.bbox_all[0], io.bbox_all[1], io.bbox_all[2], io.bbox_all[3]);
   }
   *n_app = n_all;
+  c->round_sizes.push_back(c->n_nodes);
   return CLRRT_OK;
 }
 
@@ -2962,6 +2981,7 @@ int clrrt_expand(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double budget_ms
   pf_reset(c);
   if (n_iters == 0 && !(budget_ms > 0)) return CLRRT_EINVAL;
   if (c->n_nodes <= 0) return fail(c, CLRRT_ESTATE, "tree not initialised");
+  c->round_sizes.clear();
   const bool sharded = c->sh.world > 1;
   if (sharded && mode != CLRRT_MODE_BATCH) return fail(c, CLRRT_EINVAL, "sharded expansion runs BATCH rounds only");
   HIPC(c, hipSetDevice(c->device));
@@ -3350,6 +3370,38 @@ int clrrt_nn_batch(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t
   if (out_keys)
     HIPC(c, hipMemcpyAsync(out_keys, c->ckey, sizeof(float) * CAND_K * n, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  return CLRRT_OK;
+}
+
+int clrrt_round_sizes(clrrt_ctx* c, int64_t* out, int64_t cap, int64_t* n) {
+  if (!c || cap < 0 || (cap > 0 && !out)) return CLRRT_EINVAL;
+  const int64_t m = (int64_t)c->round_sizes.size();
+  for (int64_t i = 0; i < std::min(m, cap); i++) out[i] = c->round_sizes[(size_t)i];
+  if (n) *n = m;
+  return CLRRT_OK;
+}
+
+int clrrt_walk_audit(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32_t* out) {
+  if (!c || n < 0 || (n > 0 && (!samples || !out))) return CLRRT_EINVAL;
+  pf_reset(c);
+  if (n > c->cap.max_batch) return fail(c, CLRRT_ECAPACITY, "batch larger than max_batch");
+  HIPC(c, hipSetDevice(c->device));
+  if (n == 0) return CLRRT_OK;
+  const NnSetup su = nn_setup(c);
+  if (!walk_serves(c, su)) return fail(c, CLRRT_ESTATE, "the walk does not serve this tree (too small or no region)");
+  int rc = ensure_walk(c);
+  if (rc != CLRRT_OK) return rc;
+  memcpy(c->h_samples, samples, sizeof(clrrt_sample) * n);
+  HIPC(c, hipMemcpyAsync(c->d_samples, c->h_samples, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, c->stream));
+  c->nnw_built.n = -1;
+  HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw));
+  int* d_out = nullptr;
+  HIPC(c, hipMalloc(&d_out, sizeof(int32_t) * 12 * (size_t)n));
+  hipError_t e = launch_walk_audit(c->stream, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, su.fr, c->nnw, d_out);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(int32_t) * 12 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d_out);
+  if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("clrrt_walk_audit: ") + hipGetErrorString(e));
   return CLRRT_OK;
 }
 

@@ -240,6 +240,9 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
                                  const DevParams& p, const NnFrame& fr, double x0, double y0, double x1, double y1,
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
                                  bool stateless);
+// Diagnostics: per sample, the tiles / records any search over the index in w must touch (k_walk_audit)
+hipError_t launch_walk_audit(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
+                             const NnFrame& fr, const WalkBufs& w, int* out);
 // Pipelined BATCH rounds: merges into (cand, ckey, ncand) -- the lists over nodes [0, first) -- the
 // nodes [first, first + count) appended since (k_nn_partial over them + k_nn_merge_delta).
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
@@ -263,7 +266,20 @@ hipError_t launch_nn_exact_small(hipStream_t st, const clrrt_sample* S, int B, c
 int nn_exact_small_max();
 // Round rollouts (and the pending replays a.rep[0..nrep)) as the persistent k_roll_run, behind k_roll_flag +
 // k_roll_order when a.perm / a.pflag are set (see clrrt_kernels.hip); best B ints, qnext one int.
-hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, int* qnext, int* best, int blocks);
+// prefilled: the round's prologue (launch_fill_ints) already reset *a.ncarry_out, *qnext and best[sbase, sbase + B)
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a, int B, int* qnext, int* best, int blocks,
+                                     bool prefilled = false);
+// Up to 8 int ranges set to one value each in ONE launch (a round's counter resets, which were one fill each)
+struct FillInts {
+  int* p[8];
+  int n[8];
+  int v[8];
+  int nj = 0;
+  void add(int* ptr, int count, int value) {
+    if (ptr && count > 0) { p[nj] = ptr; n[nj] = count; v[nj] = value; nj++; }
+  }
+};
+hipError_t launch_fill_ints(hipStream_t st, const FillInts& f);
 size_t roll_order_scratch_bytes(int n);  // k_roll_order's scan scratch for n jobs
 size_t replay_bytes();
 size_t carry_bytes();  // one suspended rollout (deferred samples)
@@ -310,7 +326,7 @@ hipError_t launch_defer_select(hipStream_t st, const int* gv, const uint8_t* pen
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
                           clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb, int tag_slot = 0,
-                          int tag_R = 0, int tag_B = 1);
+                          int tag_R = 0, int tag_B = 1, bool totals_zeroed = false);
 // The exchanged records (sort: by age tag, stable) into out in commit order, tags cleared; goal flags
 // counted into *goal.  keys: [4 n] scratch.
 size_t xorder_sort_bytes(int n);

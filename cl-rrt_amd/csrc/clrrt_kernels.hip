@@ -2912,12 +2912,30 @@ static hipError_t roll_order(hipStream_t st, const RollArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, int* qnext, int* best, int blocks) {
+__global__ void __launch_bounds__(256) k_fill_ints(FillInts f) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int q = 0; q < f.nj; q++)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < f.n[q]; i += stride) f.p[q][i] = f.v[q];
+}
+hipError_t launch_fill_ints(hipStream_t st, const FillInts& f) {
+  if (f.nj <= 0) return hipSuccess;
+  int mx = 0;
+  for (int q = 0; q < f.nj; q++) mx = f.n[q] > mx ? f.n[q] : mx;
+  const int blocks = (mx + 255) / 256 < 64 ? (mx + 255) / 256 : 64;
+  hipLaunchKernelGGL(k_fill_ints, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, f);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
+hipError_t launch_rollout_persistent(hipStream_t st, const RollArgs& a0, int B, int* qnext, int* best, int blocks,
+                                     bool prefilled) {
   hipError_t e;
-  if (a0.ncarry_out && (e = hipMemsetAsync(a0.ncarry_out, 0, sizeof(int), st)) != hipSuccess) return e;
+  if (!prefilled && a0.ncarry_out && (e = hipMemsetAsync(a0.ncarry_out, 0, sizeof(int), st)) != hipSuccess) return e;
   if (a0.njobs <= 0 && a0.nrep <= 0 && a0.ncarry <= 0) return hipSuccess;
-  if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
-  if (B > 0 && (e = hipMemsetAsync(best + a0.sbase, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
+  if (!prefilled) {
+    if ((e = hipMemsetAsync(qnext, 0, sizeof(int), st)) != hipSuccess) return e;
+    if (B > 0 && (e = hipMemsetAsync(best + a0.sbase, 0x7f, sizeof(int) * B, st)) != hipSuccess) return e;
+  }
   RollArgs a = a0;
   a.B = B;
   // dynamic LDS of k_roll_run: the obstacle tables (not with NEED_GAP), then (COOP) the cooperative
@@ -3085,8 +3103,8 @@ hipError_t launch_xorder(hipStream_t st, const clrrt_node* recs, int n, bool sor
 hipError_t launch_compact(hipStream_t st, int L, const clrrt_sample* S, const int* cand, const clrrt_node* reg,
                           const clrrt_node* gbn, const SampleOut* so, int64_t row_base, int rank,
                           clrrt_node* out, Job* jobs, int64_t* totals, CompactBufs& cb, int tag_slot, int tag_R,
-                          int tag_B) {
-  hipError_t e = hipMemsetAsync(totals, 0, sizeof(int64_t) * 8, st);
+                          int tag_B, bool totals_zeroed) {
+  hipError_t e = totals_zeroed ? hipSuccess : hipMemsetAsync(totals, 0, sizeof(int64_t) * 8, st);
   if (e != hipSuccess) return e;
   if (L <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_compact_count, dim3((L + 255) / 256), dim3(256), 0, st, L, so, reg, gbn, cb.packed, totals);

@@ -160,9 +160,14 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
 }
 
 // Morton key of each sample (same frame as the nodes).
+// (zero: counters the search that follows takes from -- the overflow record count and the persistent grid's per-XCD
+// sample counters -- reset here instead of by fills of their own)
 __global__ void k_walk_skeys(const clrrt_sample* __restrict__ S, int B, double x0, double y0, double scale,
-                             uint32_t* __restrict__ keys, int* __restrict__ vals) {
+                             uint32_t* __restrict__ keys, int* __restrict__ vals, int* __restrict__ zero1,
+                             int* __restrict__ zero8) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero1 && i == 0) *zero1 = 0;
+  if (zero8 && i < 8) zero8[i] = 0;
   if (i >= B) return;
   const double x = S[i].x, y = S[i].y;
   uint32_t k = 0xffffffffu;
@@ -1222,6 +1227,145 @@ __global__ void __launch_bounds__(64) k_walk_merge(const int* __restrict__ ovf_n
   walk_emit(lk, li, lane, s, sort_limit, cand, ckey, ncand, ctie);
 }
 
+// Diagnostics (clrrt_walk_audit; no product path uses it): for each sample, what any search over this index's tile
+// bounds must touch.  The sample's true 11th key kth (brute force over every record, pairs ordered as the lists
+// order them) decides which tiles can hold a list member: a tile whose bound (walk_lb, the walk's own bound, max'ed
+// with its super-tile's) exceeds kth holds none, so every tile-bound search visits at least the tiles whose bound is
+// <= kth ("admissible"), while the tiles that hold a list member -- a feasible record whose (key, id) pair does not
+// follow the 11th entry's -- ("useful") are what a perfect tile bound would leave.  out[12 s + q]: q = 0 admissible
+// tiles, 1 useful tiles, 2 feasible records with key <= kth (ties included), 3 records of admissible tiles whose
+// stage-1 lower bound (walk_key_range) is <= kth -- the exact keys a search knowing kth from its start would
+// compute, feasibility aside --, 4 admissible super-tiles, 5 explore flag, 6 kth (float bits), 7 records of
+// admissible tiles, and why those records are not members: 8 infeasible, 9 feasible but farther than kth
+// (Euclidean), 10 feasible, within kth but key > kth (heading); 11 admissible tiles holding a feasible record with
+// key <= kth (ties included).
+template <bool BRK>
+__global__ void __launch_bounds__(64) k_walk_audit(const clrrt_sample* __restrict__ S, int B,
+                                                   const NnRec* __restrict__ nodes, const float4* __restrict__ P,
+                                                   const float* __restrict__ CE, const int* __restrict__ ID,
+                                                   const WalkTile* __restrict__ tiles, int ntiles,
+                                                   const WalkTile* __restrict__ sup, DevParams p, NnFrame fr,
+                                                   int* __restrict__ out) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  if (s >= B) return;
+  const double sx = S[s].x, sy = S[s].y;
+  const bool ex = S[s].explore != 0;
+  // 1. the true list's 11th entry (kth, idk): every record's exact key and feasibleNode
+  float lk = __builtin_inff(), kth = __builtin_inff();
+  int li = 0x7fffffff, idk = 0x7fffffff;
+  const int Npad = ntiles * WALK_TILE;
+  for (int j0 = 0; j0 < Npad; j0 += 64) {
+    const int j = j0 + lane;
+    const int idj = ID[j];
+    float key = __builtin_inff();
+    bool c = false;
+    if (idj >= 0) {
+      const NnRec& r = nodes[idj];
+      key = dubins_key(sx, sy, r.x, r.y, r.c, r.s);
+      if (!ex) key = r.costE + key;
+      c = w_less(key, idj, kth, idk) && feasible_search(sx, sy, r.bx, r.by, r.ca, r.sa, r.ang_par, p.feas_len);
+    }
+    uint64_t m = __ballot(c);
+    while (m) {
+      const int l = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const float k = __shfl(key, l, 64);
+      const int i = __shfl(idj, l, 64);
+      if (w_less(k, i, kth, idk)) {
+        w_insert(lk, li, k, i, lane);
+        kth = uni(__shfl(lk, NN_K - 1, 64));
+        idk = uni(__shfl(li, NN_K - 1, 64));
+      }
+    }
+  }
+  // 2. tiles against kth (the walk's bound terms, as walk_one sets them up)
+  const float rsx = (float)(sx - fr.ox), rsy = (float)(sy - fr.oy);
+  const float dl = fr.delta;
+  const float flen_t = (float)p.feas_len * (1.f - 1e-5f) - 4.f * dl;
+  const float Rx = (float)(nodes[0].x - fr.ox), Ry = (float)(nodes[0].y - fr.oy);
+  const float dsR = sqrtf((rsx - Rx) * (rsx - Rx) + (rsy - Ry) * (rsy - Ry)) * (1.f - 1e-5f) - 2.f * dl - 1e-4f;
+  int n_adm = 0, n_use = 0, n_le = 0, n_s1 = 0, n_sup = 0, n_rec = 0, n_inf = 0, n_far = 0, n_head = 0, n_usele = 0;
+  for (int t0 = 0; t0 < ntiles / WALK_SUPER; t0 += 64) {
+    const int t = t0 + lane;
+    const bool a = t < ntiles / WALK_SUPER && !(walk_lb(sup[t], rsx, rsy, ex, flen_t, dsR) > kth);
+    n_sup += __popcll(__ballot(a));
+  }
+  for (int t0 = 0; t0 < ntiles; t0 += 64) {
+    const int t = t0 + lane;
+    bool adm = false;
+    if (t < ntiles) {
+      const float lb = fmaxf(walk_lb(tiles[t], rsx, rsy, ex, flen_t, dsR),
+                             walk_lb(sup[t / WALK_SUPER], rsx, rsy, ex, flen_t, dsR));
+      adm = !(lb > kth);
+    }
+    uint64_t m = __ballot(adm);
+    n_adm += __popcll(m);
+    while (m) {  // two admissible tiles per step (lanes 0-31 / 32-63)
+      const int ta = t0 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      int tb = -1;
+      if (m) {
+        tb = t0 + __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+      }
+      const int tt = lane < 32 ? ta : tb;
+      const int j = tt >= 0 ? tt * WALK_TILE + (lane & 31) : -1;
+      const int idj = j >= 0 ? ID[j] : -1;
+      bool member = false, le = false, s1 = false, inf = false, far = false, head = false;
+      if (idj >= 0) {
+        const NnRec& r = nodes[idj];
+        float key = dubins_key(sx, sy, r.x, r.y, r.c, r.s);
+        if (!ex) key = r.costE + key;
+        const bool feas = feasible_search(sx, sy, r.bx, r.by, r.ca, r.sa, r.ang_par, p.feas_len);
+        le = !(key > kth) && feas;
+        member = feas && (w_less(key, idj, kth, idk) || idj == idk);
+        const float ex2 = (float)(sx - r.x), ey2 = (float)(sy - r.y);
+        const float dq = sqrtf(ex2 * ex2 + ey2 * ey2) + (ex ? 0.f : r.costE);
+        inf = !feas;
+        far = feas && !le && dq > kth;
+        head = feas && !le && !(dq > kth);
+        const float4 pp = P[j];
+        const float qx = rsx - pp.x, qy = rsy - pp.y;
+        const float tx = pp.z * qx - pp.w * qy, ty = fabsf(pp.w * qx + pp.z * qy);
+        float lo, hi;
+        walk_key_range<BRK>(tx, ty, 4.f * dl + 1e-6f * (fabsf(tx) + ty), lo, hi);
+        const float tlo = (ex ? 0.f : CE[j]) + lo;
+        s1 = !(tlo - 1e-6f * fabsf(tlo) > kth);
+      }
+      const uint64_t mm = __ballot(member), ml = __ballot(le);
+      n_use += ((mm & 0xffffffffull) != 0) + ((mm >> 32) != 0);
+      n_usele += ((ml & 0xffffffffull) != 0) + ((ml >> 32) != 0);
+      n_le += __popcll(ml);
+      n_inf += __popcll(__ballot(inf));
+      n_far += __popcll(__ballot(far));
+      n_head += __popcll(__ballot(head));
+      n_s1 += __popcll(__ballot(s1));
+      n_rec += __popcll(__ballot(idj >= 0));
+    }
+  }
+  if (lane == 0) {
+    int* o = out + 12 * (size_t)s;
+    o[0] = n_adm; o[1] = n_use; o[2] = n_le; o[3] = n_s1; o[4] = n_sup; o[5] = ex; o[6] = __float_as_int(kth);
+    o[7] = n_rec; o[8] = n_inf; o[9] = n_far; o[10] = n_head; o[11] = n_usele;
+  }
+}
+
+hipError_t launch_walk_audit(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N, const DevParams& p,
+                             const NnFrame& fr, const WalkBufs& w, int* out) {
+  if (N <= 0 || B <= 0) return hipSuccess;
+  const int Npad = (N + WALK_TILE * WALK_SUPER - 1) / (WALK_TILE * WALK_SUPER) * (WALK_TILE * WALK_SUPER);
+  const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
+  // the stage-1 bracket of the walk format this tree would use (launch_nn_walk_search)
+  if (nsup > w.half_max)
+    hipLaunchKernelGGL(k_walk_audit<true>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.tiles, ntiles,
+                       w.supers, p, fr, out);
+  else
+    hipLaunchKernelGGL(k_walk_audit<false>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.tiles, ntiles,
+                       w.supers, p, fr, out);
+  LAUNCH_CHECK3();
+  return hipSuccess;
+}
+
 int64_t walk_tile_count(int64_t n) {
   const int64_t sz = WALK_TILE * WALK_SUPER;
   return (n + sz - 1) / sz * WALK_SUPER;
@@ -1433,12 +1577,11 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
     if (e != hipSuccess) return e;
   }
   const bool split = (w.bud_tiles > 0 || w.bud_ex > 0) && w.max_over > 0 && w.nch > 0 && w.ovf_n;
-  if (split) {
-    e = hipMemsetAsync(w.ovf_n, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
-  }
-  // samples in place order (radix sort of their Morton keys; the node sort's buffers are free again)
-  hipLaunchKernelGGL(k_walk_skeys, dim3((B + 255) / 256), dim3(256), 0, st, S, B, x0, y0, scale, w.keys, w.vals);
+  const bool pers_z = w.waves > 0 && w.wctr && B >= w.waves_min_batch;
+  // samples in place order (radix sort of their Morton keys; the node sort's buffers are free again); the
+  // key kernel also resets the overflow count and the persistent grid's counters
+  hipLaunchKernelGGL(k_walk_skeys, dim3((B + 255) / 256), dim3(256), 0, st, S, B, x0, y0, scale, w.keys, w.vals,
+                     split ? w.ovf_n : nullptr, pers_z ? w.wctr : nullptr);
   LAUNCH_CHECK3();
   bytes = w.tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
@@ -1447,10 +1590,6 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   // persistent waves (option nn_walk_waves): a fixed grid taking samples from per-XCD counters
   const bool pers = pers_k;
   const int grid = pers ? std::min(((B + 7) >> 3) * 8, std::max(8, w.waves & ~7)) : ((B + 7) >> 3) * 8;
-  if (pers) {
-    e = hipMemsetAsync(w.wctr, 0, 8 * sizeof(int), st);
-    if (e != hipSuccess) return e;
-  }
   int* wctr = pers ? w.wctr : nullptr;
 #define WALK_LAUNCH1(F, BK, PS)                                                                                  \
   hipLaunchKernelGGL((k_walk_search<F, false, BK, PS>), dim3(grid), dim3(64), lds, st, S, B, nodes, w.P,          \

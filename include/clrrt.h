@@ -496,6 +496,18 @@ int clrrt_search_work(clrrt_ctx* ctx, int64_t out[4]);
  * clrrt_search_work, out[4] = phase-1 super-tile bounds (samples x super-tiles of each walk search), out[5] =
  * super-tile visits (each evaluates its 32 tile bounds), out[6] = records past the prefilter, out[7] = 0. */
 int clrrt_search_work_ex(clrrt_ctx* ctx, int64_t out[8]);
+/* Diagnostics (engine extension): for samples[0 .. n) over the current tree's walk index, what any search over the
+ * index's tile bounds must touch, from the sample's true 11th key kth (brute force).  out[12 i + q]: q = 0 tiles whose
+ * bound is <= kth, 1 of them holding a list member, 2 feasible records with key <= kth (ties included), 3 records of
+ * those tiles whose stage-1 key bound is <= kth, 4 super-tiles whose bound is <= kth, 5 explore flag, 6 kth (float
+ * bits), 7 records of the tiles of q = 0, of which 8 infeasible, 9 feasible but farther than kth, 10 feasible, within
+ * kth, key > kth; 11 tiles of q = 0 holding a feasible record with key <= kth. */
+int clrrt_walk_audit(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t* out);
+/* Engine extension: the tree size after each commit of the last clrrt_expand -- its rounds in order, then the commit
+ * of the deferred samples still pending at its end (defer_steps), when there were any -- into out[0 .. min(n, cap));
+ * *n = the count.  With deferred samples, round r's samples are evaluated against the tree of out[r - 1] nodes (the
+ * tree before the expansion for r = 0) and appended by the commit that is due for them. */
+int clrrt_round_sizes(clrrt_ctx* ctx, int64_t* out, int64_t cap, int64_t* n);
 /* Diagnostics: the context's 64 raw work counters (0..2 rollout work, 8..39 search statistics,
  * 40..63 rollout profile counters of a -DCLRRT_ROLL_PROFILE build: 40..47 per-phase clocks, 48..51 wave
  * lifetimes (sum, max), busiest lane's steps, waves, 52..55 queue-drain times and tail steps). */

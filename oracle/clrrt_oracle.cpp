@@ -1121,6 +1121,39 @@ void orc_eval_iterations(void* h, int n, const double* sx, const double* sy, con
   for (auto& th : pool) th.join();
 }
 
+// orc_eval_iterations against the first `upto` nodes of the loaded tree (the frozen tree of an earlier round inside
+// a larger one), keys from cached rotations (the stable order), with each sample's deciding chain in steps
+// (IterResult::chain: the engine's deferred-sample rule commits it ceil(chain / T) - 1 rounds late).  Test
+// infrastructure (tests/test_full_size_parity.py, late-query deferred rounds).
+void orc_eval_iterations_upto(void* h, int n, const double* sx, const double* sy, const int* explore, int stable,
+                              int threads, long upto, clrrt_node* out, int* counts, long* chains) {
+  Oracle* o = (Oracle*)h;
+  const bool by_ref = o->keys_by_ref;
+  o->keys_by_ref = true;
+  cache_rotations(*o);
+  const size_t up = std::min<size_t>((size_t)std::max(0L, upto), o->tree.size());
+  std::vector<std::thread> pool;
+  const int T = std::max(1, std::min(threads, n));
+  for (int t = 0; t < T; t++)
+    pool.emplace_back([=]() {
+      for (int k = t; k < n; k += T) {
+        Pt s;
+        s.x = sx[k];
+        s.y = sy[k];
+        IterResult r = evaluate_iteration(*o, s, explore[k] != 0, up, stable != 0);
+        int m = 0;
+        Oracle tmp;
+        if (r.added) { tmp.tree.push_back(r.node); m++; }
+        if (r.gb_added) { tmp.tree.push_back(r.gb_node); m++; }
+        if (m) orc_get_nodes(&tmp, 0, m, out + 2 * k);
+        counts[k] = m;
+        chains[k] = r.chain;
+      }
+    });
+  for (auto& th : pool) th.join();
+  o->keys_by_ref = by_ref;
+}
+
 // ---- unit hooks (tests/test_ref_units.py): the same functions the tree path runs, one case per row.
 // OBB gap of the vehicle box at (x, y, th) against one obstacle at time t.
 // in: x, y, th, t, cx, cy, oth, size_x, size_y, vx, vy (11 doubles per case).

@@ -55,6 +55,8 @@ def lib():
             "orc_eval_iteration": (i, [vp, d, d, i, i, P(abi.Node)]),
             "orc_eval_iterations": (None, [vp, i, P(C.c_double), P(C.c_double), P(C.c_int), i, i, P(abi.Node),
                                            P(C.c_int)]),
+            "orc_eval_iterations_upto": (None, [vp, i, P(C.c_double), P(C.c_double), P(C.c_int), i, i, C.c_long,
+                                                P(abi.Node), P(C.c_int), P(C.c_long)]),
             "orc_extract_best_path": (i, [vp, P(i), i]),
             "orc_path_commit": (None, [vp, P(i), i]),
             "orc_path_size": (C.c_long, [vp]),
@@ -272,6 +274,22 @@ class Oracle:
         self.L.orc_eval_iterations(self.h, n, _dp(x), _dp(y), e.ctypes.data_as(P(C.c_int)), 1 if stable else 0,
                                    threads, out, cnt.ctypes.data_as(P(C.c_int)))
         return [[out[2 * k + i] for i in range(cnt[k])] for k in range(n)]
+
+    def eval_iterations_upto(self, xs, ys, explore, upto, stable=True, threads=16):
+        """eval_iterations against the first `upto` nodes of the loaded tree (a frozen round's tree inside a larger
+        one); returns (records per sample, the deciding chain in steps per sample)."""
+        n = len(xs)
+        x = np.ascontiguousarray(xs, dtype=np.float64)
+        y = np.ascontiguousarray(ys, dtype=np.float64)
+        e = np.ascontiguousarray(explore, dtype=np.int32)
+        out = (abi.Node * (2 * n))()
+        cnt = np.zeros(n, dtype=np.int32)
+        chains = np.zeros(n, dtype=np.int64)
+        P = C.POINTER
+        self.L.orc_eval_iterations_upto(self.h, n, _dp(x), _dp(y), e.ctypes.data_as(P(C.c_int)), 1 if stable else 0,
+                                        threads, int(upto), out, cnt.ctypes.data_as(P(C.c_int)),
+                                        chains.ctypes.data_as(P(C.c_long)))
+        return [[out[2 * k + i] for i in range(cnt[k])] for k in range(n)], chains
 
 
 def obb_dist(a, b):

@@ -238,3 +238,83 @@ def test_bench_settings_deferred_tree_matches_oracle(config):
         assert pl.debug_counters()[61] == 0
     finally:
         pl.close()
+
+
+@pytest.mark.timeout(900)
+def test_late_query_deferred_rounds_match_oracle():
+    """Deferral at the late-query tree sizes (verdict r05 item 4): a cfg3 tree grown past 2.2 M nodes with the bench's
+    settings (B = 16384, defer_steps 128, the lag-2 pipeline) -- where the stateless half-precision walk format and the
+    N/512 exact-key budget are live -- then 4 more deferring rounds from it.  For rounds 1-3 of those, 512 random
+    samples each are evaluated by the oracle against their ORIGIN round's frozen tree (eval_iteration = expandTree,
+    rrtplanner.cpp:123-174, BATCH tie order; the tree size before the round from clrrt_round_sizes): the records the
+    GPU appended for each sample are identical (count, parent, nrows, goal flag, state and float cost bits) and were
+    appended by the commit of round r + ceil(chain / T) - 1 (the deferred-sample rule, chain = the oracle's deciding
+    rollout chain; the drain's commit when that is past the last round), and by no other commit."""
+    B, T, lag, rounds, seed, per = 16384, 128, 2, 4, 43, 512
+    target = 4096 * 512 + 100_000
+    max_nodes = 5 << 19
+    obs = scenes.urban_scene(200)
+    pl = clrrt.Planner(clrrt.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), max_nodes=max_nodes,
+                       max_rows=max_nodes * 64, max_batch=B)
+    try:
+        pl.set_option("defer_steps", T)
+        pl.set_option("nn_lag", lag)
+        pl.set_obstacles(obs)
+        pl.tree_init()
+        rng = clrrt.Rng(seed)
+        while pl.size()[0] < target:
+            st = pl.expand(rng, n_iters=64 * B, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+            assert not st["capacity_stop"]
+        n0 = pl.size()[0]
+        rng_at = clrrt.Rng()
+        rng_at.state = abi.Rng.from_buffer_copy(bytes(rng.state))
+        st = pl.expand(rng, n_iters=rounds * B, mode=clrrt.CLRRT_MODE_BATCH, batch=B)
+        assert st["rounds"] == rounds and st["deferred"] > 0, st
+        sizes = [n0] + [int(x) for x in pl.round_sizes()]  # sizes[c + 1]: after commit c (c = rounds: the drain)
+        assert len(sizes) in (rounds + 1, rounds + 2), sizes
+        smp = rng_at.draw_samples(pl.params, rounds * B)
+        raw = pl.nodes_raw()
+        g = clrrt.nodes_to_numpy(pl.nodes_raw(n0))
+        o = Oracle(abi.default_params(collision_mode=abi.CLRRT_COLLISION_OBB), obs)
+        o.load_tree(raw)
+        del raw
+        # appended: a goal-biased node's parent is the regular node just before it (k_append resolved it)
+        idx = np.arange(len(g["parent"]), dtype=np.int64) + n0
+        is_gb = np.zeros(len(g["parent"]), dtype=bool)
+        is_gb[1:] = g["parent"][1:] == idx[:-1]
+        gb_next = np.zeros(len(g["parent"]), dtype=bool)
+        gb_next[:-1] = is_gb[1:]
+        pick_rng = np.random.default_rng(11)
+        checked = {"samples": 0, "nodes": 0, "deferred": 0}
+        for r in range(1, rounds):
+            picks = sorted(pick_rng.choice(B, per, replace=False).tolist())
+            ss = [smp[r * B + j] for j in picks]
+            want, chains = o.eval_iterations_upto([s.x for s in ss], [s.y for s in ss], [s.explore for s in ss],
+                                                  sizes[r], stable=True, threads=16)
+            bad = []
+            for j, s, w, ch in zip(picks, ss, want, chains):
+                D = (int(ch) + T - 1) // T - 1 if ch > 0 else 0
+                c = min(r + D, len(sizes) - 2)  # the commit due (the drain's when past the last round)
+                # the sample's regular record: its reference ends at the sample; the goal-biased one follows it
+                hit = np.nonzero((np.abs(g["ref_back"][:, 0] - s.x) < 1e-6) & (np.abs(g["ref_back"][:, 1] - s.y) < 1e-6)
+                                 & ~is_gb)[0]
+                got = [int(i) for i in hit]
+                got += [i + 1 for i in got if gb_next[i]]
+                got.sort()
+                lo, hi = sizes[c] - n0, sizes[c + 1] - n0
+                ok = len(got) == len(w) and all(lo <= i < hi for i in got)
+                for q, (i, rr) in enumerate(zip(got, w) if ok else ()):
+                    if q == 1:  # the goal-biased record: the oracle leaves its parent unresolved (-2)
+                        ok = ok and rr.parent == abi.CLRRT_PARENT_PREV and int(g["parent"][i]) == n0 + got[0]
+                        rr.parent = int(g["parent"][i])
+                    ok = ok and _same_node(g, i, rr)
+                checked["samples"] += 1
+                checked["nodes"] += len(w)
+                checked["deferred"] += D > 0
+                if not ok:
+                    bad.append((r, j, D, len(w), got[:2], (lo, hi)))
+            assert not bad, f"round {r}: {len(bad)} of {per} samples differ {bad[:4]}"
+        print(f"late-query deferred rounds from {n0} nodes (commits {sizes[1:]}): oracle-checked {checked}")
+        assert checked["nodes"] > 200 and checked["deferred"] > 0
+    finally:
+        pl.close()
