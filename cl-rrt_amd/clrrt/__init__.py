@@ -490,10 +490,12 @@ class Planner:
         """clrrt_walk_audit (diagnostics): per sample (n, 12) int32 -- tiles with bound <= the true 11th key kth,
         those holding a list member, feasible records with key <= kth, records past the stage-1 bound at kth,
         super-tiles with bound <= kth, explore flag, kth bits, records of the admissible tiles, of which
-        infeasible / farther than kth / within kth but key > kth, admissible tiles holding a record with key <= kth."""
+        infeasible / farther than kth / within kth but key > kth, admissible tiles holding a record with key <= kth,
+        admissible tiles whose ref.back() disc holds the sample, their disc radii summed (mm), unbounded arcs, tiles
+        inside one run of equal records, records in such runs."""
         n = len(samples)
         arr = (abi.Sample * n)(*samples)
-        out = np.zeros((n, 12), dtype=np.int32)
+        out = np.zeros((n, 20), dtype=np.int32)
         self._chk(self.L.clrrt_walk_audit(self.h, arr, n, out.ctypes.data_as(P(C.c_int32))), "walk_audit")
         return out
 

@@ -1366,7 +1366,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
-  else if (k == "nn_walk_index" && value >= 0 && value <= 4) {
+  else if (k == "nn_walk_index" && value >= 0 && value <= 5) {
     c->nnw_index = (int)value;
     c->nnw_built.n = -1;  // the kept index and sort results have the old order
     c->nnw.sorted_n = c->nnw_alt.sorted_n = c->nnw3.sorted_n = -1;
@@ -3396,9 +3396,9 @@ int clrrt_walk_audit(clrrt_ctx* c, const clrrt_sample* samples, int32_t n, int32
   c->nnw_built.n = -1;
   HIPC(c, launch_nn_walk_build(c->stream, c->nn, (int)c->n_nodes, su.fr, su.x0, su.y0, su.x1, su.y1, c->nnw));
   int* d_out = nullptr;
-  HIPC(c, hipMalloc(&d_out, sizeof(int32_t) * 12 * (size_t)n));
+  HIPC(c, hipMalloc(&d_out, sizeof(int32_t) * 20 * (size_t)n));
   hipError_t e = launch_walk_audit(c->stream, c->d_samples, n, c->nn, (int)c->n_nodes, c->dp, su.fr, c->nnw, d_out);
-  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(int32_t) * 12 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(int32_t) * 20 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(d_out);
   if (e != hipSuccess) return fail(c, CLRRT_EHIP, std::string("clrrt_walk_audit: ") + hipGetErrorString(e));

@@ -101,8 +101,12 @@ __device__ __forceinline__ uint64_t w_spread3(uint32_t v) {  // 16 bits -> every
 // within the sector), then the costE bits (top 29).  kind 1 / 2: 3D Morton code (16 bits per axis) of (x, y,
 // rho * angle) in one metric scale -- angle = the node's heading (kind 1, from the Dubins rotation (c, s) = (cos,
 // sin)(-heading)) or ang_par (kind 2), wrapped to [-pi, pi) -- then the top 16 costE bits.  kind 3 / 4: the
-// ang_par sector, then kind 1's / kind 2's 3D code, then the top 13 costE bits.  Records with equal key
-// inputs (e.g. the root's zero-length children) end up next to each other in every kind.
+// ang_par sector, then kind 1's / kind 2's 3D code, then the top 13 costE bits.  kind 5 (round 6): kind 3 with a
+// coarse 13-bit Morton code of ref.back() (7 / 6 bits of x / y) in place of the costE bits: records whose position,
+// heading and cost are equal -- the root's zero-length children, one run of 10^4 per ang_par sector whose
+// ref.back() points are their samples, anywhere -- then lie in ref.back() order, so their tiles' ref.back() discs are
+// small and the feasibleNode cone bound can drop them.  Records with equal key inputs (e.g. the root's zero-length
+// children) end up next to each other in every kind.
 __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
                             uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0, int kind = 0) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -116,7 +120,7 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
   int bin = (int)floorf((apf + 3.14159265f) * (WALK_APBINS / 6.2831853f));
   bin = bin < 0 ? 0 : (bin >= WALK_APBINS ? WALK_APBINS - 1 : bin);
   if (kind >= 3) {  // octant, then the 3D Morton code of (x, y, rho * heading | ang_par) inside it
-    const float ang = kind == 3 ? atan2f(-nodes[i].s, nodes[i].c) : apf;
+    const float ang = kind != 4 ? atan2f(-nodes[i].s, nodes[i].c) : apf;
     const double a = isfinite(ang) ? (double)ang - 6.283185307179586 * floor(((double)ang + M_PI) / 6.283185307179586)
                                    : 0.0;  // [-pi, pi)
     uint64_t m = 0xffffffffffffull;
@@ -126,8 +130,17 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
       const double fz = fmin(fmax((a + M_PI) * 4.77 * scale, 0.0), 65535.0);
       m = w_spread3((uint32_t)fx) | (w_spread3((uint32_t)fy) << 1) | (w_spread3((uint32_t)fz) << 2);
     }
-    keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | (m << (16 - WALK_SECTOR_BITS)) |
-              (__float_as_uint(nodes[i].costE) >> (16 + WALK_SECTOR_BITS));
+    uint64_t low = __float_as_uint(nodes[i].costE) >> (16 + WALK_SECTOR_BITS);
+    if (kind == 5) {  // coarse ref.back() cell instead of the cost (13 = 16 - WALK_SECTOR_BITS bits)
+      const double bx = nodes[i].bx, by = nodes[i].by;
+      uint32_t cx = 0, cy = 0;
+      if (isfinite(bx) && isfinite(by)) {
+        cx = (uint32_t)fmin(fmax((bx - x0) * scale, 0.0), 65535.0) >> 9;  // 7 bits
+        cy = (uint32_t)fmin(fmax((by - y0) * scale, 0.0), 65535.0) >> 10;  // 6 bits
+      }
+      low = (w_spread(cx) | (w_spread(cy) << 1)) & 0x1fffu;
+    }
+    keys[i] = ((uint64_t)bin << (64 - WALK_SECTOR_BITS)) | (m << (16 - WALK_SECTOR_BITS)) | low;
     vals[i] = i;
     return;
   }
@@ -1238,11 +1251,15 @@ __global__ void __launch_bounds__(64) k_walk_merge(const int* __restrict__ ovf_n
 // compute, feasibility aside --, 4 admissible super-tiles, 5 explore flag, 6 kth (float bits), 7 records of
 // admissible tiles, and why those records are not members: 8 infeasible, 9 feasible but farther than kth
 // (Euclidean), 10 feasible, within kth but key > kth (heading); 11 admissible tiles holding a feasible record with
-// key <= kth (ties included).
+// key <= kth (ties included); of the admissible tiles: 12 those whose ref.back() disc holds the sample (no
+// feasibility cone), 13 / 14 their position / ref.back() disc radii summed (mm), 15 those with an unbounded
+// heading or ang_par arc, 16 those inside one run of equal key inputs (trun), 17 their records that are in such a
+// run at all (HEAD[j] != j or the next record shares it).
 template <bool BRK>
 __global__ void __launch_bounds__(64) k_walk_audit(const clrrt_sample* __restrict__ S, int B,
                                                    const NnRec* __restrict__ nodes, const float4* __restrict__ P,
                                                    const float* __restrict__ CE, const int* __restrict__ ID,
+                                                   const int* __restrict__ HEAD, const int2* __restrict__ trun,
                                                    const WalkTile* __restrict__ tiles, int ntiles,
                                                    const WalkTile* __restrict__ sup, DevParams p, NnFrame fr,
                                                    int* __restrict__ out) {
@@ -1285,6 +1302,8 @@ __global__ void __launch_bounds__(64) k_walk_audit(const clrrt_sample* __restric
   const float Rx = (float)(nodes[0].x - fr.ox), Ry = (float)(nodes[0].y - fr.oy);
   const float dsR = sqrtf((rsx - Rx) * (rsx - Rx) + (rsy - Ry) * (rsy - Ry)) * (1.f - 1e-5f) - 2.f * dl - 1e-4f;
   int n_adm = 0, n_use = 0, n_le = 0, n_s1 = 0, n_sup = 0, n_rec = 0, n_inf = 0, n_far = 0, n_head = 0, n_usele = 0;
+  int n_in = 0, n_unb = 0, n_run1 = 0, n_inrun = 0;
+  float s_pr = 0.f, s_rr = 0.f;
   for (int t0 = 0; t0 < ntiles / WALK_SUPER; t0 += 64) {
     const int t = t0 + lane;
     const bool a = t < ntiles / WALK_SUPER && !(walk_lb(sup[t], rsx, rsy, ex, flen_t, dsR) > kth);
@@ -1300,6 +1319,16 @@ __global__ void __launch_bounds__(64) k_walk_audit(const clrrt_sample* __restric
     }
     uint64_t m = __ballot(adm);
     n_adm += __popcll(m);
+    if (adm) {
+      const WalkTile& tw = tiles[t];
+      const float ex2 = rsx - tw.rcx, ey2 = rsy - tw.rcy;
+      const bool in = sqrtf(ex2 * ex2 + ey2 * ey2) <= tw.rr;
+      n_in += in;
+      n_unb += tw.thh >= 3.f || tw.aph >= 3.f;
+      n_run1 += trun[t].x >= 0;
+      s_pr += fmaxf(tw.pr, 0.f);
+      s_rr += fmaxf(tw.rr, 0.f);
+    }
     while (m) {  // two admissible tiles per step (lanes 0-31 / 32-63)
       const int ta = t0 + __ffsll((unsigned long long)m) - 1;
       m &= m - 1;
@@ -1341,10 +1370,22 @@ __global__ void __launch_bounds__(64) k_walk_audit(const clrrt_sample* __restric
       n_head += __popcll(__ballot(head));
       n_s1 += __popcll(__ballot(s1));
       n_rec += __popcll(__ballot(idj >= 0));
+      const bool inrun = idj >= 0 && (HEAD[j] != j || (j + 1 < Npad && HEAD[j + 1] == j));
+      n_inrun += __popcll(__ballot(inrun));
     }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n_in += __shfl_xor(n_in, o, 64);
+    n_unb += __shfl_xor(n_unb, o, 64);
+    n_run1 += __shfl_xor(n_run1, o, 64);
+    s_pr += __shfl_xor(s_pr, o, 64);
+    s_rr += __shfl_xor(s_rr, o, 64);
+  }
   if (lane == 0) {
-    int* o = out + 12 * (size_t)s;
+    int* o = out + 20 * (size_t)s;
+    o[12] = n_in; o[13] = (int)fminf(s_pr * 1000.f, 2e9f); o[14] = (int)fminf(s_rr * 1000.f, 2e9f); o[15] = n_unb;
+    o[16] = n_run1; o[17] = n_inrun; o[18] = 0; o[19] = 0;
     o[0] = n_adm; o[1] = n_use; o[2] = n_le; o[3] = n_s1; o[4] = n_sup; o[5] = ex; o[6] = __float_as_int(kth);
     o[7] = n_rec; o[8] = n_inf; o[9] = n_far; o[10] = n_head; o[11] = n_usele;
   }
@@ -1357,11 +1398,11 @@ hipError_t launch_walk_audit(hipStream_t st, const clrrt_sample* S, int B, const
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   // the stage-1 bracket of the walk format this tree would use (launch_nn_walk_search)
   if (nsup > w.half_max)
-    hipLaunchKernelGGL(k_walk_audit<true>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.tiles, ntiles,
-                       w.supers, p, fr, out);
+    hipLaunchKernelGGL(k_walk_audit<true>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.HEAD, w.trun,
+                       w.tiles, ntiles, w.supers, p, fr, out);
   else
-    hipLaunchKernelGGL(k_walk_audit<false>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.tiles, ntiles,
-                       w.supers, p, fr, out);
+    hipLaunchKernelGGL(k_walk_audit<false>, dim3(B), dim3(64), 0, st, S, B, nodes, w.P, w.CE, w.ID, w.HEAD, w.trun,
+                       w.tiles, ntiles, w.supers, p, fr, out);
   LAUNCH_CHECK3();
   return hipSuccess;
 }

@@ -497,11 +497,14 @@ int clrrt_search_work(clrrt_ctx* ctx, int64_t out[4]);
  * super-tile visits (each evaluates its 32 tile bounds), out[6] = records past the prefilter, out[7] = 0. */
 int clrrt_search_work_ex(clrrt_ctx* ctx, int64_t out[8]);
 /* Diagnostics (engine extension): for samples[0 .. n) over the current tree's walk index, what any search over the
- * index's tile bounds must touch, from the sample's true 11th key kth (brute force).  out[12 i + q]: q = 0 tiles whose
+ * index's tile bounds must touch, from the sample's true 11th key kth (brute force).  out[20 i + q]: q = 0 tiles whose
  * bound is <= kth, 1 of them holding a list member, 2 feasible records with key <= kth (ties included), 3 records of
  * those tiles whose stage-1 key bound is <= kth, 4 super-tiles whose bound is <= kth, 5 explore flag, 6 kth (float
  * bits), 7 records of the tiles of q = 0, of which 8 infeasible, 9 feasible but farther than kth, 10 feasible, within
- * kth, key > kth; 11 tiles of q = 0 holding a feasible record with key <= kth. */
+ * kth, key > kth; 11 tiles of q = 0 holding a feasible record with key <= kth; 12 tiles of q = 0 whose ref.back() disc
+ * holds the sample, 13 / 14 their position / ref.back() disc radii summed (mm), 15 those with an unbounded arc, 16
+ * those inside one run of equal key inputs, 17 records of the tiles of q = 0 in such a run; 18, 19 reserved.  out
+ * holds 20 values per sample. */
 int clrrt_walk_audit(clrrt_ctx* ctx, const clrrt_sample* samples, int32_t n, int32_t* out);
 /* Engine extension: the tree size after each commit of the last clrrt_expand -- its rounds in order, then the commit
  * of the deferred samples still pending at its end (defer_steps), when there were any -- into out[0 .. min(n, cap));

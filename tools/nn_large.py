@@ -43,8 +43,8 @@ def timed(sub):
 
 
 for tgt in targets:
-    while pl.size()[0] < tgt * 1e6:
-        st = pl.expand(rng, n_iters=0, budget_ms=1000.0, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+    while pl.size()[0] < tgt * 1e6:  # fixed-count rounds: the same tree on every build (A/B runs compare)
+        st = pl.expand(rng, n_iters=16 * 16384, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
         if st["capacity_stop"]:
             break
     n = pl.size()[0]

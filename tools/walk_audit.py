@@ -39,8 +39,8 @@ def q(a, p):
 
 
 for tgt in targets:
-    while pl.size()[0] < tgt * 1e6:
-        st = pl.expand(rng, n_iters=0, budget_ms=1000.0, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
+    while pl.size()[0] < tgt * 1e6:  # fixed-count rounds: the same tree on every build
+        st = pl.expand(rng, n_iters=16 * 16384, mode=clrrt.CLRRT_MODE_BATCH, batch=16384)
         if st["capacity_stop"]:
             break
     n = pl.size()[0]
@@ -64,3 +64,9 @@ for tgt in targets:
         print(f"  {'':8s} records of admissible tiles that are no member: infeasible {inf.mean() / r:.1%}, feasible but "
               f"farther than kth {far.mean() / r:.1%}, within kth but key > kth (heading) {head.mean() / r:.1%}; "
               f"admissible tiles holding a key <= kth (ties included) {usele.mean():.1f}", flush=True)
+        kth = a[:, 6].copy().view(np.float32)
+        na = np.maximum(1, adm)
+        print(f"  {'':8s} kth p10 {q(kth, 10):.2f} p50 {q(kth, 50):.2f} p90 {q(kth, 90):.2f}; admissible tiles: the sample "
+              f"inside their ref.back() disc {(a[:, 12] / na).mean():.1%}, mean radius position {(a[:, 13] / na).mean() / 1e3:.2f} m "
+              f"ref.back() {(a[:, 14] / na).mean() / 1e3:.2f} m, unbounded arc {(a[:, 15] / na).mean():.1%}; tiles inside one "
+              f"run of equal records {a[:, 16].mean():.0f}, records in runs {a[:, 17].mean() / r:.1%}", flush=True)
