@@ -115,14 +115,18 @@ struct clrrt_ctx {
   // round, 8192 -> 45.6 vs 58-59 ms; 8 M: 3072 stays best, 25.8 vs 29.9 ms at 8192, profiles/r04as)
   bool nnw_bud_tiles_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
-  int nnw_index = 3;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind); 3 since round 5
+  int nnw_hscale = 100;     // option "nn_walk_hscale": the 3D index codes' heading axis, percent of rho per radian
+  int nnw_index = 5;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind); 5 since round 6
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
   // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
   // beside the lag-2 walk (the commit's k_select waited ~1.2 ms per round for slots behind ~1 ms walk waves)
   // and balances the walk's own tail: cfg3 1.164 -> 1.203 M nodes/s (round 4 sweep: 1024 / 1536 / 2048 /
   // 2560 waves -> 1.07 / 1.17 / 1.202 / 1.203 M), the 16 M-node search alone 62 -> 58 ms at 3072; the default
-  // grid is used for batches of >= 4x its waves (below, one wave per sample)
+  // grid is used for batches of >= 4x its waves (below, one wave per sample).  Round 6: 8 per CU -- with the
+  // rollout waves at 320 registers a walk wave fits beside them, and the rollout kernel gains more from the slots a
+  // smaller walk grid leaves than the walk loses (cfg3, kind 5: 1536 / 1792 / 2048 / 2304 / 2560 waves -> 1.238 /
+  // 1.257 / 1.275 / 1.256 / ~1.23 M nodes/s, profiles/r06i_*)
   int nnw_waves = -1;
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
@@ -1366,6 +1370,11 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "nn_walk_budget_keys" && value >= 0 && value < INT_MAX) c->nnw_bud_ex = (int)value;
   else if (k == "nn_walk_half_max" && value >= 0 && value < INT_MAX) c->nnw_half_max = (int)value;
+  else if (k == "nn_walk_hscale" && value >= 1 && value <= 10000) {  // index order: scheduling only
+    c->nnw_hscale = (int)value;
+    c->nnw_built.n = -1;
+    c->nnw.sorted_n = c->nnw_alt.sorted_n = c->nnw3.sorted_n = -1;
+  }
   else if (k == "nn_walk_index" && value >= 0 && value <= 5) {
     c->nnw_index = (int)value;
     c->nnw_built.n = -1;  // the kept index and sort results have the old order
@@ -1541,8 +1550,9 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.nch = c->nnw_chunks;
   w.half_max = c->nnw_half_max;
   w.index_kind = c->nnw_index;
+  w.hscale_pct = c->nnw_hscale;
   w.lds_floor = c->nnw_lds_floor;
-  w.waves = c->nnw_waves < 0 ? 10 * c->n_cu : c->nnw_waves;
+  w.waves = c->nnw_waves < 0 ? 8 * c->n_cu : c->nnw_waves;
   // the default grid serves batches of >= 4x its waves (cfg2's 4096-sample rounds run 4% faster with one
   // wave per sample: 1.237 vs 1.188 M nodes/s)
   w.waves_min_batch = c->nnw_waves < 0 ? 4 * w.waves : 0;

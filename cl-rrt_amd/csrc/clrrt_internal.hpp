@@ -205,10 +205,13 @@ struct WalkBufs {
   // place order of the index (option "nn_walk_index"): 0 = ang_par sector, then the 2D Morton code of the
   // position; 1 = 3D Morton code of (x, y, rho * heading) in one metric scale (the Dubins key is bounded below by
   // max(|q|, rho * beta), so tiles compact in that space prune by heading as well as by distance); 2 = the same
-  // with rho * ang_par; 3 / 4 = the ang_par sector first, then kind 1's / 2's code.  The context's default
-  // (clrrt_ctx::nnw_index) is kind 3 since round 5: 0-5% faster than kind 0 at 1.1-16 M nodes
-  // (profiles/r05c_nn_large_index_ab2.txt; kinds 1 / 2 double the tiles per sample, r05a_nn_large_index_ab.txt)
+  // with rho * ang_par; 3 / 4 = the ang_par sector first, then kind 1's / 2's code; 5 = kind 3 with records of
+  // equal position, heading and cost in ref.back() order (k_walk_keys).  The context's default (clrrt_ctx::nnw_index)
+  // is kind 5 since round 6 (2.8 M nodes 10.82 -> 10.35 ms per 16384-sample search, cfg3 +1.6 %,
+  // profiles/r06g_nn_large_k*.txt); kind 3 was 0-5% faster than kind 0 at 1.1-16 M nodes (round 5,
+  // profiles/r05c_nn_large_index_ab2.txt; kinds 1 / 2 double the tiles per sample, r05a_nn_large_index_ab.txt)
   int index_kind = 0;
+  int hscale_pct = 100;  // the 3D codes' heading axis: percent of rho metres per radian (option nn_walk_hscale)
   int* wctr = nullptr;  // [8] the per-XCD sample counters
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)

@@ -1544,6 +1544,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
   bool qdone = false;  // wave-uniform: a fetch of this wave found the job queue empty
+#ifdef CLRRT_LANE_STATS
+  // diagnostics (work counters 33..38, instead of CLRRT_COLL_STATS'): wave-steps and lanes stepping in them while the
+  // queue still has jobs / after this wave found it empty, and the wave-steps with at most 8 lanes stepping
+  unsigned long long ls_w[2] = {0, 0}, ls_l[2] = {0, 0}, ls_sparse[2] = {0, 0};
+#endif
   // lanes that take jobs (a.lanes_per_wave: a short queue is spread over the grid's waves, so a rollout
   // shares its wave with few others -- each step of a wave runs the union of its lanes' paths -- and the
   // idle lanes still serve the cooperative collision checks)
@@ -1753,6 +1758,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
     // the lanes with a rollout in flight take a step; with the cooperative collision check (COOP) the
     // whole wave takes part in its SAT tests, so the check sits outside the lanes' divergent region
     const bool act = j >= 0 && fin < 0;
+#ifdef CLRRT_LANE_STATS
+    {
+      const int na = __popcll(__ballot(act));
+      if (na > 0) {
+        ls_w[qdone]++;
+        ls_l[qdone] += na;
+        ls_sparse[qdone] += na <= 8;
+      }
+    }
+#endif
     if (!COOP && !act) continue;
     int best_s = 0x7fffffff;
     double d2 = 0.0;
@@ -1817,6 +1832,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLRRT_
       if (n_rep_bad) atomicAdd(&a.ctr[61], n_rep_bad);
     }
   }
+#ifdef CLRRT_LANE_STATS
+  if (a.ctr && lane == 0)
+    for (int q = 0; q < 2; q++) {
+      atomicAdd(&a.ctr[33 + 3 * q], ls_w[q]);
+      atomicAdd(&a.ctr[34 + 3 * q], ls_l[q]);
+      atomicAdd(&a.ctr[35 + 3 * q], ls_sparse[q]);
+    }
+#endif
 #ifdef CLRRT_ROLL_PROFILE
   if (a.ctr && lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&a.ctr[40 + q], (unsigned long long)pclk.wq[1 + q]);

@@ -108,7 +108,8 @@ __device__ __forceinline__ uint64_t w_spread3(uint32_t v) {  // 16 bits -> every
 // small and the feasibleNode cone bound can drop them.  Records with equal key inputs (e.g. the root's zero-length
 // children) end up next to each other in every kind.
 __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, double y0, double scale,
-                            uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0, int kind = 0) {
+                            uint64_t* __restrict__ keys, int* __restrict__ vals, int first = 0, int kind = 0,
+                            double hrho = 4.77) {
   const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (k0 >= N - first) return;
   const int i = first + k0;
@@ -127,7 +128,7 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
     if (isfinite(x) && isfinite(y)) {
       const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
       const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
-      const double fz = fmin(fmax((a + M_PI) * 4.77 * scale, 0.0), 65535.0);
+      const double fz = fmin(fmax((a + M_PI) * hrho * scale, 0.0), 65535.0);
       m = w_spread3((uint32_t)fx) | (w_spread3((uint32_t)fy) << 1) | (w_spread3((uint32_t)fz) << 2);
     }
     uint64_t low = __float_as_uint(nodes[i].costE) >> (16 + WALK_SECTOR_BITS);
@@ -152,7 +153,7 @@ __global__ void k_walk_keys(const NnRec* __restrict__ nodes, int N, double x0, d
     if (isfinite(x) && isfinite(y)) {
       const double fx = fmin(fmax((x - x0) * scale, 0.0), 65535.0);
       const double fy = fmin(fmax((y - y0) * scale, 0.0), 65535.0);
-      const double fz = fmin(fmax((a + M_PI) * 4.77 * scale, 0.0), 65535.0);
+      const double fz = fmin(fmax((a + M_PI) * hrho * scale, 0.0), 65535.0);
       m = w_spread3((uint32_t)fx) | (w_spread3((uint32_t)fy) << 1) | (w_spread3((uint32_t)fz) << 2);
     }
     keys[i] = (m << 16) | (__float_as_uint(nodes[i].costE) >> 16);
@@ -1514,7 +1515,10 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
   const int ntiles = Npad / WALK_TILE, nsup = ntiles / WALK_SUPER;
   const int kind = w.index_kind;
   // 3D keys: one metric scale for x, y and rho * angle (2 pi rho = 30 m of the third axis)
-  const double span = kind ? fmax(fmax(x1 - x0, y1 - y0), 2.0 * M_PI * 4.77) : fmax(x1 - x0, y1 - y0);
+  // the 3D codes' third axis: heading (or ang_par) x hrho metres per radian (rho = 4.77 by default, option
+  // nn_walk_hscale: percent of rho)
+  const double hrho = 4.77 * (w.hscale_pct > 0 ? w.hscale_pct : 100) * 0.01;
+  const double span = kind ? fmax(fmax(x1 - x0, y1 - y0), 2.0 * M_PI * hrho) : fmax(x1 - x0, y1 - y0);
   // (kinds 3 / 4 keep the sector on top: the same scale)
   const double scale = span > 0 ? 65535.0 / span : 1.0;
   hipError_t e;
@@ -1525,7 +1529,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
     const int n0 = (int)prev->sorted_n, nn = N - n0;
     if (nn > 0) {
       hipLaunchKernelGGL(k_walk_keys, dim3((nn + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
-                         (uint64_t*)w.keys, w.vals, n0, kind);
+                         (uint64_t*)w.keys, w.vals, n0, kind, hrho);
       LAUNCH_CHECK3();
       size_t bytes = w.tmp_bytes;
       e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, (uint64_t*)w.keys2, w.vals,
@@ -1544,7 +1548,7 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
     }
   } else {
     hipLaunchKernelGGL(k_walk_keys, dim3((N + 63) / 64), dim3(64), 0, st, nodes, N, x0, y0, scale,
-                       (uint64_t*)w.keys, w.vals, 0, kind);
+                       (uint64_t*)w.keys, w.vals, 0, kind, hrho);
     LAUNCH_CHECK3();
     size_t bytes = w.tmp_bytes;
     e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, (const uint64_t*)w.keys, w.skeys, w.vals, w.sids, N, 0, 64,
