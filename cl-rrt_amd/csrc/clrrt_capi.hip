@@ -115,7 +115,9 @@ struct clrrt_ctx {
   // round, 8192 -> 45.6 vs 58-59 ms; 8 M: 3072 stays best, 25.8 vs 29.9 ms at 8192, profiles/r04as)
   bool nnw_bud_tiles_set = false;
   int nnw_half_max = 4096;  // option "nn_walk_half_max": super-tiles up to which the walk keeps fp16 LDS bounds
-  int nnw_hscale = 100;     // option "nn_walk_hscale": the 3D index codes' heading axis, percent of rho per radian
+  // option "nn_walk_hscale": the 3D index codes' heading axis, percent of rho per radian (round 6: 25 / 50 / 100 / 200
+  // -> cfg3 1.289 / 1.293 / 1.274 / 1.232 M nodes/s, profiles/r06k_*)
+  int nnw_hscale = 50;
   int nnw_index = 5;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind); 5 since round 6
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
@@ -232,6 +234,22 @@ struct clrrt_ctx {
   // highest priority and the walk streams (side, side2) its lowest, so the commit and merge kernels are
   // not queued behind thousands of walk waves (kernel trace: k_select 16 us -> 1.9 ms late in a query)
   hipStream_t mst = nullptr;
+  // option "nn_split_delta" (default 0, round 6): the appended-node search of a slot is split by commit.  The
+  // nodes a commit appends are searched for the round-after-next's samples (slot B) on mst as soon as that slot's
+  // walk is done (its list seeds the chunk caps: unseeded, the search costs ~4x, profiles/r06l_*), beside the next
+  // round's rollouts; after the next commit only that commit's nodes remain, and the walk list, the first partial
+  // lists and the second are merged.  Round 5's single search of both commits' nodes started after the walk and
+  // was ~1.2 ms of the round's critical path (profiles/r06j_*).  (A stream of its own for the first searches made
+  // every rollout kernel ~60% slower, split or not -- 4.1 vs 2.6 ms per round, profiles/r06n_*: with 4 hardware
+  // queues per process, one more stream shares the main stream's queue with a walk stream.)  On mst the lists are
+  // the same and the round is not faster (cfg3 1.281 / 1.275 vs 1.292 M nodes/s, list wait 1.06 / 0.95 vs 1.08 ms,
+  // profiles/r06o_*): the lists wait for the walk, not for this search.
+  int nn_split_delta = 0;
+  float* nn_seed2 = nullptr;                   // [max_batch] the first searches' chunk caps
+  float* d1pk[3] = {nullptr, nullptr, nullptr};  // per slot: the first partial lists (partial_cap entries)
+  int* d1pi[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_d1[3] = {nullptr, nullptr, nullptr};  // recorded after a slot's first partial search
+  hipEvent_t ev_s[3] = {nullptr, nullptr, nullptr};   // recorded after a slot's samples reached the device
   hipEvent_t ev_lagw[3] = {nullptr, nullptr, nullptr};
   int stream_prio = 1;
   int walk_cu_reserve = 0;  // option "walk_cu_reserve" k = 1..7: lag-2 walk streams kept off k/8 of the CUs
@@ -602,6 +620,13 @@ static void free_all(clrrt_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->mst) hipStreamSynchronize(c->mst);
   if (c->mst) hipStreamDestroy(c->mst);
+  for (int q = 0; q < 3; q++) {
+    if (c->ev_d1[q]) hipEventDestroy(c->ev_d1[q]);
+    if (c->ev_s[q]) hipEventDestroy(c->ev_s[q]);
+    if (c->d1pk[q]) hipFree(c->d1pk[q]);
+    if (c->d1pi[q]) hipFree(c->d1pi[q]);
+  }
+  if (c->nn_seed2) hipFree(c->nn_seed2);
   if (c->side) hipStreamSynchronize(c->side);
   if (c->ev_tree) hipEventDestroy(c->ev_tree);
   if (c->ev_walk) hipEventDestroy(c->ev_walk);
@@ -1389,6 +1414,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   }
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
+  else if (k == "nn_split_delta") c->nn_split_delta = value != 0 ? 1 : 0;  // scheduling only: same lists
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "fail_at_round" && value >= 0 && value < INT_MAX) c->fail_at_round = (int)value;  // fault injection
   else if (k == "fail_after_exchange" && value >= 0 && value < INT_MAX) c->fail_after_exchange = (int)value;
@@ -2666,6 +2692,13 @@ struct LagSlot {
   int64_t g = 0;            // samples of the round (all ranks)
   int64_t tree_n = 0;       // size of the tree its walk searched
   int stream = 0;           // side stream index
+  // nn_split_delta: the first partial search (the nodes of the commit after its walk's tree), its lists and events
+  float* d1pk = nullptr;
+  int* d1pi = nullptr;
+  int d1_chunks = 0;
+  int64_t d1_count = 0;     // nodes it covered ([tree_n, tree_n + d1_count)); 0: none
+  hipEvent_t evd1 = nullptr;
+  hipEvent_t evs = nullptr; // the samples are on the device
 };
 
 static int lag_alloc(clrrt_ctx* c) {
@@ -2689,6 +2722,13 @@ static int lag_alloc(clrrt_ctx* c) {
     HIPC(c, hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking));
   }
   HIPC(c, hipStreamCreateWithFlags(&c->mst, hipStreamNonBlocking));
+  HIPC(c, dalloc(&c->nn_seed2, B));
+  for (int q = 0; q < 3; q++) {
+    HIPC(c, dalloc(&c->d1pk[q], c->partial_cap));
+    HIPC(c, dalloc(&c->d1pi[q], c->partial_cap));
+    HIPC(c, hipEventCreateWithFlags(&c->ev_d1[q], hipEventDisableTiming));
+    HIPC(c, hipEventCreateWithFlags(&c->ev_s[q], hipEventDisableTiming));
+  }
   return CLRRT_OK;
 }
 
@@ -2755,8 +2795,14 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   A.ctie = c->ctie2; A.ev = c->ev_lag[0]; A.evw = c->ev_lagw[0];
   B.d = c->d_samples3; B.h = c->h_samples3; B.cand = c->cand3; B.ckey = c->ckey3; B.ncand = c->ncand3;
   B.ctie = c->ctie3; B.ev = c->ev_lag[1]; B.evw = c->ev_lagw[1];
+  A.d1pk = c->d1pk[0]; A.d1pi = c->d1pi[0]; A.evd1 = c->ev_d1[0]; A.evs = c->ev_s[0];
+  B.d1pk = c->d1pk[1]; B.d1pi = c->d1pi[1]; B.evd1 = c->ev_d1[1]; B.evs = c->ev_s[1];
   hipEvent_t cur_ev = c->ev_lag[2];  // the event of the set this round's lists are in
   hipEvent_t cur_evw = c->ev_lagw[2];
+  float* cur_d1pk = c->d1pk[2];       // ... and that set's split-delta buffers and events
+  int* cur_d1pi = c->d1pi[2];
+  hipEvent_t cur_evd1 = c->ev_d1[2], cur_evs = c->ev_s[2];
+  const bool split_delta = c->nn_split_delta != 0;
   // The three list sets rotate every round; whichever way the function is left (an error return of HIPC
   // included), the buffers the context's other paths use get their roles back: (d_samples, cand, ...) and
   // the *2 set are whichever two of the three sets, *3 the third, each freed once by free_all.
@@ -2806,6 +2852,9 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     c->nn_samples += n;
     HIPC(c, hipStreamWaitEvent(s, c->ev_tree, 0));
     HIPC(c, hipMemcpyAsync(sl.d, sl.h, sizeof(clrrt_sample) * n, hipMemcpyHostToDevice, s));
+    HIPC(c, hipEventRecord(sl.evs, s));  // (the split delta's first search reads them on mst)
+    sl.d1_count = 0;
+    sl.d1_chunks = 0;
     c->nn_super_bounds += (int64_t)n * walk_super_count(c->n_nodes);
     {
       KTimer kt(c, 0, s), kt3(c, 3, s);
@@ -2919,9 +2968,35 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     const double ms_commit = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if ((rc = commit_round(c, nn, ms_commit, &n_app)) != CLRRT_OK) break;
     // slot A: merge the nodes appended since its walk's tree
-    if (A.n > 0) {
-      hipStream_t s = c->mst;  // behind the commit and slot A's walk
+    if ((A.n > 0 || (split_delta && B.n > 0)))
       HIPC(c, hipEventRecord(c->ev_commit, c->stream));
+    if (A.n > 0 && split_delta) {
+      // the nodes its first partial search did not cover (this commit's), their key caps seeded from its walk list;
+      // then the walk list, the first partial lists and these are merged
+      hipStream_t s = c->mst;
+      HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
+      HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
+      const int64_t first2 = A.tree_n + A.d1_count, cnt2 = c->n_nodes - first2;
+      int nch2 = 0;
+      if (cnt2 > 0) {
+        KTimer kt(c, 0, s);
+        c->nn_bf_keys += (int64_t)A.n * cnt2;
+        const NnSetup su2 = nn_setup(c);
+        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
+        HIPC(c, launch_nn_delta_partial(s, A.d, A.n, c->nn, (int)first2, (int)cnt2, c->dp, su2.fr, c->pk, c->pi,
+                                        max_chunks, A.ckey, A.ncand, c->nn_seed, &nch2));
+      }
+      if (A.d1_count > 0) HIPC(c, hipStreamWaitEvent(s, A.evd1, 0));
+      {
+        KTimer kt(c, 0, s);
+        if (A.d1_count > 0)
+          HIPC(c, launch_nn_delta_merge(s, A.n, A.d1_chunks, c->dp, A.d1pk, A.d1pi, (int)A.tree_n, A.cand, A.ckey,
+                                        A.ncand, A.ctie));
+        HIPC(c, launch_nn_delta_merge(s, A.n, nch2, c->dp, c->pk, c->pi, (int)first2, A.cand, A.ckey, A.ncand, A.ctie));
+      }
+      HIPC(c, hipEventRecord(A.ev, s));
+    } else if (A.n > 0) {
+      hipStream_t s = c->mst;  // behind the commit and slot A's walk
       HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
       HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
       const int64_t first = A.tree_n, cnt = c->n_nodes - A.tree_n;
@@ -2934,6 +3009,26 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
                                 A.cand, A.ckey, A.ncand, A.ctie, c->nn_seed));
       }
       HIPC(c, hipEventRecord(A.ev, s));
+    }
+    // slot B (split delta): this commit's nodes, searched for the round-after-next's samples beside the next
+    // round's rollouts (merged into B's list after the next commit, when B is slot A); behind slot A's merges
+    if (split_delta && B.n > 0) {
+      hipStream_t s2 = c->mst;
+      HIPC(c, hipStreamWaitEvent(s2, c->ev_commit, 0));
+      HIPC(c, hipStreamWaitEvent(s2, B.evs, 0));
+      HIPC(c, hipStreamWaitEvent(s2, B.evw, 0));  // (its walk list seeds the key caps)
+      const int64_t cnt1 = c->n_nodes - B.tree_n;
+      B.d1_count = cnt1;
+      B.d1_chunks = 0;
+      if (cnt1 > 0) {
+        KTimer kt(c, 0, s2);
+        c->nn_bf_keys += (int64_t)B.n * cnt1;
+        const NnSetup su1 = nn_setup(c);
+        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)B.n * NN_K));
+        HIPC(c, launch_nn_delta_partial(s2, B.d, B.n, c->nn, (int)B.tree_n, (int)cnt1, c->dp, su1.fr, B.d1pk, B.d1pi,
+                                        max_chunks, B.ckey, B.ncand, c->nn_seed2, &B.d1_chunks));
+      }
+      HIPC(c, hipEventRecord(B.evd1, s2));
     }
     // the next round's index (the walk of round r+3's samples searches it)
     {
@@ -2954,11 +3049,13 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       LagSlot old;
       old.d = c->d_samples; old.h = c->h_samples; old.cand = c->cand; old.ckey = c->ckey; old.ncand = c->ncand;
       old.ctie = c->ctie; old.ev = cur_ev; old.evw = cur_evw; old.stream = cur_stream;
+      old.d1pk = cur_d1pk; old.d1pi = cur_d1pi; old.evd1 = cur_evd1; old.evs = cur_evs;
       have_cur = A.n > 0;
       c->d_samples = A.d; c->h_samples = A.h; c->cand = A.cand; c->ckey = A.ckey; c->ncand = A.ncand; c->ctie = A.ctie;
       cur_ev = A.ev;
       cur_evw = A.evw;
       cur_stream = A.stream;
+      cur_d1pk = A.d1pk; cur_d1pi = A.d1pi; cur_evd1 = A.evd1; cur_evs = A.evs;
       A = B;
       B = old;
       B.n = 0;

@@ -251,6 +251,13 @@ hipError_t launch_walk_audit(hipStream_t st, const clrrt_sample* S, int B, const
 hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first, int count,
                            const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks, int* cand,
                            float* ckey, int* ncand, int* ctie, float* seed);
+// launch_nn_delta split in two: the partial lists over the appended nodes (caps shared between chunks from +inf in
+// gcap[B], no older list needed; *nchunks_out lists per sample in pk / pi), and their merge into a list.
+hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
+                                   int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
+                                   const float* ckey, const int* ncand, float* gcap, int* nchunks_out);
+hipError_t launch_nn_delta_merge(hipStream_t st, int B, int nchunks, const DevParams& p, const float* pk, const int* pi,
+                                 int id0, int* cand, float* ckey, int* ncand, int* ctie);
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose
 // selection involves equal keys are re-sorted with the replay of std::sort.  seed: [B] scratch for the
 // chunks' shared key caps (or null).

@@ -2857,6 +2857,40 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
   return hipSuccess;
 }
 
+// The appended-node search in two halves, for callers that split it (expand_lag2 with nn_split_delta): the partial
+// lists of samples S over nodes [first, first + count) -- the chunks' shared key caps in gcap seeded from the samples'
+// older list (ckey / ncand, the walk's: no node above its sort_limit-th key can enter; +inf without one, which costs
+// ~4x: k_nn_partial 4.9 vs 1.15 ms per cfg3 launch, profiles/r06l_*) -- and the merge of such partial lists (ids
+// relative to id0) into a list.
+hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
+                                   int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
+                                   const float* ckey, const int* ncand, float* gcap, int* nchunks_out) {
+  *nchunks_out = 0;
+  if (count <= 0 || B <= 0) return hipSuccess;
+  const int groups = (B + CLRRT_PATH_BLK - 1) / CLRRT_PATH_BLK;
+  int nchunks = (count + 255) / 256;
+  const int want = max(1, 2048 / max(1, groups));
+  nchunks = max(1, min(nchunks, min(want, max_chunks)));
+  int chunk = (count + nchunks - 1) / nchunks;
+  chunk = (chunk + 255) & ~255;
+  nchunks = (count + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, ckey ? p.sort_limit : 0, ckey, ncand, gcap);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(CLRRT_PATH_BLK), 0, st, S, B, nodes + first, count, chunk,
+                     nchunks, p, fr, pk, pi, gcap, nullptr);
+  LAUNCH_CHECK();
+  *nchunks_out = nchunks;
+  return hipSuccess;
+}
+hipError_t launch_nn_delta_merge(hipStream_t st, int B, int nchunks, const DevParams& p, const float* pk, const int* pi,
+                                 int id0, int* cand, float* ckey, int* ncand, int* ctie) {
+  if (nchunks <= 0 || B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 63) / 64), dim3(64), 0, st, B, nchunks, p.sort_limit, pk, pi, id0, cand,
+                     ckey, ncand, ctie);
+  LAUNCH_CHECK();
+  return hipSuccess;
+}
+
 hipError_t launch_nn_exact_only(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                 const DevParams& p, const int* ctie, KeyId* scratch, int* cand, float* ckey,
                                 int* ncand) {
