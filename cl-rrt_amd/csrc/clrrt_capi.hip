@@ -118,17 +118,21 @@ struct clrrt_ctx {
   // option "nn_walk_hscale": the 3D index codes' heading axis, percent of rho per radian (round 6: 25 / 50 / 100 / 200
   // -> cfg3 1.289 / 1.293 / 1.274 / 1.232 M nodes/s, profiles/r06k_*)
   int nnw_hscale = 50;
+  int nnw_lpt = 0;          // option "nn_walk_lpt": optimize samples first in each XCD's eighth (k_walk_lpt)
   int nnw_index = 5;        // option "nn_walk_index": the index's place order (WalkBufs::index_kind); 5 since round 6
   int nnw_lds_floor = 0;    // option "nn_walk_lds_floor": LDS bytes each walk wave reserves at least
   // option "nn_walk_waves": the walk's persistent grid (waves taking samples from per-XCD counters; 0 = one
-  // wave per sample; -1, the default: 10 per CU).  A fixed grid leaves wave slots to the kernels that run
+  // wave per sample; -1, the default: 9 per CU).  A fixed grid leaves wave slots to the kernels that run
   // beside the lag-2 walk (the commit's k_select waited ~1.2 ms per round for slots behind ~1 ms walk waves)
   // and balances the walk's own tail: cfg3 1.164 -> 1.203 M nodes/s (round 4 sweep: 1024 / 1536 / 2048 /
   // 2560 waves -> 1.07 / 1.17 / 1.202 / 1.203 M), the 16 M-node search alone 62 -> 58 ms at 3072; the default
   // grid is used for batches of >= 4x its waves (below, one wave per sample).  Round 6: 8 per CU -- with the
   // rollout waves at 320 registers a walk wave fits beside them, and the rollout kernel gains more from the slots a
   // smaller walk grid leaves than the walk loses (cfg3, kind 5: 1536 / 1792 / 2048 / 2304 / 2560 waves -> 1.238 /
-  // 1.257 / 1.275 / 1.256 / ~1.23 M nodes/s, profiles/r06i_*)
+  // 1.257 / 1.275 / 1.256 / ~1.23 M nodes/s, profiles/r06i_*); then 9 per CU with the walk kernels at 96 VGPRs
+  // (CLRRT_WALK_WAVES 5, clrrt_nnwalk.hip: two walk waves fit beside a rollout wave; 2048 / 2304 / 2560 / 2816 /
+  // 3072 waves -> 1.285 / 1.310, 1.306 / 1.292, 1.303 / 1.287, 1.288 / 1.269 M against 1.288-1.290 M for the
+  // 128-VGPR walk at 2048, profiles/r06r_*, r06s_*)
   int nnw_waves = -1;
   int nnw_double = 1;  // "nn_walk_double": build the next round's index while the side search runs
   WalkBufs nnw{};                      // allocated on first use
@@ -239,9 +243,9 @@ struct clrrt_ctx {
   // walk is done (its list seeds the chunk caps: unseeded, the search costs ~4x, profiles/r06l_*), beside the next
   // round's rollouts; after the next commit only that commit's nodes remain, and the walk list, the first partial
   // lists and the second are merged.  Round 5's single search of both commits' nodes started after the walk and
-  // was ~1.2 ms of the round's critical path (profiles/r06j_*).  (A stream of its own for the first searches made
-  // every rollout kernel ~60% slower, split or not -- 4.1 vs 2.6 ms per round, profiles/r06n_*: with 4 hardware
-  // queues per process, one more stream shares the main stream's queue with a walk stream.)  On mst the lists are
+  // was ~1.2 ms of the round's critical path (profiles/r06j_*).  (A fifth stream of its own for the first searches
+  // made every rollout kernel ~60% slower, split or not -- 4.1 vs 2.6 ms per round, profiles/r06n_*; not the
+  // hardware queue count: GPU_MAX_HW_QUEUES 2 / 4 / 8 / 16 leave the default build unchanged, r06p_*.)  On mst the lists are
   // the same and the round is not faster (cfg3 1.281 / 1.275 vs 1.292 M nodes/s, list wait 1.06 / 0.95 vs 1.08 ms,
   // profiles/r06o_*): the lists wait for the walk, not for this search.
   int nn_split_delta = 0;
@@ -1400,6 +1404,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
     c->nnw_built.n = -1;
     c->nnw.sorted_n = c->nnw_alt.sorted_n = c->nnw3.sorted_n = -1;
   }
+  else if (k == "nn_walk_lpt") c->nnw_lpt = value != 0;  // scheduling only: same lists
   else if (k == "nn_walk_index" && value >= 0 && value <= 5) {
     c->nnw_index = (int)value;
     c->nnw_built.n = -1;  // the kept index and sort results have the old order
@@ -1577,8 +1582,9 @@ static int ensure_walk_set(clrrt_ctx* c, WalkBufs& w) {
   w.half_max = c->nnw_half_max;
   w.index_kind = c->nnw_index;
   w.hscale_pct = c->nnw_hscale;
+  w.lpt = c->nnw_lpt;
   w.lds_floor = c->nnw_lds_floor;
-  w.waves = c->nnw_waves < 0 ? 8 * c->n_cu : c->nnw_waves;
+  w.waves = c->nnw_waves < 0 ? 9 * c->n_cu : c->nnw_waves;
   // the default grid serves batches of >= 4x its waves (cfg2's 4096-sample rounds run 4% faster with one
   // wave per sample: 1.237 vs 1.188 M nodes/s)
   w.waves_min_batch = c->nnw_waves < 0 ? 4 * w.waves : 0;

@@ -213,6 +213,7 @@ struct WalkBufs {
   int index_kind = 0;
   int hscale_pct = 100;  // the 3D codes' heading axis: percent of rho metres per radian (option nn_walk_hscale)
   int* wctr = nullptr;  // [8] the per-XCD sample counters
+  int lpt = 0;          // the persistent grid's eighths: optimize samples first (k_walk_lpt, option nn_walk_lpt)
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists

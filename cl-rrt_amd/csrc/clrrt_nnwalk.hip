@@ -194,6 +194,40 @@ __global__ void k_walk_skeys(const clrrt_sample* __restrict__ S, int B, double x
   vals[i] = i;
 }
 
+// Longest-first order inside each XCD's eighth of the place-ordered samples (option nn_walk_lpt): the persistent
+// walk hands an eighth's samples out in order, so its optimize samples (several times an explore sample's exact
+// keys, profiles/r06g_walk_audit.txt) go first and the cheap explore samples fill the end; each class keeps its
+// place order (a stable partition, one 1024-thread block per eighth).  Scheduling only: every list is the same.
+__global__ void __launch_bounds__(1024) k_walk_lpt(const clrrt_sample* __restrict__ S, int B,
+                                                   const int* __restrict__ sorder, int* __restrict__ out) {
+  __shared__ int part[1024];
+  const int per = (B + 7) >> 3;
+  const int base = (int)blockIdx.x * per;
+  const int n = min(per, B - base);
+  if (n <= 0) return;
+  const int t = threadIdx.x;
+  const int ipt = (n + 1023) >> 10;
+  const int i0 = min(n, t * ipt), i1 = min(n, i0 + ipt);
+  int c = 0;
+  for (int i = i0; i < i1; i++) c += S[sorder[base + i]].explore == 0;
+  part[t] = c;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive scan of the optimize counts
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int total = part[1023];
+  int po = part[t] - c;  // optimize samples before this thread's items
+  int pe = i0 - po;      // explore samples before them
+  for (int i = i0; i < i1; i++) {
+    const int v = sorder[base + i];
+    if (S[v].explore == 0) out[base + po++] = v;
+    else out[base + total + pe++] = v;
+  }
+}
+
 // Per tile: (run head, smallest id) when all 32 records lie in one run of equal key inputs (HEAD is the
 // run's first record: equal at the tile's ends), else (-1, -1).
 __global__ void k_walk_trun(const int* __restrict__ HEAD, const int* __restrict__ ID, int ntiles,
@@ -553,8 +587,11 @@ __device__ __forceinline__ int lc_le(float v) {  // the largest code c with lc_d
 // super-tile (16 KB at 16 M nodes: LDS, not registers, sets the walk's occupancy on large trees).
 // Tiles taken by the super-tile visits go to a small LDS stack and are visited four at a time (128
 // records over the 64 lanes), so the visits' lanes stay busy however few tiles each super-tile gives.
+// Waves per SIMD the walk kernels are compiled for: 5 since round 6 (96 VGPRs, 64-128 B/lane of scratch for the
+// persistent variants), so two walk waves fit on a SIMD beside a 320-register rollout wave (4: 128 VGPRs, one); with
+// a 2304-wave grid cfg3 1.289 -> 1.306-1.310 M nodes/s (profiles/r06r_*, r06s_*).
 #ifndef CLRRT_WALK_WAVES
-#define CLRRT_WALK_WAVES 4
+#define CLRRT_WALK_WAVES 5
 #endif
 // STATE = true (trees up to ~1.3 M nodes): per super-tile a float bound and a visited-tile mask
 // (8 bytes) instead of the stateless coded interval scheme, which spends an extra bound per visit.
@@ -1631,6 +1668,12 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
   bytes = w.tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(w.tmp, bytes, w.keys, w.keys2, w.vals, w.sorder, B, 0, 32, st);
   if (e != hipSuccess) return e;
+  const int* sorder = w.sorder;
+  if (w.lpt && B >= 8) {  // (the sorted keys in keys2 are not read again: its 2 M words hold the new order)
+    hipLaunchKernelGGL(k_walk_lpt, dim3(8), dim3(1024), 0, st, S, B, (const int*)w.sorder, (int*)w.keys2);
+    LAUNCH_CHECK3();
+    sorder = (const int*)w.keys2;
+  }
   const int bt = split ? w.bud_tiles : 0, be = split ? w.bud_ex : 0;
   // persistent waves (option nn_walk_waves): a fixed grid taking samples from per-XCD counters
   const bool pers = pers_k;
@@ -1639,7 +1682,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
 #define WALK_LAUNCH1(F, BK, PS)                                                                                  \
   hipLaunchKernelGGL((k_walk_search<F, false, BK, PS>), dim3(grid), dim3(64), lds, st, S, B, nodes, w.P,          \
                      w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie,  \
-                     w.sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup, wctr)
+                     sorder, stats, bt, be, w.ovf_n, w.ovf, w.max_over, w.nch, w.pk, w.pi, nsup, wctr)
 #define WALK_LAUNCH(F, BK)            \
   do {                                \
     if (pers) WALK_LAUNCH1(F, BK, true);  \
@@ -1664,7 +1707,7 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
 #define WALK_SPLIT(BK)                                                                                           \
   hipLaunchKernelGGL((k_walk_search<WALK_FMT_STATE, true, BK>), dim3(w.max_over * w.nch), dim3(64),               \
                      2 * sizeof(float) * (size_t)nl, st, S, B, nodes, w.P, w.Q, w.CE, w.ID, w.HEAD, w.trun, w.tiles, \
-                     ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, w.sorder, stats, 0, 0, w.ovf_n, w.ovf,  \
+                     ntiles, w.supers, nsup, p, fr, cand, ckey, ncand, ctie, sorder, stats, 0, 0, w.ovf_n, w.ovf,  \
                      w.max_over, w.nch, w.pk, w.pi, nl, nullptr)
     if (brk) WALK_SPLIT(true);
     else WALK_SPLIT(false);
