@@ -249,6 +249,13 @@ struct clrrt_ctx {
   // the same and the round is not faster (cfg3 1.281 / 1.275 vs 1.292 M nodes/s, list wait 1.06 / 0.95 vs 1.08 ms,
   // profiles/r06o_*): the lists wait for the walk, not for this search.
   int nn_split_delta = 0;
+  // option "nn_delta_early" (default 1, round 6): the appended-node search of a slot starts after its walk's main grid
+  // (key caps from k_walk_seed, per slot in wseed) instead of after the overflow split and its merge, so it runs beside
+  // the split (a cfg3 trace: main grid done 1.7 ms before the rollout kernel, split until 0.6 ms after it, the search
+  // after that until 1.9 ms, profiles/r06w_cfg3_list_crit.txt); the merge still waits for the whole walk.
+  int nn_delta_early = 1;
+  float* wseed[3] = {nullptr, nullptr, nullptr};      // per slot: [max_batch] caps taken after the main walk grid
+  hipEvent_t ev_wm[3] = {nullptr, nullptr, nullptr};  // per slot: recorded after the main walk grid (and wseed)
   float* nn_seed2 = nullptr;                   // [max_batch] the first searches' chunk caps
   float* d1pk[3] = {nullptr, nullptr, nullptr};  // per slot: the first partial lists (partial_cap entries)
   int* d1pi[3] = {nullptr, nullptr, nullptr};
@@ -628,6 +635,8 @@ static void free_all(clrrt_ctx* c) {
     if (c->ev_d1[q]) hipEventDestroy(c->ev_d1[q]);
     if (c->ev_s[q]) hipEventDestroy(c->ev_s[q]);
     if (c->d1pk[q]) hipFree(c->d1pk[q]);
+    if (c->wseed[q]) hipFree(c->wseed[q]);
+    if (c->ev_wm[q]) hipEventDestroy(c->ev_wm[q]);
     if (c->d1pi[q]) hipFree(c->d1pi[q]);
   }
   if (c->nn_seed2) hipFree(c->nn_seed2);
@@ -1420,6 +1429,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_walk_double") c->nnw_double = value != 0;
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_split_delta") c->nn_split_delta = value != 0 ? 1 : 0;  // scheduling only: same lists
+  else if (k == "nn_delta_early") c->nn_delta_early = value != 0 ? 1 : 0;  // scheduling only: same lists
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "fail_at_round" && value >= 0 && value < INT_MAX) c->fail_at_round = (int)value;  // fault injection
   else if (k == "fail_after_exchange" && value >= 0 && value < INT_MAX) c->fail_after_exchange = (int)value;
@@ -2705,6 +2715,9 @@ struct LagSlot {
   int64_t d1_count = 0;     // nodes it covered ([tree_n, tree_n + d1_count)); 0: none
   hipEvent_t evd1 = nullptr;
   hipEvent_t evs = nullptr; // the samples are on the device
+  // nn_delta_early: the appended-node search's caps taken after the walk's main grid, and the event recorded there
+  float* wseed = nullptr;
+  hipEvent_t evm = nullptr;
 };
 
 static int lag_alloc(clrrt_ctx* c) {
@@ -2731,6 +2744,8 @@ static int lag_alloc(clrrt_ctx* c) {
   HIPC(c, dalloc(&c->nn_seed2, B));
   for (int q = 0; q < 3; q++) {
     HIPC(c, dalloc(&c->d1pk[q], c->partial_cap));
+    HIPC(c, dalloc(&c->wseed[q], B));
+    HIPC(c, hipEventCreateWithFlags(&c->ev_wm[q], hipEventDisableTiming));
     HIPC(c, dalloc(&c->d1pi[q], c->partial_cap));
     HIPC(c, hipEventCreateWithFlags(&c->ev_d1[q], hipEventDisableTiming));
     HIPC(c, hipEventCreateWithFlags(&c->ev_s[q], hipEventDisableTiming));
@@ -2803,6 +2818,11 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
   B.ctie = c->ctie3; B.ev = c->ev_lag[1]; B.evw = c->ev_lagw[1];
   A.d1pk = c->d1pk[0]; A.d1pi = c->d1pi[0]; A.evd1 = c->ev_d1[0]; A.evs = c->ev_s[0];
   B.d1pk = c->d1pk[1]; B.d1pi = c->d1pi[1]; B.evd1 = c->ev_d1[1]; B.evs = c->ev_s[1];
+  A.wseed = c->wseed[0]; A.evm = c->ev_wm[0];
+  B.wseed = c->wseed[1]; B.evm = c->ev_wm[1];
+  float* cur_wseed = c->wseed[2];
+  hipEvent_t cur_evm = c->ev_wm[2];
+  const bool early = c->nn_delta_early != 0;
   hipEvent_t cur_ev = c->ev_lag[2];  // the event of the set this round's lists are in
   hipEvent_t cur_evw = c->ev_lagw[2];
   float* cur_d1pk = c->d1pk[2];       // ... and that set's split-delta buffers and events
@@ -2864,8 +2884,14 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
     c->nn_super_bounds += (int64_t)n * walk_super_count(c->n_nodes);
     {
       KTimer kt(c, 0, s), kt3(c, 3, s);
-      HIPC(c, launch_nn_walk_search(s, sl.d, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1, su.y1,
-                                    *W[k], sl.cand, sl.ckey, sl.ncand, sl.ctie, c->work_ctr + 18, c->nnw_stateless));
+      W[k]->seed_out = early ? sl.wseed : nullptr;
+      W[k]->ev_main = early ? sl.evm : nullptr;
+      const hipError_t ew = launch_nn_walk_search(s, sl.d, n, c->nn, (int)c->n_nodes, c->dp, su.fr, su.x0, su.y0, su.x1,
+                                                  su.y1, *W[k], sl.cand, sl.ckey, sl.ncand, sl.ctie, c->work_ctr + 18,
+                                                  c->nnw_stateless);
+      W[k]->seed_out = nullptr;
+      W[k]->ev_main = nullptr;
+      HIPC(c, ew);
     }
     HIPC(c, hipEventRecord(sl.evw, s));
     sl.n = n;
@@ -2981,7 +3007,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       // then the walk list, the first partial lists and these are merged
       hipStream_t s = c->mst;
       HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
-      HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
+      HIPC(c, hipStreamWaitEvent(s, early ? A.evm : A.evw, 0));
       const int64_t first2 = A.tree_n + A.d1_count, cnt2 = c->n_nodes - first2;
       int nch2 = 0;
       if (cnt2 > 0) {
@@ -2990,8 +3016,9 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         const NnSetup su2 = nn_setup(c);
         const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
         HIPC(c, launch_nn_delta_partial(s, A.d, A.n, c->nn, (int)first2, (int)cnt2, c->dp, su2.fr, c->pk, c->pi,
-                                        max_chunks, A.ckey, A.ncand, c->nn_seed, &nch2));
+                                        max_chunks, A.ckey, A.ncand, early ? A.wseed : c->nn_seed, early, &nch2));
       }
+      if (early) HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
       if (A.d1_count > 0) HIPC(c, hipStreamWaitEvent(s, A.evd1, 0));
       {
         KTimer kt(c, 0, s);
@@ -2999,6 +3026,28 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
           HIPC(c, launch_nn_delta_merge(s, A.n, A.d1_chunks, c->dp, A.d1pk, A.d1pi, (int)A.tree_n, A.cand, A.ckey,
                                         A.ncand, A.ctie));
         HIPC(c, launch_nn_delta_merge(s, A.n, nch2, c->dp, c->pk, c->pi, (int)first2, A.cand, A.ckey, A.ncand, A.ctie));
+      }
+      HIPC(c, hipEventRecord(A.ev, s));
+    } else if (A.n > 0 && early) {
+      // behind the commit and slot A's main walk grid (caps from its k_walk_seed), beside the walk's overflow split;
+      // the merge behind the whole walk
+      hipStream_t s = c->mst;
+      HIPC(c, hipStreamWaitEvent(s, c->ev_commit, 0));
+      HIPC(c, hipStreamWaitEvent(s, A.evm, 0));
+      const int64_t first = A.tree_n, cnt = c->n_nodes - A.tree_n;
+      int nch = 0;
+      if (cnt > 0) {
+        KTimer kt(c, 0, s);
+        c->nn_bf_keys += (int64_t)A.n * cnt;
+        const NnSetup su2 = nn_setup(c);
+        const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
+        HIPC(c, launch_nn_delta_partial(s, A.d, A.n, c->nn, (int)first, (int)cnt, c->dp, su2.fr, c->pk, c->pi,
+                                        max_chunks, nullptr, nullptr, A.wseed, true, &nch));
+      }
+      HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
+      {
+        KTimer kt(c, 0, s);
+        HIPC(c, launch_nn_delta_merge(s, A.n, nch, c->dp, c->pk, c->pi, (int)first, A.cand, A.ckey, A.ncand, A.ctie));
       }
       HIPC(c, hipEventRecord(A.ev, s));
     } else if (A.n > 0) {
@@ -3022,7 +3071,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       hipStream_t s2 = c->mst;
       HIPC(c, hipStreamWaitEvent(s2, c->ev_commit, 0));
       HIPC(c, hipStreamWaitEvent(s2, B.evs, 0));
-      HIPC(c, hipStreamWaitEvent(s2, B.evw, 0));  // (its walk list seeds the key caps)
+      HIPC(c, hipStreamWaitEvent(s2, early ? B.evm : B.evw, 0));  // (its walk list seeds the key caps)
       const int64_t cnt1 = c->n_nodes - B.tree_n;
       B.d1_count = cnt1;
       B.d1_chunks = 0;
@@ -3032,7 +3081,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         const NnSetup su1 = nn_setup(c);
         const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)B.n * NN_K));
         HIPC(c, launch_nn_delta_partial(s2, B.d, B.n, c->nn, (int)B.tree_n, (int)cnt1, c->dp, su1.fr, B.d1pk, B.d1pi,
-                                        max_chunks, B.ckey, B.ncand, c->nn_seed2, &B.d1_chunks));
+                                        max_chunks, B.ckey, B.ncand, early ? B.wseed : c->nn_seed2, early,
+                                        &B.d1_chunks));
       }
       HIPC(c, hipEventRecord(B.evd1, s2));
     }
@@ -3056,12 +3106,14 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
       old.d = c->d_samples; old.h = c->h_samples; old.cand = c->cand; old.ckey = c->ckey; old.ncand = c->ncand;
       old.ctie = c->ctie; old.ev = cur_ev; old.evw = cur_evw; old.stream = cur_stream;
       old.d1pk = cur_d1pk; old.d1pi = cur_d1pi; old.evd1 = cur_evd1; old.evs = cur_evs;
+      old.wseed = cur_wseed; old.evm = cur_evm;
       have_cur = A.n > 0;
       c->d_samples = A.d; c->h_samples = A.h; c->cand = A.cand; c->ckey = A.ckey; c->ncand = A.ncand; c->ctie = A.ctie;
       cur_ev = A.ev;
       cur_evw = A.evw;
       cur_stream = A.stream;
       cur_d1pk = A.d1pk; cur_d1pi = A.d1pi; cur_evd1 = A.evd1; cur_evs = A.evs;
+      cur_wseed = A.wseed; cur_evm = A.evm;
       A = B;
       B = old;
       B.n = 0;

@@ -214,6 +214,10 @@ struct WalkBufs {
   int hscale_pct = 100;  // the 3D codes' heading axis: percent of rho metres per radian (option nn_walk_hscale)
   int* wctr = nullptr;  // [8] the per-XCD sample counters
   int lpt = 0;          // the persistent grid's eighths: optimize samples first (k_walk_lpt, option nn_walk_lpt)
+  // set by the caller around one launch_nn_walk_search: [B] key caps for the appended-node search written right after
+  // the main grid (k_walk_seed), and an event recorded there (before the overflow split); null: neither
+  float* seed_out = nullptr;
+  hipEvent_t ev_main = nullptr;
   int* ovf_n;    // [1] overflow records claimed
   int4* ovf;     // [max_over] (sample, kth bits, idk + 1, 0)
   float* pk;     // [max_over * nch * 11] partial lists
@@ -256,7 +260,7 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
 // gcap[B], no older list needed; *nchunks_out lists per sample in pk / pi), and their merge into a list.
 hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
                                    int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
-                                   const float* ckey, const int* ncand, float* gcap, int* nchunks_out);
+                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* nchunks_out);
 hipError_t launch_nn_delta_merge(hipStream_t st, int B, int nchunks, const DevParams& p, const float* pk, const int* pi,
                                  int id0, int* cand, float* ckey, int* ncand, int* ctie);
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose

@@ -2861,10 +2861,10 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
 // lists of samples S over nodes [first, first + count) -- the chunks' shared key caps in gcap seeded from the samples'
 // older list (ckey / ncand, the walk's: no node above its sort_limit-th key can enter; +inf without one, which costs
 // ~4x: k_nn_partial 4.9 vs 1.15 ms per cfg3 launch, profiles/r06l_*) -- and the merge of such partial lists (ids
-// relative to id0) into a list.
+// relative to id0) into a list.  seeded: gcap already holds caps (no seed kernel).
 hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
                                    int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
-                                   const float* ckey, const int* ncand, float* gcap, int* nchunks_out) {
+                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* nchunks_out) {
   *nchunks_out = 0;
   if (count <= 0 || B <= 0) return hipSuccess;
   const int groups = (B + CLRRT_PATH_BLK - 1) / CLRRT_PATH_BLK;
@@ -2874,8 +2874,11 @@ hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B,
   int chunk = (count + nchunks - 1) / nchunks;
   chunk = (chunk + 255) & ~255;
   nchunks = (count + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, ckey ? p.sort_limit : 0, ckey, ncand, gcap);
-  LAUNCH_CHECK();
+  if (!seeded) {  // (seeded: the caller's caps, e.g. k_walk_seed's)
+    hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, ckey ? p.sort_limit : 0, ckey, ncand,
+                       gcap);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(CLRRT_PATH_BLK), 0, st, S, B, nodes + first, count, chunk,
                      nchunks, p, fr, pk, pi, gcap, nullptr);
   LAUNCH_CHECK();

@@ -1624,6 +1624,30 @@ hipError_t launch_nn_walk_build(hipStream_t st, const NnRec* nodes, int N, const
 }
 
 // The walk search of samples S[0, B) over the index launch_nn_walk_build made of nodes [0, N).
+// Key caps for the appended-node search taken right after the main walk grid (WalkBufs::seed_out: expand_lag2 starts
+// that search before the overflow split and its merge have run).  A sample the main grid finished: its sort_limit-th
+// key (+inf with fewer); an overflow record's sample, whose list the split's merge writes later: the 11th key it handed
+// over, which bounds its final list's (the split only adds candidates).  Both caps bound the final list's from above,
+// so no appended node that can enter it is cut (k_nn_partial keeps every key <= its cap).
+__device__ __forceinline__ unsigned int w_ord32(float f) {
+  const unsigned int b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);  // (clrrt_kernels.hip ord_enc32)
+}
+__global__ void k_walk_seed(int B, int limit, const float* __restrict__ ckey, const int* __restrict__ ncand,
+                            float* __restrict__ seed) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B) return;
+  const float k = (limit > 0 && ncand[s] >= limit) ? ckey[s * CAND_K + limit - 1] : __builtin_inff();
+  ((unsigned int*)seed)[s] = w_ord32(k);
+}
+__global__ void k_walk_seed_ovf(const int* __restrict__ ovf_n, const int4* __restrict__ ovf, int max_over,
+                                float* __restrict__ seed) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= min(*ovf_n, max_over)) return;
+  const int4 rec = ovf[o];
+  ((unsigned int*)seed)[rec.x] = w_ord32(__int_as_float(rec.y));
+}
+
 hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int N,
                                  const DevParams& p, const NnFrame& fr, double x0, double y0, double x1, double y1,
                                  WalkBufs& w, int* cand, float* ckey, int* ncand, int* ctie, unsigned long long* stats,
@@ -1694,6 +1718,17 @@ hipError_t launch_nn_walk_search(hipStream_t st, const clrrt_sample* S, int B, c
 #undef WALK_LAUNCH
 #undef WALK_LAUNCH1
   LAUNCH_CHECK3();
+  if (w.seed_out) {  // the appended-node search's caps, before the split (its records are claimed by now)
+    hipLaunchKernelGGL(k_walk_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, p.sort_limit, (const float*)ckey,
+                       (const int*)ncand, w.seed_out);
+    LAUNCH_CHECK3();
+    if (split) {
+      hipLaunchKernelGGL(k_walk_seed_ovf, dim3((w.max_over + 63) / 64), dim3(64), 0, st, (const int*)w.ovf_n,
+                         (const int4*)w.ovf, w.max_over, w.seed_out);
+      LAUNCH_CHECK3();
+    }
+  }
+  if (w.ev_main && (e = hipEventRecord(w.ev_main, st)) != hipSuccess) return e;
   if (split) {
     // the overflow records' split waves (state LDS over their interleaved super-tiles; blocks beyond the
     // claimed records exit at once) and the merge

@@ -2,6 +2,7 @@
 # kernel (wave states; VALU lane utilisation) and of the walk (a full 2 s query, so the large-tree format runs), a
 # kernel-trace --stats profile of a cfg3 bench, the default bench line (CPU baselines and EXACT included) and the
 # cfg2 / cfg5 lines.  Every summary records the sources' fingerprint (bench.py picks the pass of its own build).
+# Part A (counters and trace; part B: tools/gpu_final6b.sh).
 # Usage (repo root on the GPU box): bash tools/gpu_final6.sh <tag>
 set -e
 tag=${1:-r06final}
@@ -36,8 +37,4 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/t
   --warmup 1 --no-cpu --no-exact --no-sync > $out/trace_bench.json 2> $out/trace_bench.err
 gzip -f $out/trace/p_kernel_trace.csv
 echo trace done
-timeout -k 10 500 python3 -u bench.py > $out/cfg3_bench.json 2> $out/cfg3_bench.err
-cut -c1-200 $out/cfg3_bench.json
-timeout -k 10 200 python3 -u bench.py --config cfg2 --steps 10 --warmup 2 --no-cpu > $out/cfg2_bench.json 2> $out/cfg2_bench.err
-timeout -k 10 200 python3 -u bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu > $out/cfg5_bench.json 2> $out/cfg5_bench.err
-echo all done
+echo part A done
