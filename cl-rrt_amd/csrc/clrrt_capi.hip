@@ -254,6 +254,10 @@ struct clrrt_ctx {
   // the split (a cfg3 trace: main grid done 1.7 ms before the rollout kernel, split until 0.6 ms after it, the search
   // after that until 1.9 ms, profiles/r06w_cfg3_list_crit.txt); the merge still waits for the whole walk.
   int nn_delta_early = 1;
+  // option "nn_lane_order" (default 1, round 6): the lag-2 appended-node search puts optimize samples on their own
+  // lanes (k_nn_order), so explore lanes do not idle while optimize lanes compute exact keys
+  int nn_lane_order = 1;
+  int* nn_order = nullptr;  // [max_batch]
   float* wseed[3] = {nullptr, nullptr, nullptr};      // per slot: [max_batch] caps taken after the main walk grid
   hipEvent_t ev_wm[3] = {nullptr, nullptr, nullptr};  // per slot: recorded after the main walk grid (and wseed)
   float* nn_seed2 = nullptr;                   // [max_batch] the first searches' chunk caps
@@ -636,6 +640,7 @@ static void free_all(clrrt_ctx* c) {
     if (c->ev_s[q]) hipEventDestroy(c->ev_s[q]);
     if (c->d1pk[q]) hipFree(c->d1pk[q]);
     if (c->wseed[q]) hipFree(c->wseed[q]);
+    if (q == 0 && c->nn_order) hipFree(c->nn_order);
     if (c->ev_wm[q]) hipEventDestroy(c->ev_wm[q]);
     if (c->d1pi[q]) hipFree(c->d1pi[q]);
   }
@@ -1430,6 +1435,7 @@ int clrrt_set_option(clrrt_ctx* c, const char* key, int64_t value) {
   else if (k == "nn_lag" && (value == 0 || value == 1 || value == 2)) c->nn_lag = (int)value;
   else if (k == "nn_split_delta") c->nn_split_delta = value != 0 ? 1 : 0;  // scheduling only: same lists
   else if (k == "nn_delta_early") c->nn_delta_early = value != 0 ? 1 : 0;  // scheduling only: same lists
+  else if (k == "nn_lane_order") c->nn_lane_order = value != 0 ? 1 : 0;  // scheduling only: same lists
   else if (k == "nn_debug" && value >= 0) c->nn_debug = (int)value;  // diagnostics: changes results
   else if (k == "fail_at_round" && value >= 0 && value < INT_MAX) c->fail_at_round = (int)value;  // fault injection
   else if (k == "fail_after_exchange" && value >= 0 && value < INT_MAX) c->fail_after_exchange = (int)value;
@@ -2745,6 +2751,7 @@ static int lag_alloc(clrrt_ctx* c) {
   for (int q = 0; q < 3; q++) {
     HIPC(c, dalloc(&c->d1pk[q], c->partial_cap));
     HIPC(c, dalloc(&c->wseed[q], B));
+    if (q == 0) HIPC(c, dalloc(&c->nn_order, B));
     HIPC(c, hipEventCreateWithFlags(&c->ev_wm[q], hipEventDisableTiming));
     HIPC(c, dalloc(&c->d1pi[q], c->partial_cap));
     HIPC(c, hipEventCreateWithFlags(&c->ev_d1[q], hipEventDisableTiming));
@@ -3016,7 +3023,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         const NnSetup su2 = nn_setup(c);
         const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
         HIPC(c, launch_nn_delta_partial(s, A.d, A.n, c->nn, (int)first2, (int)cnt2, c->dp, su2.fr, c->pk, c->pi,
-                                        max_chunks, A.ckey, A.ncand, early ? A.wseed : c->nn_seed, early, &nch2));
+                                        max_chunks, A.ckey, A.ncand, early ? A.wseed : c->nn_seed, early,
+                                        c->nn_lane_order ? c->nn_order : nullptr, &nch2));
       }
       if (early) HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
       if (A.d1_count > 0) HIPC(c, hipStreamWaitEvent(s, A.evd1, 0));
@@ -3042,7 +3050,8 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         const NnSetup su2 = nn_setup(c);
         const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)A.n * NN_K));
         HIPC(c, launch_nn_delta_partial(s, A.d, A.n, c->nn, (int)first, (int)cnt, c->dp, su2.fr, c->pk, c->pi,
-                                        max_chunks, nullptr, nullptr, A.wseed, true, &nch));
+                                        max_chunks, nullptr, nullptr, A.wseed, true,
+                                        c->nn_lane_order ? c->nn_order : nullptr, &nch));
       }
       HIPC(c, hipStreamWaitEvent(s, A.evw, 0));
       {
@@ -3082,7 +3091,7 @@ static int expand_lag2(clrrt_ctx* c, clrrt_rng* rng, int64_t n_iters, double bud
         const int max_chunks = (int)std::max<int64_t>(1, c->partial_cap / ((int64_t)B.n * NN_K));
         HIPC(c, launch_nn_delta_partial(s2, B.d, B.n, c->nn, (int)B.tree_n, (int)cnt1, c->dp, su1.fr, B.d1pk, B.d1pi,
                                         max_chunks, B.ckey, B.ncand, early ? B.wseed : c->nn_seed2, early,
-                                        &B.d1_chunks));
+                                        c->nn_lane_order ? c->nn_order : nullptr, &B.d1_chunks));
       }
       HIPC(c, hipEventRecord(B.evd1, s2));
     }

@@ -260,7 +260,8 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
 // gcap[B], no older list needed; *nchunks_out lists per sample in pk / pi), and their merge into a list.
 hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
                                    int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
-                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* nchunks_out);
+                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* order,
+                                   int* nchunks_out);
 hipError_t launch_nn_delta_merge(hipStream_t st, int B, int nchunks, const DevParams& p, const float* pk, const int* pi,
                                  int id0, int* cand, float* ckey, int* ncand, int* ctie);
 // Nearest-node search.  exact_scratch != nullptr (EXACT mode, B*N KeyId entries): samples whose

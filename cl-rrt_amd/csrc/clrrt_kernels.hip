@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
                                                     const NnRec* __restrict__ nodes, int N, int chunk,
                                                     int nchunks, DevParams p, NnFrame fr, float* __restrict__ pk,
                                                     int* __restrict__ pi, const float* __restrict__ seed,
-                                                    unsigned long long* tstat) {
+                                                    unsigned long long* tstat, const int* __restrict__ sord) {
   int n_queued = 0, n_exact = 0;
   __shared__ float4 s_r[256];   // node x, y and ref.back() x, y relative to the frame origin (float)
   __shared__ double2 s_p[256];  // node x, y
@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
   const int n0 = c * chunk;
   const int n1 = min(N, n0 + chunk);
   const bool act = t < B;
-  const int s = t;
+  const int s = act && sord ? sord[t] : t;  // sord: the samples' order over the lanes (k_nn_order)
   double sx = 0, sy = 0;
   int ex = 1;
   if (act) { sx = S[s].x; sy = S[s].y; ex = S[s].explore; }
@@ -237,13 +237,39 @@ __global__ void __launch_bounds__(256) k_nn_partial(const clrrt_sample* __restri
     drain(b, cnt);
   }
   if (act) {
-    size_t base = ((size_t)t * nchunks + c) * NN_K;
+    size_t base = ((size_t)s * nchunks + c) * NN_K;
 #pragma unroll
     for (int j = 0; j < NN_K; j++) { pk[base + j] = keys[j]; pi[base + j] = ids[j]; }
   }
   if (tstat) {  // diagnostics: queued pairs, exact keys
     atomicAdd(&tstat[2], (unsigned long long)n_queued);
     atomicAdd(&tstat[3], (unsigned long long)n_exact);
+  }
+}
+
+// Lanes of the appended-node search by heuristic (launch_nn_delta_partial with an order buffer): optimize samples
+// (their cost-shifted caps admit many more pairs, each an exact key) first, explore samples after, each class in
+// sample order, so a wave's lanes drain queues of similar length.  One block: a stable partition of the B samples.
+__global__ void __launch_bounds__(1024) k_nn_order(const clrrt_sample* __restrict__ S, int B, int* __restrict__ out) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int ipt = (B + 1023) >> 10;
+  const int i0 = min(B, t * ipt), i1 = min(B, i0 + ipt);
+  int c = 0;
+  for (int i = i0; i < i1; i++) c += S[i].explore == 0;
+  part[t] = c;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int total = part[1023];
+  int po = part[t] - c, pe = i0 - po;
+  for (int i = i0; i < i1; i++) {
+    if (S[i].explore == 0) out[po++] = i;
+    else out[total + pe++] = i;
   }
 }
 
@@ -2849,7 +2875,7 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
   hipLaunchKernelGGL(k_nn_delta_seed, dim3((B + 63) / 64), dim3(64), 0, st, B, p.sort_limit, ckey, ncand, seed);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(CLRRT_PATH_BLK), 0, st, S, B, nodes + first, count, chunk,
-                     nchunks, p, fr, pk, pi, seed, nullptr);
+                     nchunks, p, fr, pk, pi, seed, nullptr, nullptr);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge_delta, dim3((B + 63) / 64), dim3(64), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      first, cand, ckey, ncand, ctie);
@@ -2864,9 +2890,16 @@ hipError_t launch_nn_delta(hipStream_t st, const clrrt_sample* S, int B, const N
 // relative to id0) into a list.  seeded: gcap already holds caps (no seed kernel).
 hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B, const NnRec* nodes, int first,
                                    int count, const DevParams& p, const NnFrame& fr, float* pk, int* pi, int max_chunks,
-                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* nchunks_out) {
+                                   const float* ckey, const int* ncand, float* gcap, bool seeded, int* order,
+                                   int* nchunks_out) {
   *nchunks_out = 0;
   if (count <= 0 || B <= 0) return hipSuccess;
+  const int* sord = nullptr;
+  if (order) {  // optimize samples on their own lanes (one 1024-thread block: a stable partition of the batch)
+    hipLaunchKernelGGL(k_nn_order, dim3(1), dim3(1024), 0, st, S, B, order);
+    LAUNCH_CHECK();
+    sord = order;
+  }
   const int groups = (B + CLRRT_PATH_BLK - 1) / CLRRT_PATH_BLK;
   int nchunks = (count + 255) / 256;
   const int want = max(1, 2048 / max(1, groups));
@@ -2880,7 +2913,7 @@ hipError_t launch_nn_delta_partial(hipStream_t st, const clrrt_sample* S, int B,
     LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(CLRRT_PATH_BLK), 0, st, S, B, nodes + first, count, chunk,
-                     nchunks, p, fr, pk, pi, gcap, nullptr);
+                     nchunks, p, fr, pk, pi, gcap, nullptr, sord);
   LAUNCH_CHECK();
   *nchunks_out = nchunks;
   return hipSuccess;
@@ -2914,7 +2947,7 @@ static hipError_t launch_nn_brute(hipStream_t st, const clrrt_sample* S, int B, 
   chunk = (chunk + 255) & ~255;  // tiles of 256 nodes never straddle chunks
   nchunks = (N + chunk - 1) / chunk;
   hipLaunchKernelGGL(k_nn_partial, dim3(groups, nchunks), dim3(threads), 0, st, S, B, nodes, N, chunk, nchunks,
-                     p, fr, pk, pi, seed, tstat);
+                     p, fr, pk, pi, seed, tstat, nullptr);
   LAUNCH_CHECK();
   hipLaunchKernelGGL(k_nn_merge, dim3((B + 255) / 256), dim3(256), 0, st, B, nchunks, p.sort_limit, pk, pi,
                      cand, ckey, ncand, ctie);

@@ -5,7 +5,7 @@
 # Part A (counters and trace; part B: tools/gpu_final6b.sh).
 # Usage (repo root on the GPU box): bash tools/gpu_final6.sh <tag>
 set -e
-tag=${1:-r06z}
+tag=${1:-r06zz}
 out=gpurun_out/$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -5,7 +5,7 @@
 # Part B (bench lines and smoke; part A: tools/gpu_final6.sh).
 # Usage (repo root on the GPU box): bash tools/gpu_final6b.sh <tag>
 set -e
-tag=${1:-r06z}
+tag=${1:-r06zz}
 out=gpurun_out/$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
